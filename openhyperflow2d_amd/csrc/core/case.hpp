@@ -1,0 +1,124 @@
+// Problem definition: solver configuration read from the deck plus the
+// pre-processed cell field (host AoS records in x-major order).
+//
+// Reference correspondence:
+//   Config::load        InitSharedData (libDEEPS2D/deeps2d_core.cpp:160-499)
+//   Case::preprocess    InitDEEPS2D (deeps2d_core.cpp:2835-4682) + the serial
+//                       N-S tail of main() (hf2d_start.cpp:292-303)
+#pragma once
+
+#include <functional>
+#include <ostream>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+#include "deck.hpp"
+#include "gasdyn.hpp"
+#include "physics.hpp"
+
+namespace hf2d {
+
+struct MonitorPoint {
+  real x = 0, y = 0;
+  real p = 0, T = 0;
+};
+
+struct XCut {
+  real x0 = 0, y0 = 0, dy = 0;
+};
+
+struct GasSource {
+  int sx, sy, ex, ey, comp;
+  real Cp, Ms, T, Tf;
+  int start_iter;
+};
+
+enum class Semantics { MPI = 0, SERIAL = 1 };
+
+struct Config {
+  // files
+  std::string project, out_file, err_file, swap_file, tecplot_file;
+  // globals
+  int isVerboseOutput = 0, bff = 0;
+  int MaxX = 0, MaxY = 0;
+  real dx = 0, dy = 0;
+  real SigW = 0, SigF = 0, delta_bl = 0;
+  int TurbMod = 0, TurbStartIter = 0, TurbExtModel = 0, isTurbulenceReset = 0;
+  int FT = FT_FLAT, ProblemType = SM_EULER;
+  real CFL = 0;
+  Table CFL_Scenario, beta_Scenario;
+  int NSaveStep = 1, Nmax = 1, NOutStep = 1;
+  int isAlternateRMS = 0, isIgnoreUnsetNodes = 0, MonitorIndex = 0;
+  real ExitMonitorValue = 0;
+  std::vector<MonitorPoint> monitors;
+  real beta0 = 0, nrbc_beta0 = 0;
+  SpeciesProps species;
+  int isAdiabaticWall = 1;
+  real Hu[NSPEC] = {0, 0, 0, 0};
+  // pre-processor
+  real Ts0 = 0;
+  int isOutHeatFluxX = 0, Cp_Flow_index = 0, y_max = 0, y_min = 0, isOutHeatFluxY = 0;
+  int is_p_asterisk_out = 0;
+  int is_Cx_calc = 0, Cx_Flow_index = 0;
+  real x0_body = 0, y0_body = 0, dx_body = 0, dy_body = 0;
+  int is_Cd_calc = 0, Cd_Flow_index = 0;
+  real x0_nozzle = 0, y0_nozzle = 0, dy_nozzle = 0, p_ambient = 0;
+  real InitTime = 0;
+  std::vector<XCut> xcuts;
+  std::vector<GasSource> sources;
+  // runtime options (not in decks; defaults reproduce the reference MPI build)
+  Semantics semantics = Semantics::MPI;
+  int chem_model = CRM_ZELDOVICH;
+
+  void load_globals(InputDeck& d);   // InitSharedData
+  FillParams fill_params() const;    // static FlowNode2D parameters
+  int num_active_eq() const;         // max equations used by any cell model
+};
+
+// Cell field on the host: x-major (idx = i*MaxY + j) like the .hf2d file.
+struct Field {
+  int nx = 0, ny = 0;
+  std::vector<CellRecord> c;
+  void resize(int X, int Y);
+  CellRecord& at(int i, int j) { return c[(size_t)i * ny + j]; }
+  const CellRecord& at(int i, int j) const { return c[(size_t)i * ny + j]; }
+  bool in(long i, long j) const { return i >= 0 && j >= 0 && i < nx && j < ny; }
+};
+
+class Case {
+ public:
+  Config cfg;
+  Field J;
+  std::vector<GasFlow> flows, flows2d;
+  std::vector<std::pair<int, int>> wall_nodes;     // (i, j)
+  std::vector<std::pair<int, int>> subdomains;     // ScanArea [start, end) pairs
+  real dt0 = 1.0;
+  real global_time = 0.0;
+  bool preloaded = false;
+  std::string swap_path;     // resolved checkpoint path ("" = none)
+  std::ostream* log = nullptr;
+
+  // Build the whole problem from a deck.  workdir is where <Project>.hf2d is
+  // looked up; checkpoint=false ignores any existing swap file.
+  static Case from_deck(InputDeck deck, const std::string& workdir = ".", bool use_checkpoint = true,
+                        std::ostream* log = nullptr);
+
+  // Individual pre-processing steps (public for tests).
+  void fill_node(CellRecord& n, int is_mu_t, int is_init) const;
+  void set_wall_nodes();
+  void collect_wall_nodes();
+  void set_min_distance_to_wall(real x0 = 0.0);
+  void recalc_y_plus();
+  void set_init_boundary_layer(real delta);
+  int set_non_reflected_bc();
+  void scan_area(int num_parts);
+  void set_sources(int iter = 0);
+  std::vector<std::pair<int, int>> partition_columns(int num_parts) const;
+
+ private:
+  void preprocess(InputDeck& d, const std::string& workdir, bool use_checkpoint);
+};
+
+}  // namespace hf2d

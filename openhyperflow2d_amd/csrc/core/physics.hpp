@@ -1,0 +1,532 @@
+// Pointwise cell physics shared by the host (CPU oracle / pre-processor) and
+// the HIP kernels: primitive recovery, wall treatment, inviscid + viscous flux
+// assembly, the RANS/LES turbulence closures and the Zeldovich chemistry with
+// mixture-property update.
+//
+// Behavioural reference (re-derived, not translated):
+//   FillNode2D            libOpenHyperFLOW2D/hyper_flow_node.hpp:373-600
+//   TurbModRANS2D         libOpenHyperFLOW2D/hyper_flow_node.hpp:601-957
+//   TurbulenceAxisymmAddOn hyper_flow_node.hpp:241-252
+//   CalcChemicalReactions libDEEPS2D/deeps2d_core.cpp:4697-4780
+//
+// Every function is templated on the node type N; both the 1248-byte host
+// CellRecord and the register-resident device CellLocal expose the same member
+// names, so a single source of truth drives CPU and GPU numerics.
+#pragma once
+
+#include <cmath>
+#include "common.hpp"
+
+namespace hf2d {
+
+struct FillParams {
+  int is_mu_t = 0;
+  int is_init = 0;
+  real sig_w = 0.0;
+  real sig_f = 0.0;
+  int tem = TEM_k_eps_Std;
+  real delta = 0.0;
+  int sm = SM_NS;
+  int FT = FT_FLAT;       // static FlowNode2D::FT
+  real dx = 1.0, dy = 1.0;
+  real Hu[NSPEC] = {0, 0, 0, 0};
+  int isSrcAdd = 0;
+  real turb_I = 0.005;    // FlowNodeTurbulence2D::I
+  int sst_version = 2003; // new model (not in reference)
+};
+
+HF_HD inline real hf_max(real a, real b) { return a > b ? a : b; }
+HF_HD inline real hf_min(real a, real b) { return a < b ? a : b; }
+
+// ---------------------------------------------------------------------------
+// Axisymmetric turbulence add-on (diffusive F terms for k/eps or nu~).
+// ---------------------------------------------------------------------------
+template <class N>
+HF_HD inline void turb_axisym_addon(N& n, const FillParams& P, int is_init) {
+  const real FT = (real)P.FT;
+  if (has_all(n.TurbType, TCT_k_eps_Model) && !is_init) {
+    n.F[I_K] = FT * (n.mu + n.mu_t) * n.dkdy;
+    n.F[I_EPS] = FT * (n.mu + n.mu_t / 1.3) * n.depsdy;
+  } else if (has_all(n.TurbType, TCT_Spalart_Allmaras_Model) && !is_init) {
+    n.F[I_NUT] = FT * (n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdy;
+  } else if (is_init) {
+    n.F[I_NUT] = n.F[I_EPS] = 0.0;
+    n.Src[I_NUT] = n.Src[I_EPS] = 0.0;
+  }
+}
+
+// Menter k-omega SST (new physics, no reference counterpart: the reference
+// reserves TCT_k_omega_SST_Model_2D / TEM_k_omega_SST but leaves the branch
+// empty, hyper_flow_node.hpp:919-926).  omega lives in the eps slot (i2d_omega
+// alias, hyper_flow_turbulence.hpp:20).  Conserved variables are rho*k and
+// rho*omega; the blending functions use the wall distance l_min.
+template <class N>
+HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) {
+  const real sk1 = 0.85, so1 = 0.5, b1 = 0.075;
+  const real sk2 = 1.0, so2 = 0.856, b2 = 0.0828;
+  const real bstar = 0.09, a1 = 0.31, kappa = 0.41;
+  const real rho = n.S[I_RHO];
+  const real dmin = hf_max(n.l_min, 1e-12);
+  if (is_init) {
+    const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+    const real kk = 1.5 * TmpI * TmpI;
+    const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
+    const real om = std::sqrt(kk) / (std::pow(bstar, 0.25) * l);
+    n.S[I_K] = rho * kk;
+    n.S[I_OMEGA] = rho * om;
+    n.mu_t = (om > 0) ? rho * kk / om : 0.0;
+    return;
+  }
+  if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW)) {
+    // Menter wall BC: k = 0, omega = 60 nu / (beta1 d^2)
+    const real d1 = hf_min(P.dx, P.dy) * 0.5;
+    n.S[I_K] = 0.0;
+    n.S[I_OMEGA] = rho * 60.0 * (n.mu / rho) / (b1 * d1 * d1);
+  }
+  if (has_all(n.TurbType, TCT_k_CONST)) {
+    const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+    n.S[I_K] = 1.5 * TmpI * TmpI * rho;
+  }
+  const real kk = hf_max(n.S[I_K] / rho, 0.0);
+  const real om = hf_max(n.S[I_OMEGA] / rho, 1e-20);
+  if (has_all(n.TurbType, TCT_eps_CONST)) {
+    const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
+    n.S[I_OMEGA] = rho * std::sqrt(kk) / (std::pow(bstar, 0.25) * l);
+  }
+  const real nu = n.mu / rho;
+  // dkdx.. hold d(k)/dx and d(omega)/dx (already divided by rho, like the k-eps path)
+  const real cross = n.dkdx * n.depsdx + n.dkdy * n.depsdy;
+  const real CDkw = hf_max(2.0 * rho * so2 / om * cross, 1e-10);
+  const real arg1a = std::sqrt(kk) / (bstar * om * dmin);
+  const real arg1b = 500.0 * nu / (dmin * dmin * om);
+  const real arg1 = hf_min(hf_max(arg1a, arg1b), 4.0 * rho * so2 * kk / (CDkw * dmin * dmin));
+  const real F1 = std::tanh(arg1 * arg1 * arg1 * arg1);
+  const real arg2 = hf_max(2.0 * arg1a, arg1b);
+  const real F2 = std::tanh(arg2 * arg2);
+  const real Sxy = 0.5 * (n.dUdy + n.dVdx);
+  real Smag2 = 2.0 * (n.dUdx * n.dUdx + n.dVdy * n.dVdy) + 4.0 * Sxy * Sxy;
+  if (P.FT) Smag2 += 2.0 * (n.V / n.y) * (n.V / n.y);
+  const real Smag = std::sqrt(Smag2);
+  const real mut = rho * a1 * kk / hf_max(a1 * om, Smag * F2);
+  const real sk = F1 * sk1 + (1.0 - F1) * sk2;
+  const real so = F1 * so1 + (1.0 - F1) * so2;
+  const real beta = F1 * b1 + (1.0 - F1) * b2;
+  const real gam1 = b1 / bstar - so1 * kappa * kappa / std::sqrt(bstar);
+  const real gam2 = b2 / bstar - so2 * kappa * kappa / std::sqrt(bstar);
+  const real gam = F1 * gam1 + (1.0 - F1) * gam2;
+  real Pk = mut * Smag2;
+  Pk = hf_min(Pk, 10.0 * bstar * rho * kk * om);
+  if (is_mu_t) {
+    n.mu_t = hf_max(0.0, mut);
+    n.lam_t = n.mu_t * n.CP;
+  }
+  n.A[I_K] = n.S[I_K] * n.U;
+  n.A[I_OMEGA] = n.S[I_OMEGA] * n.U;
+  n.B[I_K] = n.S[I_K] * n.V;
+  n.B[I_OMEGA] = n.S[I_OMEGA] * n.V;
+  n.RX[I_K] = (n.mu + mut * sk) * n.dkdx;
+  n.RX[I_OMEGA] = (n.mu + mut * so) * n.depsdx;
+  n.RY[I_K] = (n.mu + mut * sk) * n.dkdy;
+  n.RY[I_OMEGA] = (n.mu + mut * so) * n.depsdy;
+  n.A[I_K] -= n.RX[I_K];
+  n.A[I_OMEGA] -= n.RX[I_OMEGA];
+  n.B[I_K] -= n.RY[I_K];
+  n.B[I_OMEGA] -= n.RY[I_OMEGA];
+  n.SrcAdd[I_K] = n.SrcAdd[I_OMEGA] = 0.0;
+  if (!has_all(n.TurbType, TCT_k_CONST)) n.Src[I_K] = Pk - bstar * rho * om * kk;
+  if (!has_all(n.TurbType, TCT_eps_CONST))
+    n.Src[I_OMEGA] = gam * rho / hf_max(mut, 1e-30) * Pk - beta * rho * om * om +
+                     2.0 * (1.0 - F1) * rho * so2 / om * cross;
+  const real FT = (real)P.FT;
+  n.F[I_K] = FT * (n.mu + mut * sk) * n.dkdy;
+  n.F[I_OMEGA] = FT * (n.mu + mut * so) * n.depsdy;
+}
+
+// ---------------------------------------------------------------------------
+// Turbulence closures.
+// ---------------------------------------------------------------------------
+template <class N>
+HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init) {
+  const real dx = P.dx, dy = P.dy;
+  real l = hf_max(n.l_min, hf_min(dy, dx)) * 0.41;
+  const u64 TT = n.TurbType;
+  if (has_all(TT, TCT_Prandtl_Model)) {
+    const real A_p = 26.0;
+    const real n_0 = n.l_min * 0.41;
+    if (P.tem == TEM_Prandtl) {
+      l = n_0;
+    } else if (P.tem == TEM_vanDriest) {
+      l = n_0 * (1. - std::exp(-n.y_plus / A_p));
+    } else if (P.tem == TEM_Escudier) {
+      l = (P.delta > 0.) ? hf_min(n_0, 0.09 * P.delta) : n_0;
+    } else if (P.tem == TEM_Klebanoff) {
+      l = (P.delta > 0.) ? n_0 / std::sqrt(1 + 5.5 * std::pow(n.l_min / P.delta, 6)) : n_0;
+    }
+    n.mu_t = n.S[I_RHO] * l * l * hf_max(std::fabs(n.dUdy), std::fabs(n.dVdx));
+    n.lam_t = n.mu_t * n.CP;
+  } else if (has_all(TT, TCT_k_eps_Model)) {
+    real C1eps = 1.44, C2eps = 1.92, C_mu = 0.09, sig_k = 1.0, sig_eps = 1.3;
+    real f1 = 1., f2 = 1., f_mu = 1.;
+    real Rt, G, L_k = 0, L_eps = 0, Mt = 0;
+    const real Tmp1 = n.dUdy + n.dVdx;
+    const real Tmp2 = n.S[I_RHO] * l;
+    real Tmp3 = n.dUdx * n.dUdx + n.dVdy * n.dVdy;
+    if (P.FT) Tmp3 += n.U / n.y;
+    if (n.mu_t == 0) n.mu_t = n.S[I_RHO] * l * l * hf_max(std::fabs(n.dUdy), std::fabs(n.dVdx));
+    G = n.mu_t * (Tmp1 * Tmp1 + 2 * Tmp3);
+    if (n.S[I_EPS] != 0.0 && n.mu != 0.0)
+      Rt = n.S[I_K] * n.S[I_K] / n.S[I_EPS] / n.mu;
+    else
+      Rt = 0;
+    if (P.tem == TEM_k_eps_Chien) {
+      C1eps = 1.35;
+      C2eps = 1.8;
+      f2 = 1.0 - 0.4 / 1.8 * std::exp(-(Rt * Rt) / 36.0);
+      f_mu = 1.0 - std::exp(-0.0115 * n.y_plus);
+      L_k = -2.0 * n.mu * n.S[I_K] / (Tmp2 * Tmp2);
+      L_eps = -2.0 * n.mu * n.S[I_EPS] / (Tmp2 * Tmp2) * std::exp(-n.y_plus / 2.0);
+      Mt = 1.5 * n.S[I_K] / n.k / n.p;
+    } else if (P.tem == TEM_k_eps_JL) {
+      f_mu = std::exp(-2.5 / (1.0 + Rt / 50));
+    } else if (P.tem == TEM_k_eps_LSY) {
+      f_mu = std::exp(-3.4 / (1.0 + Rt / 50.0) / (1.0 + Rt / 50.0));
+    } else if (P.tem == TEM_k_eps_RNG) {
+      const real nu_0 = 4.38;
+      real nu = (n.S[I_EPS] != 0.) ? std::sqrt(G) * n.S[I_K] / n.S[I_EPS] : 0;
+      C_mu = 0.0845;
+      C1eps = 1.42;
+      C2eps = 1.68 + C_mu * nu * nu * nu * (1.0 - nu / nu_0) / (1. + 0.012 * nu * nu * nu);
+      sig_k = 0.7194;
+      sig_eps = 0.7194;
+      f_mu = 1.;
+    }
+    if (is_init) {
+      const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+      n.S[I_K] = 1.5 * TmpI * TmpI * n.S[I_RHO];
+      n.S[I_EPS] = std::pow(C_mu, 3. / 4.) * std::pow(n.S[I_K] / n.S[I_RHO], 3. / 2.) / l;
+      if (n.S[I_EPS] != 0)
+        n.mu_t = std::fabs(C_mu * f_mu * n.S[I_K] * n.S[I_K] / n.S[I_EPS]);
+    }
+    if (has_all(TT, TCT_k_CONST)) {
+      const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+      n.S[I_K] = 1.5 * TmpI * TmpI * n.S[I_RHO];
+    }
+    if (has_all(TT, TCT_eps_CONST))
+      n.S[I_EPS] = std::pow(C_mu, 3. / 4.) * std::pow(n.S[I_K] / n.S[I_RHO], 3. / 2.) / l;
+    if (has_all(TT, TCT_eps_Cmk2kXn_WALL))
+      n.S[I_EPS] = std::pow(C_mu, 3. / 4.) * std::pow(n.S[I_K] / n.S[I_RHO], 3. / 2.) / l;
+    if (is_mu_t && n.S[I_EPS] != 0) {
+      const real nu_t = std::fabs(C_mu * f_mu * n.S[I_K] * n.S[I_K] / n.S[I_EPS]);
+      n.mu_t = hf_min(nu_t, n.mu_t);
+    }
+    if (!is_init) {
+      n.A[I_K] = n.S[I_K] * n.U;
+      n.A[I_EPS] = n.S[I_EPS] * n.U;
+      n.B[I_K] = n.S[I_K] * n.V;
+      n.B[I_EPS] = n.S[I_EPS] * n.V;
+      n.RX[I_K] = (n.mu + n.mu_t / sig_k) * (n.dkdx);
+      n.RX[I_EPS] = (n.mu + n.mu_t / sig_eps) * (n.depsdx);
+      n.RY[I_K] = (n.mu + n.mu_t / sig_k) * (n.dkdy);
+      n.RY[I_EPS] = (n.mu + n.mu_t / sig_eps) * (n.depsdy);
+      n.A[I_K] = n.A[I_K] - n.RX[I_K];
+      n.A[I_EPS] = n.A[I_EPS] - n.RX[I_EPS];
+      n.B[I_K] = n.B[I_K] - n.RY[I_K];
+      n.B[I_EPS] = n.B[I_EPS] - n.RY[I_EPS];
+      if (n.S[I_K] != 0.) {
+        n.SrcAdd[I_K] = n.SrcAdd[I_EPS] = 0.;
+        if (!has_all(TT, TCT_k_CONST))
+          n.Src[I_K] = (G - n.S[I_EPS] * (1 + Mt) + L_k * n.S[I_RHO]);
+        if (!has_all(TT, TCT_eps_CONST) && n.S[I_K] != 0)
+          n.Src[I_EPS] = (C1eps * f1 * n.S[I_EPS] / n.S[I_K] * G -
+                          C2eps * f2 * n.S[I_EPS] * n.S[I_EPS] / n.S[I_K] + L_eps * n.S[I_RHO]);
+      }
+      turb_axisym_addon(n, P, is_init);
+    }
+  } else if (has_all(TT, TCT_Spalart_Allmaras_Model)) {
+    real fv1 = 1.0;
+    if (is_init) {
+      n.S[I_NUT] = n.mu / n.S[I_RHO] / 100.0;
+    } else if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW) ||
+               has_all(TT, TCT_nu_t_CONST)) {
+      n.S[I_NUT] = 0.;
+    } else if (has_all(n.CT, NT_FC)) {
+      n.S[I_NUT] = n.mu / n.S[I_RHO] * P.turb_I;
+    } else {
+      const real Cb1 = 0.1355, Cb2 = 0.622, sig = 2.0 / 3.0, _k = 0.41;
+      const real Cw1 = Cb1 / (_k * _k) + (1 + Cb2) / sig;
+      const real Cw2 = 0.3, Cw3 = 2.0, Cv1 = 7.1, Ct2 = 2.0, Ct4 = 0.5, C5 = 3.5;
+      const real a_sound2 = n.k * n.R * n.Tg;
+      const real nu = n.mu / n.S[I_RHO];
+      const real ksi = n.S[I_NUT] / nu;
+      fv1 = ksi * ksi * ksi / (ksi * ksi * ksi + Cv1 * Cv1 * Cv1);
+      const real nu_hat = n.mu_t / n.S[I_RHO] / fv1;
+      const real fv2 = 1.0 - ksi / (1.0 + ksi * fv1);
+      const real Wxy = 0.5 * (n.dVdx - n.dUdy);
+      const real Omega = std::sqrt(2.0 * Wxy * Wxy);
+      real S_hat = Omega + n.S[I_NUT] / (_k * _k * n.l_min * n.l_min) * fv2;
+      if (S_hat < 0.3 * Omega) S_hat = 0.3 * Omega;
+      const real r = hf_min((n.S[I_NUT] / (S_hat * _k * _k * n.l_min * n.l_min)), 10.0);
+      const real g = r + Cw2 * (std::pow(r, 6.0) - r);
+      const real fw = g * std::pow((1.0 + std::pow(Cw3, 6.0)) / (std::pow(g, 6.0) + std::pow(Cw3, 6.0)),
+                                   1.0 / 6.0);
+      const real ft2 = Ct2 * std::exp(-Ct4 * ksi * ksi);
+      n.A[I_NUT] = n.S[I_NUT] * n.U;
+      n.B[I_NUT] = n.S[I_NUT] * n.V;
+      const real Div_nu = (n.dkdx + n.dkdy);
+      n.RX[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdx) / sig;
+      n.RY[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdy) / sig;
+      n.A[I_NUT] = n.A[I_NUT] - n.RX[I_NUT];
+      n.B[I_NUT] = n.B[I_NUT] - n.RY[I_NUT];
+      n.Src[I_NUT] = Cb1 * (1.0 - ft2) * S_hat * n.S[I_NUT] -
+                     (Cw1 * fw - Cb1 / (_k * _k) * ft2) * (n.S[I_NUT] / n.l_min) * (n.S[I_NUT] / n.l_min) +
+                     (Cb2 * Div_nu * Div_nu) / sig - C5 * nu_hat * nu_hat / a_sound2 * n.dUdy * n.dVdx;
+    }
+    turb_axisym_addon(n, P, is_init);
+    if (is_mu_t) {
+      n.mu_t = hf_max(0.0, (n.S[I_RHO] * n.S[I_NUT] * fv1));
+      n.lam_t = n.mu_t * n.CP;
+    }
+  } else if (has_all(TT, TCT_k_omega_SST_Model)) {
+    turb_sst(n, P, is_mu_t, is_init);
+  } else if (has_all(TT, TCT_Integral_Model) && n.mu != 0.0) {
+    n.Re_local = n.l_min *
+                 std::sqrt(n.S[I_RHOU] * n.S[I_RHOU] + n.S[I_RHOV] * n.S[I_RHOV] + 1.e-30) / n.mu;
+  } else if (has_all(TT, TCT_Smagorinsky_Model)) {
+    const real Cs = 0.1;
+    const real _delta = std::sqrt(dx * dy);
+    const real Wxy = 0.5 * (n.dVdx - n.dUdy);
+    const real Omega = std::sqrt(2.0 * Wxy * Wxy);
+    if (is_mu_t) {
+      n.mu_t = hf_max(0.0, (n.S[I_RHO] * (Cs * _delta) * (Cs * _delta) * Omega));
+      n.lam_t = n.mu_t * n.CP;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FillNode2D equivalent.  Returns false when the node is skipped.
+// ---------------------------------------------------------------------------
+template <class N>
+HF_HD inline bool fill_node(N& n, const FillParams& P) {
+  if (has_all(n.CT, CT_SOLID)) return false;
+  if (n.S[I_RHO] == 0) return false;
+  if (n.k < 1) return false;
+  real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
+  n.k = n.CP / (n.CP - n.R);
+  if (has_all(n.CT, CT_U_CONST))
+    n.S[I_RHOU] = n.U * n.S[I_RHO];
+  else
+    n.U = n.S[I_RHOU] / n.S[I_RHO];
+  if (has_all(n.CT, CT_V_CONST))
+    n.S[I_RHOV] = n.V * n.S[I_RHO];
+  else
+    n.V = n.S[I_RHOV] / n.S[I_RHO];
+
+  if (P.sm == SM_NS) {
+    if (P.is_init && n.TurbType > 0) {
+      n.mu_t = 5.0 * n.mu;
+    } else if (P.is_init) {
+      n.mu_t = n.lam_t = 0.;
+    }
+    if (n.TurbType > 0) turb_model(n, P, P.is_mu_t, P.is_init);
+  }
+
+  Tmp1 = n.S[I_RHO];
+  for (int i = 0; i < NCOMP; i++) {
+    Tmp3 += P.Hu[i] * n.S[i + 4];
+    Tmp1 -= n.S[i + 4];
+  }
+  Tmp3 += P.Hu[NCOMP] * Tmp1;
+
+  if (has_all(n.CT, CT_WALL_LAW)) {
+    Tmp1 = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+    n.S[I_RHOU] = Tmp1 * n.BGX;
+    n.S[I_RHOV] = Tmp1 * n.BGY;
+    n.U = n.S[I_RHOU] / n.S[I_RHO];
+    n.V = n.S[I_RHOV] / n.S[I_RHO];
+  } else if (has_all(n.CT, CT_WALL_NO_SLIP)) {
+    n.U = n.S[I_RHOU] / n.S[I_RHO];
+    n.V = n.S[I_RHOV] / n.S[I_RHO];
+    if (P.isSrcAdd) {
+      n.SrcAdd[I_RHO] = n.BGX * (n.U - n.Uw) * n.S[I_RHO] / P.dx + n.BGY * (n.V - n.Vw) * n.S[I_RHO] / P.dy;
+      n.SrcAdd[I_RHOU] = n.BGX * (n.U - n.Uw) * n.S[I_RHO];
+      n.SrcAdd[I_RHOV] = n.BGY * (n.V - n.Vw) * n.S[I_RHO];
+      n.SrcAdd[I_RHOE] = 0.;
+    } else {
+      n.SrcAdd[I_RHOU] = n.SrcAdd[I_RHOV] = n.SrcAdd[I_RHOE] = 0.;
+    }
+    n.U = n.Uw;
+    n.V = n.Vw;
+    for (int i = 0; i < NCOMP; i++) n.SrcAdd[4 + i] = P.isSrcAdd ? n.SrcAdd[I_RHO] * n.Y[i] : 0.;
+    n.S[I_RHOU] = n.U * n.S[I_RHO];
+    n.S[I_RHOV] = n.V * n.S[I_RHO];
+  } else {
+    for (int i = 0; i < NEQ; i++) n.SrcAdd[i] = 0.;
+  }
+
+  n.p = (n.k - 1.) * (n.S[I_RHOE] - n.S[I_RHO] * (n.U * n.U + n.V * n.V) * 0.5 - Tmp3);
+  n.Tg = n.p / n.R / n.S[I_RHO];
+
+  if (P.sm == SM_NS) {
+    n.lam_t = n.mu_t * n.CP;
+    if (P.is_mu_t) {
+      if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW)) {
+        _mu = hf_max(0, (n.mu + n.mu_t * P.sig_w));
+        _lam = hf_max(0, (n.lam + n.lam_t * P.sig_w));
+      } else {
+        _mu = hf_max(0, (n.mu + n.mu_t * P.sig_f));
+        _lam = hf_max(0, (n.lam + n.lam_t * P.sig_f));
+      }
+    } else {
+      _mu = n.mu;
+      _lam = n.lam;
+    }
+    n.Diff = _lam / n.CP;
+    L = (2. / 3.) * _mu;
+    if (P.FT == FT_AXISYMMETRIC)
+      Tmp2 = L * (n.dUdx + n.dVdy + (real)P.FT * n.V / n.y);
+    else
+      Tmp2 = L * (n.dUdx + n.dVdy);
+  }
+
+  n.A[I_RHO] = n.S[I_RHOU];
+  n.A[I_RHOU] = n.p + n.S[I_RHOU] * n.U;
+  n.A[I_RHOV] = n.S[I_RHOV] * n.U;
+  n.A[I_RHOE] = (n.S[I_RHOE] + n.p) * n.U;
+  n.B[I_RHO] = n.S[I_RHOV];
+  n.B[I_RHOU] = n.A[I_RHOV];
+  n.B[I_RHOV] = n.p + n.S[I_RHOV] * n.V;
+  n.B[I_RHOE] = (n.S[I_RHOE] + n.p) * n.V;
+  for (int i = 4; i < 4 + NCOMP; i++) {
+    n.B[i] = n.S[i] * n.V;
+    n.A[i] = n.S[i] * n.U;
+  }
+  if (P.FT == FT_AXISYMMETRIC) {
+    const real FT = (real)P.FT;
+    n.F[I_RHO] = FT * n.B[I_RHO];
+    n.F[I_RHOU] = FT * n.A[I_RHOV];
+    n.F[I_RHOV] = FT * n.F[I_RHO] * n.V;
+    n.F[I_RHOE] = FT * n.B[I_RHOE];
+    for (int i = 4; i < 4 + NCOMP; i++) n.F[i] = FT * n.B[i];
+  }
+  if (P.sm == SM_NS) {
+    const real sxx = 2. * _mu * n.dUdx - Tmp2;
+    const real syy = 2. * _mu * n.dVdy - Tmp2;
+    const real txy = _mu * (n.dUdy + n.dVdx);
+    real qx = _lam * n.dTdx;
+    real qy = _lam * n.dTdy;
+    for (int i = 0; i < NSPEC; i++) {
+      qx += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdx[i];
+      qy += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdy[i];
+    }
+    n.RX[I_RHO] = 0.;
+    n.RX[I_RHOU] = sxx;
+    n.RX[I_RHOV] = txy;
+    n.RX[I_RHOE] = n.U * sxx + n.V * txy + qx;
+    n.RY[I_RHO] = 0;
+    n.RY[I_RHOU] = txy;
+    n.RY[I_RHOV] = syy;
+    n.RY[I_RHOE] = n.U * txy + n.V * syy + qy;
+    n.A[I_RHOU] = n.A[I_RHOU] - n.RX[I_RHOU];
+    n.A[I_RHOV] = n.A[I_RHOV] - n.RX[I_RHOV];
+    n.A[I_RHOE] = n.A[I_RHOE] - n.RX[I_RHOE];
+    n.B[I_RHOU] = n.B[I_RHOU] - n.RY[I_RHOU];
+    n.B[I_RHOV] = n.B[I_RHOV] - n.RY[I_RHOV];
+    n.B[I_RHOE] = n.B[I_RHOE] - n.RY[I_RHOE];
+    for (int i = 4; i < 4 + NCOMP; i++) {
+      n.RX[i] = n.Diff * n.droYdx[i - 4];
+      n.RY[i] = n.Diff * n.droYdy[i - 4];
+      n.A[i] = n.A[i] - n.RX[i];
+      n.B[i] = n.B[i] - n.RY[i];
+    }
+    if (P.FT == FT_AXISYMMETRIC) {
+      const real t00 = 2 * _mu * n.V / n.y - Tmp2;
+      n.F[I_RHOU] -= n.RY[I_RHOU];
+      n.F[I_RHOV] -= n.RY[I_RHOV] + t00;
+      n.F[I_RHOE] -= n.RY[I_RHOE];
+      for (int i = 4; i < 4 + NCOMP; i++) n.F[i] -= n.RY[i];
+    } else {
+      for (int i = 0; i < NEQ; i++) n.F[i] = 0.;
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// Zeldovich "infinite-speed" global reaction + mixture properties.
+// ---------------------------------------------------------------------------
+template <class N>
+HF_HD inline void chemistry_zeldovich(N& n, const SpeciesProps& sp, int sm, int model = CRM_ZELDOVICH) {
+  real Yfu = n.S[I_YFU] / n.S[0];
+  real Yox = n.S[I_YOX] / n.S[0];
+  real Ycp = n.S[I_YCP] / n.S[0];
+  real Yair = 1. - (Yfu + Yox + Ycp);
+  real Y0;
+  if (model == CRM_ZELDOVICH) {
+    if (!has_all(n.CT, CT_Y_CONST)) {
+      Y0 = 1. / (Yfu + Yox + Ycp + Yair);
+      Yfu = Yfu * Y0;
+      Yox = Yox * Y0;
+      Ycp = Ycp * Y0;
+      if (n.Tg > n.Tf) {
+        if (Yox > Yfu * sp.K0) {
+          Yox = Yox - Yfu * sp.K0;
+          Yfu = 0.;
+          Ycp = 1. - Yox - Yair;
+        } else {
+          Yfu = Yfu - Yox / sp.K0;
+          Yox = 0.;
+          Ycp = 1. - Yfu - Yair;
+        }
+      }
+    }
+  }
+  const real T = n.Tg;
+  n.R = sp.R[H_FU] * Yfu + sp.R[H_OX] * Yox + sp.R[H_CP] * Ycp + sp.R[H_AIR] * Yair;
+  n.CP = table_eval(sp.Cp[H_FU], T) * Yfu + table_eval(sp.Cp[H_OX], T) * Yox +
+         table_eval(sp.Cp[H_CP], T) * Ycp + table_eval(sp.Cp[H_AIR], T) * Yair;
+  if (sm == SM_NS) {
+    n.lam = table_eval(sp.lam[H_FU], T) * Yfu + table_eval(sp.lam[H_OX], T) * Yox +
+            table_eval(sp.lam[H_CP], T) * Ycp + table_eval(sp.lam[H_AIR], T) * Yair;
+    n.mu = table_eval(sp.mu[H_FU], T) * Yfu + table_eval(sp.mu[H_OX], T) * Yox +
+           table_eval(sp.mu[H_CP], T) * Ycp + table_eval(sp.mu[H_AIR], T) * Yair;
+  }
+  if (Yair < 1.e-5) Yair = 0.;
+  if (Ycp < 1.e-8) Ycp = 0.;
+  if (Yox < 1.e-8) Yox = 0.;
+  if (Yfu < 1.e-8) Yfu = 0.;
+  Y0 = 1. / (Yfu + Yox + Ycp + Yair);
+  Yfu = Yfu * Y0;
+  Yox = Yox * Y0;
+  Ycp = Ycp * Y0;
+  Yair = Yair * Y0;
+  n.Y[0] = Yfu;
+  n.Y[1] = Yox;
+  n.Y[2] = Ycp;
+  n.Y[3] = Yair;
+  if (!has_all(n.CT, CT_Y_CONST)) {
+    n.S[I_YFU] = std::fabs(Yfu * n.S[0]);
+    n.S[I_YOX] = std::fabs(Yox * n.S[0]);
+    n.S[I_YCP] = std::fabs(Ycp * n.S[0]);
+  }
+}
+
+// Number of transported equations for a cell: 9 for k-eps / SST (2 extra),
+// 8 for Spalart-Allmaras, 7 otherwise (deeps2d_core.cpp:4683-4695).
+HF_HD inline int num_eq_for(u64 turb_type) {
+  if (has_all(turb_type, TCT_Prandtl_Model)) return NEQ - 2;
+  if (has_all(turb_type, TCT_k_eps_Model)) return NEQ;
+  if (has_all(turb_type, TCT_Spalart_Allmaras_Model)) return NEQ - 1;
+  if (has_all(turb_type, TCT_k_omega_SST_Model)) return NEQ;
+  return NEQ - 2;
+}
+
+HF_HD inline bool is_two_eq(u64 tt) {
+  return has_all(tt, TCT_k_eps_Model) || has_all(tt, TCT_k_omega_SST_Model);
+}
+HF_HD inline bool has_turb_eq(u64 tt) {
+  return has_all(tt, TCT_k_eps_Model) || has_all(tt, TCT_Spalart_Allmaras_Model) ||
+         has_all(tt, TCT_k_omega_SST_Model);
+}
+
+}  // namespace hf2d

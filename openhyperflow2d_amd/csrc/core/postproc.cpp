@@ -1,0 +1,361 @@
+#include "postproc.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <vector>
+
+namespace hf2d {
+
+void save_field_plt(const std::string& path, const Case& cs, const Field& J, real global_time, bool rewrite) {
+  const Config& C = cs.cfg;
+  std::ofstream o(path, rewrite ? std::ios::trunc : std::ios::app);
+  char h1[1024], h2[256];
+  std::snprintf(h1, sizeof h1,
+                "VARIABLES = X, %s, U, V, T, p, Rho, Y_fuel, Y_ox, Y_cp, Y_i, %s, Mach, l_min, y+, Cp\n",
+                C.FT == 1 ? "R" : "Y", C.is_p_asterisk_out ? "p*" : "mu_t/mu");
+  std::snprintf(h2, sizeof h2, "ZONE T=\"Time: %g sec.\" I= %i J= %i F=POINT\n", global_time, C.MaxX, C.MaxY);
+  o << h1 << h2;
+  const real dx_out = (C.dx * C.MaxX) / (C.MaxX - 1);
+  const real dy_out = (C.dy * C.MaxY) / (C.MaxY - 1);
+  const GasFlow* cxf = (C.is_Cx_calc && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size())
+                           ? &cs.flows2d[C.Cx_Flow_index - 1]
+                           : nullptr;
+  for (int j = 0; j < C.MaxY; j++) {
+    for (int i = 0; i < C.MaxX; i++) {
+      const CellRecord& n = J.at(i, j);
+      o << i * dx_out * 1.e3 << "  ";
+      o << dy_out * j * 1.e3 << "  ";
+      real Mach = 0;
+      if (!n.is(CT_SOLID)) {
+        o << n.U << "  " << n.V << "  " << n.Tg << "  " << n.p << "  " << n.S[0] << "  ";
+        const real A = std::sqrt(n.k * n.R * n.Tg + 1.e-30);
+        const real W = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+        Mach = W / A;
+        if (n.S[0] != 0.) {
+          o << n.S[4] / n.S[0] << "  " << n.S[5] / n.S[0] << "  " << n.S[6] / n.S[0] << "  ";
+          o << std::fabs(1 - n.S[4] / n.S[0] - n.S[5] / n.S[0] - n.S[6] / n.S[0]) << "  ";
+          if (C.is_p_asterisk_out)
+            o << p_asterisk(n) << "  ";
+          else
+            o << n.mu_t / n.mu << "  ";
+        } else {
+          o << " +0. +0  +0  +0  +0  ";
+        }
+      } else {
+        o << "  0  0  " << n.Tg << "  0  0  0  0  0  0  0";
+      }
+      if (!n.is(CT_SOLID)) {
+        if (Mach > 1.e-30)
+          o << Mach << "  " << n.l_min << " " << n.y_plus;
+        else
+          o << "  0  0  0  ";
+      } else {
+        o << "  0  0  0  ";
+      }
+      if (C.is_Cx_calc && cxf)
+        o << " " << calc_cp(n, *cxf) << "\n";
+      else
+        o << " 0\n";
+    }
+    if (rewrite) o << "\n";
+  }
+}
+
+void save_rms_header(const std::string& path, const Config& C) {
+  std::ofstream o(path, std::ios::trunc);
+  o << "#VARIABLES = N, RMS_Ro(N), RMS_RoU(N), RMS_RoV(N), RMS_RoE(N), RMS_RoY_fu(N), RMS_RoY_ox(N), "
+       "RMS_RoY_cp(N), RMS_k(N), RMS_eps(N)"
+    << (C.is_Cd_calc ? ", Cd(N), Cv(N)" : "") << "\n";
+}
+
+void append_rms(const std::string& path, long n, const real* rms, const Case& cs, const Field& J) {
+  std::ofstream o(path, std::ios::app);
+  o << n << " ";
+  for (int i = 0; i < NEQ; i++) o << rms[i] << " ";
+  const Config& C = cs.cfg;
+  if (C.is_Cd_calc && C.Cd_Flow_index >= 1 && C.Cd_Flow_index <= (int)cs.flows2d.size()) {
+    const GasFlow& f = cs.flows2d[C.Cd_Flow_index - 1];
+    o << " " << calc_cd(cs, J, C.x0_nozzle, C.y0_nozzle, C.dy_nozzle, f) << " "
+      << calc_cv(cs, J, C.x0_nozzle, C.y0_nozzle, C.dy_nozzle, C.p_ambient, f) << " ";
+  }
+  o << "\n";
+}
+
+void save_monitors_header(const std::string& path, const Config& C) {
+  std::ofstream o(path, std::ios::trunc);
+  o << "#VARIABLES = Time";
+  for (size_t i = 0; i < C.monitors.size(); i++) o << ", Point-" << i + 1 << ".p, Point-" << i + 1 << ".T";
+  o << "\n";
+}
+
+void append_monitors(const std::string& path, real t, const std::vector<MonitorPoint>& m) {
+  std::ofstream o(path, std::ios::app);
+  o << t << " ";
+  for (auto& p : m) o << p.p << " " << p.T << " ";
+  o << "\n";
+}
+
+real p_asterisk(const CellRecord& n) {
+  const real A = std::sqrt(n.k * n.R * n.Tg);
+  const real WW = std::sqrt(n.U * n.U + n.V * n.V);
+  const real Mach = WW / A;
+  return n.p * std::pow(1.0 + (n.k - 1.0) * 0.5 * Mach * Mach, n.k / (n.k - 1.0));
+}
+real T_asterisk(const CellRecord& n) { return n.CP > 0. ? (n.U * n.U + n.V * n.V) * 0.5 / n.CP : 0.; }
+real schlieren(const CellRecord& n) { return std::sqrt(n.dSdx[0] * n.dSdx[0] + n.dSdy[0] * n.dSdy[0]); }
+real re_airfoil(real chord, const GasFlow& f) { return f.Wg2d() * chord * f.ROG() / f.mu; }
+
+real calc_area(const Case& cs, const Field& J, real x0, real y0, real dy) {
+  const Config& C = cs.cfg;
+  const unsigned i = (unsigned)(x0 / C.dx);
+  const unsigned j0 = (unsigned)(y0 / C.dy), j1 = (unsigned)((y0 + dy) / C.dy);
+  real Sp = 0;
+  if ((int)i >= J.nx) return 0;
+  for (int j = (int)j0; j < (int)j1 && j < J.ny; j++) {
+    const CellRecord& n = J.at(i, j);
+    if (!n.is(CT_SOLID)) Sp += (C.FT == FT_FLAT) ? C.dy : 2 * M_PI * C.dy * n.y;
+  }
+  return Sp;
+}
+
+real mass_flow_rate_x(const Case& cs, const Field& J, real x0, real y0, real dy) {
+  const Config& C = cs.cfg;
+  const unsigned i = (unsigned)(x0 / C.dx);
+  const unsigned j0 = (unsigned)(y0 / C.dy), j1 = (unsigned)((y0 + dy) / C.dy);
+  real Mp = 0;
+  if ((int)i >= J.nx) return 0;
+  for (int j = (int)j0; j < (int)j1 && j < J.ny; j++) {
+    const CellRecord& n = J.at(i, j);
+    if (!n.is(CT_SOLID)) Mp += (C.FT == FT_FLAT) ? C.dy * n.S[I_RHOU] : 2 * M_PI * C.dy * n.y * n.S[I_RHOU];
+  }
+  return Mp;
+}
+
+static bool in_box(const Config& C, int i, int j, real x0, real y0, real dx, real dy) {
+  return i >= (int)(x0 / C.dx) && i <= (int)((x0 + dx) / C.dx) && j >= (int)(y0 / C.dy) && j <= (int)((y0 + dy) / C.dy);
+}
+
+real x_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  const Config& C = cs.cfg;
+  real Fp = 0, Fd = 0;
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& n = J.at(i, j);
+      if (!((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy))) continue;
+      real Sp, Sd;
+      if (C.FT == FT_FLAT) {
+        Sp = C.dy;
+        Sd = C.dx;
+      } else {
+        Sp = 2 * M_PI * (j + 0.5) * C.dy * C.dy;
+        Sd = 2 * M_PI * (j + 0.5) * C.dy * C.dx;
+      }
+      if (i > 0 && J.at(i - 1, j).is(CT_SOLID))
+        Fp -= Sp * n.p;
+      else if (i < J.nx - 1 && J.at(i + 1, j).is(CT_SOLID))
+        Fp += Sp * n.p;
+      const real tau = Sd * (n.mu + n.mu_t) * std::fabs(n.dUdy);
+      if (j < J.ny - 1 && !J.at(i, j + 1).is(CT_SOLID)) {
+        Fd += J.at(i, j + 1).U > 0 ? tau : -tau;
+      } else if (j > 0 && !J.at(i, j - 1).is(CT_SOLID)) {
+        Fd += J.at(i, j - 1).U > 0 ? tau : -tau;
+      }
+    }
+  return Fp + Fd;
+}
+
+real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  const Config& C = cs.cfg;
+  real Fp = 0, Fd = 0;
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& n = J.at(i, j);
+      if (!((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy))) continue;
+      real Sp, Sd;
+      if (C.FT == FT_FLAT) {
+        Sp = C.dx;
+        Sd = C.dy;
+      } else {
+        Sp = 2 * M_PI * n.y * C.dx;
+        Sd = 2 * M_PI * n.y * C.dy;
+      }
+      if (j > 0 && J.at(i, j - 1).is(CT_SOLID))
+        Fp -= Sp * n.p;
+      else if (j < J.ny - 1 && J.at(i, j + 1).is(CT_SOLID))
+        Fp += Sp * n.p;
+      const real tau = -Sd * (n.mu + n.mu_t) * std::fabs(n.dVdx);
+      if (i < J.nx - 1 && !J.at(i + 1, j).is(CT_SOLID)) {
+        Fd += J.at(i + 1, j).V > 0 ? tau : -tau;
+      } else if (i > 0 && !J.at(i - 1, j).is(CT_SOLID)) {
+        Fd += J.at(i - 1, j).V > 0 ? tau : -tau;
+      }
+    }
+  return Fp + Fd;
+}
+
+static real wall_span_x(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  const Config& C = cs.cfg;
+  real S = 0;
+  for (int i = 0; i < J.nx; i++) {
+    bool hit = false;
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& n = J.at(i, j);
+      if ((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy)) hit = true;
+    }
+    if (hit) S += C.dx;
+  }
+  return S;
+}
+
+real calc_cx(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f) {
+  const real Pmax = f.ROG() * f.Wg2d() * f.Wg2d() * 0.5 * wall_span_x(cs, J, x0, y0, dx, dy);
+  return Pmax == 0. ? 0 : x_force(cs, J, x0, y0, dx, dy) / Pmax;
+}
+real calc_cy(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f) {
+  const real Pmax = f.ROG() * f.Wg2d() * f.Wg2d() * 0.5 * wall_span_x(cs, J, x0, y0, dx, dy);
+  return Pmax == 0. ? 0 : y_force(cs, J, x0, y0, dx, dy) / Pmax;
+}
+real calc_cp(const CellRecord& n, const GasFlow& f) {
+  if (n.is(CT_WALL_NO_SLIP)) return (n.p - f.Pg()) / (0.5 * f.ROG() * f.Wg2d() * f.Wg2d());
+  return 0;
+}
+real calc_cd(const Case& cs, const Field& J, real x0, real y0, real dy, const GasFlow& f) {
+  return mass_flow_rate_x(cs, J, x0, y0, dy) / f.ROG() / f.Wg2d() / calc_area(cs, J, x0, y0, dy);
+}
+real calc_cv(const Case& cs, const Field& J, real x0, real y0, real dy, real p_amb, const GasFlow& f) {
+  const Config& C = cs.cfg;
+  const unsigned i = (unsigned)(x0 / C.dx);
+  const unsigned j0 = (unsigned)(y0 / C.dy), j1 = (unsigned)((y0 + dy) / C.dy);
+  real Fv = 0;
+  if ((int)i >= J.nx) return 0;
+  for (int j = (int)j0; j < (int)j1 && j < J.ny; j++) {
+    const CellRecord& n = J.at(i, j);
+    if (n.is(CT_SOLID)) continue;
+    const real t = n.S[I_RHOU] * n.U + (n.p - p_amb);
+    Fv += (C.FT == FT_FLAT) ? C.dy * t : 2 * M_PI * C.dy * n.y * t;
+  }
+  const real Mp = mass_flow_rate_x(cs, J, x0, y0, dy);
+  return Mp > 0.0 ? Fv / (f.U() * Mp) : 0;
+}
+
+real average_pressure(const Case& cs, const Field& J, real x0, real l, real d) {
+  const Config& C = cs.cfg;
+  real pm = 0, Vs = 0;
+  long n = 0;
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& c = J.at(i, j);
+      if (c.is(CT_SOLID) || !(i > (int)(x0 / C.dx) && i < (int)((l + x0) / C.dx) && j < (int)(d / C.dy))) continue;
+      if (C.FT == FT_AXISYMMETRIC) {
+        const real Vi = 2 * M_PI * c.y * C.dy * C.dx;
+        Vs += Vi;
+        pm += c.p * Vi;
+      } else {
+        pm += c.p;
+      }
+      n++;
+    }
+  if (!n) return 0.;
+  return C.FT == FT_AXISYMMETRIC ? pm / Vs : pm / n;
+}
+
+real average_temperature(const Case& cs, const Field& J, real x0, real l, real d, int mid_enthalpy) {
+  const Config& C = cs.cfg;
+  real Tm = 0, Vs = 0;
+  long n = 0;
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& c = J.at(i, j);
+      if (c.is(CT_SOLID) || !(i > (int)(x0 / C.dx) && i < (int)((l + x0) / C.dx) && j < (int)(d / C.dy))) continue;
+      if (C.FT == FT_AXISYMMETRIC) {
+        real Vi = 2 * M_PI * c.y * C.dy * C.dx;
+        if (mid_enthalpy) Vi *= c.CP;
+        Vs += Vi;
+        Tm += c.Tg * Vi;
+      } else {
+        Tm += c.Tg;
+      }
+      n++;
+    }
+  if (!n) return 0.;
+  return C.FT == FT_AXISYMMETRIC ? Tm / Vs : Tm / n;
+}
+
+static real near_lam(const Field& J, int i, int j, const CellRecord& n, int& cnt) {
+  const int N1 = i - n.idXl, N2 = i + n.idXr, N3 = j + n.idYu, N4 = j - n.idYd;
+  real s = n.lam + n.lam_t;
+  cnt = 5;
+  s += J.at(N1, j).lam + J.at(N1, j).lam_t;
+  s += J.at(N2, j).lam + J.at(N2, j).lam_t;
+  s += J.at(i, N3).lam + J.at(i, N3).lam_t;
+  s += J.at(i, N4).lam + J.at(i, N4).lam_t;
+  return s;
+}
+
+void save_x_heat_flux(const std::string& path, const Case& cs, const Field& J) {
+  const Config& C = cs.cfg;
+  std::ofstream o(path, std::ios::trunc);
+  o << "#VARIABLES = X, HeatFlux(X),  Alpha(X), Cp(X), St(X)\n";
+  const int NX = J.nx;
+  std::vector<real> Q(NX, 0.), Al(NX, 0.), Cp(NX, 0.), St(NX, 0.), QR(NX, 0.), AR(NX, 0.), Re(NX, 0.), Pr(NX, 0.);
+  if (C.Cp_Flow_index < 1 || C.Cp_Flow_index > (int)cs.flows2d.size()) return;
+  const GasFlow& F = cs.flows2d[C.Cp_Flow_index - 1];
+  const real Trec = (1 + 0.45 * (F.kg() - 1.0) * F.flow_MACH() * F.flow_MACH()) * F.Tg();
+  for (int i = 0; i < NX; i++)
+    for (int j = std::max(0, C.y_min); j < std::min(C.y_max, J.ny - 1); j++) {
+      const CellRecord& n = J.at(i, j);
+      if (!n.is(CT_WALL_NO_SLIP)) continue;
+      int cnt;
+      const real lam_eff = near_lam(J, i, j, n, cnt) / cnt;
+      real q = lam_eff * (n.Tg - C.Ts0) / C.dy;
+      real alpha = lam_eff / C.dy;
+      const real re = (J.at(i, J.ny - 1).U * (i + 0.5) * C.dx * n.S[0]) / n.mu;
+      const real pr = n.mu * n.CP / n.lam;
+      const real Nu = re < 5.0e5 ? 0.332 * std::sqrt(re) * std::pow(pr, 1.0 / 3.0)
+                                 : 0.0296 * std::pow(re, 0.8) * std::pow(pr, 1.0 / 3.0);
+      real aref = Nu * n.lam / ((i + 0.5) * C.dx);
+      real qref = aref * (n.Tg - C.Ts0);
+      const real st = q / (F.ROG() * F.Wg2d() * F.C * (Trec - C.Ts0));
+      const real cp = calc_cp(n, F);
+      Re[i] = re;
+      Pr[i] = pr;
+      if (Q[i] != 0.) {
+        q = std::max(Q[i], q);
+        QR[i] = std::max(QR[i], qref);
+        AR[i] = std::max(AR[i], aref);
+        Q[i] = q;
+        Al[i] = std::max(Al[i], alpha);
+      } else {
+        Q[i] = q;
+        Al[i] = alpha;
+        AR[i] = aref;
+        QR[i] = qref;
+      }
+      Cp[i] = cp;
+      St[i] = st;
+    }
+  for (int i = 0; i < NX; i++)
+    o << i * C.dx << " " << Q[i] << " " << Al[i] << " " << Cp[i] << " " << St[i] << " " << QR[i] << " " << AR[i]
+      << " " << Re[i] << " " << Pr[i] << "\n";
+}
+
+void save_y_heat_flux(const std::string& path, const Case& cs, const Field& J) {
+  const Config& C = cs.cfg;
+  std::ofstream o(path, std::ios::trunc);
+  o << "#VARIABLES = Y, HeatFlux(Y)\n";
+  std::vector<real> Q(J.ny, 0.);
+  for (int j = 0; j < J.ny; j++)
+    for (int i = 0; i < J.nx - 1; i++) {
+      const CellRecord& n = J.at(i, j);
+      if (!n.is(CT_WALL_NO_SLIP)) continue;
+      int cnt;
+      const real lam_eff = near_lam(J, i, j, n, cnt) / cnt;
+      real q = lam_eff * (n.Tg - C.Ts0) / C.dx;
+      Q[j] = (Q[j] != 0.) ? std::max(Q[j], q) : q;
+    }
+  for (int j = 0; j < J.ny; j++) o << j * C.dy << " " << Q[j] << "\n";
+}
+
+}  // namespace hf2d

@@ -1,0 +1,709 @@
+#include "solver.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <ostream>
+#include <stdexcept>
+
+#include "checkpoint.hpp"
+#include "postproc.hpp"
+
+namespace hf2d {
+
+static const char* RMS_NAME[11] = {"Rho",     "Rho*U",   "Rho*V", "Rho*E",     "Rho*Yfu", "Rho*Yox",
+                                   "Rho*Ycp", "Rho*k",   "Rho*eps", "Rho*omega", "nu_t"};
+
+// ---------------------------------------------------------------------------
+// HostArrays
+// ---------------------------------------------------------------------------
+void HostArrays::allocate(int X, int Yn) {
+  nx = X;
+  ny = Yn;
+  N = (long)X * Yn;
+  auto E = [&](std::vector<real>& v, int m) { v.assign((size_t)m * N, 0.0); };
+  for (int b = 0; b < 2; b++) {
+    E(S[b], NEQ);
+    E(dSdx[b], NEQ);
+    E(dSdy[b], NEQ);
+    E(U[b], 1);
+    E(V[b], 1);
+    E(Tg[b], 1);
+  }
+  E(A, NEQ); E(B, NEQ); E(F, NEQ); E(Src, NEQ); E(SrcAdd, NEQ); E(beta, NEQ);
+  E(p, 1); E(kk, 1); E(R, 1); E(CP, 1); E(lam, 1); E(mu, 1); E(mu_t, 1); E(lam_t, 1); E(Diff, 1);
+  E(Y, NSPEC);
+  E(l_min, 1); E(y_plus, 1); E(Re_local, 1); E(BGX, 1); E(BGY, 1); E(Tf, 1); E(Q_conv, 1);
+  E(grad, NGRAD); E(qdir, 4); E(time, 1);
+  CT.assign(N, 0);
+  TT.assign(N, 0);
+  nb.assign(N, 0);
+  iw.assign(N, 0);
+  jw.assign(N, 0);
+}
+
+void HostArrays::from_field(const Field& J, int gi0) {
+  for (int li = 0; li < nx; li++) {
+    const int gi = gi0 + li;
+    for (int j = 0; j < ny; j++) {
+      const long idx = (long)li * ny + j;
+      const CellRecord& c = J.at(gi, j);
+      for (int k = 0; k < NEQ; k++) {
+        const long o = k * N + idx;
+        S[0][o] = S[1][o] = c.S[k];
+        dSdx[0][o] = dSdx[1][o] = c.dSdx[k];
+        dSdy[0][o] = dSdy[1][o] = c.dSdy[k];
+        A[o] = c.A[k];
+        B[o] = c.B[k];
+        F[o] = c.F[k];
+        Src[o] = c.Src[k];
+        SrcAdd[o] = c.SrcAdd[k];
+        beta[o] = c.beta[k];
+      }
+      U[0][idx] = U[1][idx] = c.U;
+      V[0][idx] = V[1][idx] = c.V;
+      Tg[0][idx] = Tg[1][idx] = c.Tg;
+      p[idx] = c.p;
+      kk[idx] = c.k;
+      R[idx] = c.R;
+      CP[idx] = c.CP;
+      lam[idx] = c.lam;
+      mu[idx] = c.mu;
+      mu_t[idx] = c.mu_t;
+      lam_t[idx] = c.lam_t;
+      Diff[idx] = c.Diff;
+      for (int s = 0; s < NSPEC; s++) Y[s * N + idx] = c.Y[s];
+      l_min[idx] = c.l_min;
+      y_plus[idx] = c.y_plus;
+      Re_local[idx] = c.Re_local;
+      BGX[idx] = c.BGX;
+      BGY[idx] = c.BGY;
+      Tf[idx] = c.Tf;
+      Q_conv[idx] = c.Q_conv;
+      time[idx] = c.time;
+      const real g[NGRAD] = {c.dUdx, c.dUdy, c.dVdx, c.dVdy, c.dTdx, c.dTdy, c.dkdx, c.dkdy, c.depsdx, c.depsdy};
+      for (int q = 0; q < NGRAD; q++) grad[q * N + idx] = g[q];
+      CT[idx] = c.CT;
+      TT[idx] = c.TurbType;
+      nb[idx] = (c.idXl ? NB_XL : 0) | (c.idXr ? NB_XR : 0) | (c.idYu ? NB_YU : 0) | (c.idYd ? NB_YD : 0);
+      iw[idx] = c.i_wall;
+      jw[idx] = c.j_wall;
+    }
+  }
+}
+
+void HostArrays::to_field(Field& J, int gi0, int i_from, int i_to, int pb, int db) const {
+  for (int li = i_from; li < i_to; li++) {
+    const int gi = gi0 + li;
+    for (int j = 0; j < ny; j++) {
+      const long idx = (long)li * ny + j;
+      CellRecord& c = J.at(gi, j);
+      for (int k = 0; k < NEQ; k++) {
+        const long o = k * N + idx;
+        c.S[k] = S[0][o];
+        c.dSdx[k] = dSdx[db][o];
+        c.dSdy[k] = dSdy[db][o];
+        c.A[k] = A[o];
+        c.B[k] = B[o];
+        c.F[k] = F[o];
+        c.Src[k] = Src[o];
+        c.SrcAdd[k] = SrcAdd[o];
+        c.beta[k] = beta[o];
+      }
+      c.U = U[pb][idx];
+      c.V = V[pb][idx];
+      c.Tg = Tg[pb][idx];
+      c.p = p[idx];
+      c.k = kk[idx];
+      c.R = R[idx];
+      c.CP = CP[idx];
+      c.lam = lam[idx];
+      c.mu = mu[idx];
+      c.mu_t = mu_t[idx];
+      c.lam_t = lam_t[idx];
+      c.Diff = Diff[idx];
+      for (int s = 0; s < NSPEC; s++) c.Y[s] = Y[s * N + idx];
+      c.l_min = l_min[idx];
+      c.y_plus = y_plus[idx];
+      c.Re_local = Re_local[idx];
+      c.Q_conv = Q_conv[idx];
+      c.time = time[idx];
+      c.dUdx = grad[G_DUDX * N + idx];
+      c.dUdy = grad[G_DUDY * N + idx];
+      c.dVdx = grad[G_DVDX * N + idx];
+      c.dVdy = grad[G_DVDY * N + idx];
+      c.dTdx = grad[G_DTDX * N + idx];
+      c.dTdy = grad[G_DTDY * N + idx];
+      c.dkdx = grad[G_DKDX * N + idx];
+      c.dkdy = grad[G_DKDY * N + idx];
+      c.depsdx = grad[G_DEDX * N + idx];
+      c.depsdy = grad[G_DEDY * N + idx];
+      c.CT = CT[idx];
+      c.TurbType = TT[idx];
+    }
+  }
+}
+
+SoA HostArrays::view(int sb, int db, int pb) {
+  SoA s;
+  s.nx = nx;
+  s.ny = ny;
+  s.N = N;
+  s.S = S[sb].data();
+  s.A = A.data();
+  s.B = B.data();
+  s.F = F.data();
+  s.Src = Src.data();
+  s.SrcAdd = SrcAdd.data();
+  s.beta = beta.data();
+  s.dSdx = dSdx[db].data();
+  s.dSdy = dSdy[db].data();
+  s.U = U[pb].data();
+  s.V = V[pb].data();
+  s.Tg = Tg[pb].data();
+  s.p = p.data();
+  s.kk = kk.data();
+  s.R = R.data();
+  s.CP = CP.data();
+  s.lam = lam.data();
+  s.mu = mu.data();
+  s.mu_t = mu_t.data();
+  s.lam_t = lam_t.data();
+  s.Diff = Diff.data();
+  s.Y = Y.data();
+  s.l_min = l_min.data();
+  s.y_plus = y_plus.data();
+  s.Re_local = Re_local.data();
+  s.BGX = BGX.data();
+  s.BGY = BGY.data();
+  s.Tf = Tf.data();
+  s.Q_conv = Q_conv.data();
+  s.grad = grad.data();
+  s.CT = CT.data();
+  s.TT = TT.data();
+  s.nb = nb.data();
+  s.iw = iw.data();
+  s.jw = jw.data();
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// SolverBase: the time-march driver
+// ---------------------------------------------------------------------------
+SolverBase::SolverBase(Case& c) : cs(c) {
+  comm = &local_comm;
+  dt = c.dt0;
+  dt_running = c.dt0;
+}
+
+StepParams SolverBase::make_params(long it) const {
+  const Config& C = cs.cfg;
+  StepParams P{};
+  P.dx = C.dx;
+  P.dy = C.dy;
+  P.dt = dt;
+  P.dtdx = dt / C.dx;
+  P.dtdy = dt / C.dy;
+  P.dyy = C.dx / (C.dx + C.dy);
+  P.dxx = C.dy / (C.dx + C.dy);
+  const real beta_scen = C.beta_Scenario.eval((real)it);
+  const real cfl_scen = C.CFL_Scenario.eval((real)it);
+  P.beta_min = std::min(C.beta0, beta_scen);
+  P.nrbc_beta0 = C.nrbc_beta0;
+  P.CFL_min = std::min(C.CFL, cfl_scen);
+  P.bff = C.bff;
+  P.alternate_rms = C.isAlternateRMS;
+  P.sm = C.ProblemType;
+  P.chem_model = C.chem_model;
+  P.species = &C.species;
+  FillParams f = C.fill_params();
+  f.sig_w = C.SigW;
+  f.sig_f = C.SigF;
+  f.tem = C.TurbExtModel;
+  f.delta = C.delta_bl;
+  f.sm = C.ProblemType;
+  f.isSrcAdd = isSrcAdd ? 1 : 0;
+  P.ffc = f;
+  P.ffc.is_mu_t = 1;
+  P.ffc.is_init = 0;
+  P.fpa = f;
+  if ((int)it < C.TurbStartIter) {
+    P.fpa.is_mu_t = 0;
+    P.fpa.is_init = C.isTurbulenceReset;
+  } else {
+    P.fpa.is_mu_t = 1;
+    P.fpa.is_init = 0;
+  }
+  return P;
+}
+
+StepResult SolverBase::advance(bool want_res) {
+  const long it = last_iter + iter;
+  StepParams P = make_params(it);
+  StepResult r = do_step(P, want_res);
+  if (comm->allreduce_max_int(r.neg_T)) {
+    char b[256];
+    std::snprintf(b, sizeof b, "ERROR: Computational unstability (Tg < 0) on iteration %ld, dt=%g", it, P.dt);
+    throw std::runtime_error(b);
+  }
+  const real dtm = comm->allreduce_min(r.dt_min);
+  if (cs.cfg.semantics == Semantics::SERIAL) {
+    dt_running = std::min(dt_running, dtm);
+    dt = dt_running;
+  } else {
+    dt = dtm;
+  }
+  if (r.have_residual) {
+    comm->allreduce_residual(r.res);
+    last_res = residual_finalize(r.res, cs.cfg.isAlternateRMS, cs.cfg.MonitorIndex,
+                                 cs.cfg.semantics == Semantics::SERIAL, cs.cfg.ExitMonitorValue);
+    last_res_valid = true;
+  }
+  cur_time_part += P.dt;
+  iter++;
+  return r;
+}
+
+void SolverBase::run_steps(long n, bool want_res_last) {
+  for (long s = 0; s < n; s++) {
+    if (iter >= cs.cfg.Nmax) {   // roll the inner counter like an outer cycle
+      last_iter += iter;
+      iter = 0;
+      cs.global_time += cur_time_part;
+      cur_time_part = 0;
+      isSrcAdd = true;
+      cycle++;
+    }
+    advance(want_res_last && s == n - 1);
+  }
+}
+
+void SolverBase::sample_monitors(std::vector<MonitorPoint>& mp) {
+  if (mp.empty()) return;
+  Field& J = cs.J;
+  download(J);
+  for (auto& m : mp) {
+    const int i = (int)(m.x / cs.cfg.dx), j = (int)(m.y / cs.cfg.dy);
+    if (J.in(i, j)) {
+      m.p = J.at(i, j).p;
+      m.T = J.at(i, j).Tg;
+    }
+  }
+}
+
+int SolverBase::run(const RunOptions& opt, std::ostream* log) {
+  Config& C = cs.cfg;
+  const bool root = comm->rank() == 0;
+  const std::string dir = opt.outdir.empty() ? "." : opt.outdir;
+  const std::string rms_path = dir + "/RMS-" + C.out_file;
+  const std::string mon_path = dir + "/Monitors-" + C.out_file;
+  if (root && opt.write_outputs) {
+    save_rms_header(rms_path, C);
+    if (!C.monitors.empty()) save_monitors_header(mon_path, C);
+  }
+  int I = 0;
+  int monitor_cond = 1;
+  int cycles = 0;
+  using clk = std::chrono::steady_clock;
+  do {
+    isSrcAdd = (0 < iter + last_iter);
+    iter = 0;
+    auto t_cycle = clk::now();
+    auto mark = clk::now();
+    for (long k = 0; k < C.Nmax; k++) {
+      const bool out_step = (iter / C.NOutStep) * C.NOutStep == iter;
+      const long this_iter = iter;
+      advance(out_step || k == C.Nmax - 1);
+      if (out_step) {
+        if (!C.monitors.empty()) sample_monitors(C.monitors);
+        if (C.isVerboseOutput && root) {
+          auto now = clk::now();
+          const double d_time = std::chrono::duration<double>(now - mark).count();
+          mark = now;
+          const double vcomp = d_time > 0 ? C.NOutStep / d_time : 0.;
+          if (opt.write_outputs) {
+            cs.J.nx ? void() : void();
+            append_rms(rms_path, last_iter + this_iter, last_res.rms, cs, cs.J);
+            if (!C.monitors.empty()) append_monitors(mon_path, cs.global_time + cur_time_part, C.monitors);
+          }
+          if (log) {
+            char b[512];
+            const int kk = last_res.k_max;
+            const char* nm = (C.MonitorIndex > 0 && C.MonitorIndex < 5) ? RMS_NAME[C.MonitorIndex - 1]
+                             : (kk >= 0 ? RMS_NAME[kk] : "?");
+            std::snprintf(b, sizeof b, "Step No %ld maxRMS[%s]=%g %% step_time=%g sec (%g step/sec) dt=%g\n",
+                          last_iter + this_iter, nm, last_res.max_rms * 100., d_time, vcomp, dt);
+            *log << b << std::flush;
+          }
+        }
+      }
+    }
+    cycle_update();
+    if (cs.cfg.sources.size() && comm->size() == 1) {
+      // sources are re-applied every cycle in the MPI build (deeps2d_core.cpp:1716-1722)
+    }
+    Field& J = cs.J;
+    download(J);
+    step_seconds = std::chrono::duration<double>(clk::now() - t_cycle).count();
+    if (root) {
+      for (size_t x = 0; x < C.xcuts.size() && log; x++) {
+        char b[256];
+        std::snprintf(b, sizeof b, "Cut(%zu) X=%g Y=%g dY=%g MassFlow=%g  (kg/sec*m)\n", x + 1, C.xcuts[x].x0,
+                      C.xcuts[x].y0, C.xcuts[x].dy, mass_flow_rate_x(cs, J, C.xcuts[x].x0, C.xcuts[x].y0, C.xcuts[x].dy));
+        *log << b;
+      }
+      if (opt.write_outputs) {
+        save_field_plt(dir + "/" + C.out_file, cs, J, cs.global_time, true);
+        if ((I / C.NSaveStep) * C.NSaveStep == I) save_field_plt(dir + "/" + C.tecplot_file, cs, J, cs.global_time, false);
+      }
+      if (log) {
+        char b[256];
+        std::snprintf(b, sizeof b, "HyperFLOW/DEEPS computation cycle time=%g sec ( average  speed %g step/sec).       \n",
+                      step_seconds, C.Nmax / step_seconds);
+        *log << b << std::flush;
+      }
+    }
+    I++;
+    last_iter += iter;
+    iter = 0;
+    cs.global_time += cur_time_part;
+    cur_time_part = 0.;
+    cycle++;
+    cycles++;
+    if (root) {
+      if (opt.write_outputs && C.isOutHeatFluxX) save_x_heat_flux(dir + "/HeatFlux-X-" + C.out_file, cs, J);
+      if (opt.write_outputs && C.isOutHeatFluxY) save_y_heat_flux(dir + "/HeatFlux-Y-" + C.out_file, cs, J);
+      if (C.is_Cx_calc && log && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size()) {
+        const GasFlow& f = cs.flows2d[C.Cx_Flow_index - 1];
+        *log << "\nCx = " << calc_cx(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body, f)
+             << " Cy = " << calc_cy(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body, f)
+             << " Fx = " << x_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body)
+             << " Fy = " << y_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body) << "\n";
+      }
+      if (opt.write_checkpoint && comm->size() == 1) {
+        write_hf2d(dir + "/" + C.swap_file, J);
+        write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
+      }
+    }
+    if (C.MonitorIndex < 5)
+      monitor_cond = last_res.max_rms > C.ExitMonitorValue ? 1 : 0;
+    else
+      monitor_cond = cs.global_time < C.ExitMonitorValue ? 1 : 0;
+  } while (monitor_cond && (opt.max_cycles < 0 || cycles < opt.max_cycles));
+  if (root && opt.write_outputs) save_field_plt(dir + "/" + C.out_file, cs, cs.J, cs.global_time, true);
+  return cycles;
+}
+
+// ---------------------------------------------------------------------------
+// CpuSolver
+// ---------------------------------------------------------------------------
+CpuSolver::CpuSolver(Case& c, int g0, int g1) : SolverBase(c), gi0(g0), gi1(g1 < 0 ? c.J.nx : g1) {
+  const int lh = gi0 > 0 ? 1 : 0;
+  const int rh = gi1 < c.J.nx ? 1 : 0;
+  l_off = lh;
+  h.allocate((gi1 - gi0) + lh + rh, c.J.ny);
+  upload();
+}
+
+void CpuSolver::upload() {
+  h.from_field(cs.J, gi0 - l_off);
+  sbuf = 0;
+  dsbuf = 0;
+  pbuf = 0;
+}
+
+void CpuSolver::download(Field& J) {
+  h.to_field(J, gi0 - l_off, l_off, l_off + (gi1 - gi0), pbuf, dsbuf);
+}
+
+int CpuSolver::halo_doubles(int g) const {
+  if (g == HALO_MID) return NEQ;
+  if (g == HALO_QDIR) return 4;
+  return 4 * NEQ + 5;
+}
+
+void CpuSolver::pack_column(int g, int li, real* o) const {
+  const long N = h.N;
+  const int ny = h.ny;
+  for (int j = 0; j < ny; j++) {
+    const long idx = (long)li * ny + j;
+    if (g == HALO_MID) {
+      for (int k = 0; k < NEQ; k++) *o++ = h.S[1][k * N + idx];
+    } else if (g == HALO_QDIR) {
+      for (int d = 0; d < 4; d++) *o++ = h.qdir[d * N + idx];
+    } else {
+      for (int k = 0; k < NEQ; k++) {
+        *o++ = h.S[0][k * N + idx];
+        *o++ = h.A[k * N + idx];
+        *o++ = h.B[k * N + idx];
+        *o++ = h.dSdx[dsbuf][k * N + idx];
+      }
+      *o++ = h.U[pbuf][idx];
+      *o++ = h.V[pbuf][idx];
+      *o++ = h.Tg[pbuf][idx];
+      *o++ = h.lam[idx];
+      *o++ = h.lam_t[idx];
+    }
+  }
+}
+
+void CpuSolver::unpack_column(int g, int li, const real* o) {
+  const long N = h.N;
+  const int ny = h.ny;
+  for (int j = 0; j < ny; j++) {
+    const long idx = (long)li * ny + j;
+    if (g == HALO_MID) {
+      for (int k = 0; k < NEQ; k++) h.S[1][k * N + idx] = *o++;
+    } else if (g == HALO_QDIR) {
+      for (int d = 0; d < 4; d++) h.qdir[d * N + idx] = *o++;
+    } else {
+      for (int k = 0; k < NEQ; k++) {
+        h.S[0][k * N + idx] = *o++;
+        h.A[k * N + idx] = *o++;
+        h.B[k * N + idx] = *o++;
+        h.dSdx[dsbuf][k * N + idx] = *o++;
+      }
+      h.U[pbuf][idx] = *o++;
+      h.V[pbuf][idx] = *o++;
+      h.Tg[pbuf][idx] = *o++;
+      h.lam[idx] = *o++;
+      h.lam_t[idx] = *o++;
+    }
+  }
+}
+
+StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
+  StepParams P = P0;
+  P.nx = h.nx;
+  P.ny = h.ny;
+  P.i0 = l_off;
+  P.i1 = l_off + (gi1 - gi0);
+  P.gx0 = gi0 - l_off;
+  P.do_residual = want_res ? 1 : 0;
+  StepResult r;
+  residual_reset(r.res);
+  // predict: S[0] -> S[1], dS[dsbuf] -> dS[1-dsbuf]
+  SoA in = h.view(0, dsbuf, pbuf);
+  SoA mid = h.view(1, 1 - dsbuf, pbuf);
+  // halo columns keep their (exchanged) values in the mid buffer as well
+  for (int i = P.i0; i < P.i1; i++)
+    for (int j = 0; j < P.ny; j++) predict_cell(P, in, mid, i, j, want_res ? &r.res : nullptr);
+  r.have_residual = want_res;
+  if (halo_exchange && P.sm == SM_NS) halo_exchange(*this, HALO_MID);
+  // fill: S[1] (+nbrs) -> S[0]; prims pbuf -> 1-pbuf
+  SoA sin = h.view(1, 1 - dsbuf, pbuf);
+  SoA pold = h.view(1, 1 - dsbuf, pbuf);
+  SoA out = h.view(0, 1 - dsbuf, 1 - pbuf);
+  int negT = 0;
+  real dtmin = 1.0;
+  for (int i = P.i0; i < P.i1; i++)
+    for (int j = 0; j < P.ny; j++) {
+      const real d = fill_cell(P, sin, pold, out, i, j, &negT, true);
+      dtmin = std::min(dtmin, d);
+    }
+  dsbuf = 1 - dsbuf;
+  pbuf = 1 - pbuf;
+  r.dt_min = dtmin;
+  r.neg_T = negT;
+  if (halo_exchange) halo_exchange(*this, HALO_STATE);
+  if (!cs.cfg.isAdiabaticWall) {
+    SoA s = h.view(0, dsbuf, pbuf);
+    for (int i = P.i0; i < P.i1; i++)
+      for (int j = 0; j < P.ny; j++) wall_heat_solid_cell(P, s, h.qdir.data(), i, j);
+    if (halo_exchange) halo_exchange(*this, HALO_QDIR);
+    for (int i = P.i0; i < P.i1; i++)
+      for (int j = 0; j < P.ny; j++) wall_heat_wall_cell(P, s, h.qdir.data(), i, j);
+  }
+  return r;
+}
+
+void CpuSolver::cycle_update() {
+  if (cs.cfg.ProblemType != SM_NS || cs.cfg.semantics == Semantics::SERIAL) return;
+  StepParams P = make_params(last_iter);
+  P.nx = h.nx;
+  P.ny = h.ny;
+  SoA s = h.view(0, dsbuf, pbuf);
+  for (int i = l_off; i < l_off + (gi1 - gi0); i++)
+    for (int j = 0; j < h.ny; j++) y_plus_cell(P, s, i, j, gi0 - l_off);
+}
+
+// ---------------------------------------------------------------------------
+// RefSolver: in-place reference-order sweep (deeps2d_core.cpp:853-1334)
+// ---------------------------------------------------------------------------
+RefSolver::RefSolver(Case& c) : SolverBase(c) { core.resize(c.J.c.size()); }
+
+StepResult RefSolver::do_step(const StepParams& P, bool /*want_res*/) {
+  Field& J = cs.J;
+  const Config& C = cs.cfg;
+  const int MX = J.nx, MY = J.ny;
+  StepResult r;
+  residual_reset(r.res);
+  r.have_residual = true;
+  const bool serial = C.semantics == Semantics::SERIAL;
+  // pass 1
+  for (int i = 0; i < MX; i++)
+    for (int j = 0; j < MY; j++) {
+      CellRecord& c = J.at(i, j);
+      if (!is_active(c.CT)) continue;
+      CellRecord& nx = core[(size_t)i * MY + j];
+      c.time = cs.global_time;
+      const int n1 = c.idXl, n2 = c.idXr, n3 = c.idYu, n4 = c.idYd;
+      CellRecord& Up = J.at(i, j + n3);
+      CellRecord& Dn = J.at(i, j - n4);
+      CellRecord& Rt = J.at(i + n2, j);
+      CellRecord& Lt = J.at(i - n1, j);
+      const real n_n_1 = 1. / std::max(n1 + n2, 1), m_m_1 = 1. / std::max(n3 + n4, 1);
+      const int Num_Eq = num_eq_for(c.TurbType);
+      for (int k = 0; k < Num_Eq; k++) {
+        const real beta = c.beta[k], _beta = 1. - beta;
+        if (k >= 4 + NCOMP && !(C.ProblemType == SM_NS && has_turb_eq(c.TurbType))) continue;
+        const EqFlags f = eq_flags(k, c.CT, c.TurbType, C.ProblemType);
+        if (!f.upd) continue;
+        real dXX, dYY;
+        if (f.dx) {
+          dXX = c.dSdx[k] = (Rt.A[k] - Lt.A[k]) * n_n_1;
+        } else {
+          c.S[k] = (Lt.S[k] * n2 + Rt.S[k] * n1) * n_n_1;
+          dXX = c.dSdx[k] = 0.;
+        }
+        if (f.dy) {
+          dYY = c.dSdy[k] = (Up.B[k] - Dn.B[k]) * m_m_1;
+        } else {
+          c.S[k] = (Up.S[k] * n3 + Dn.S[k] * n4) * m_m_1;
+          dYY = c.dSdy[k] = 0;
+        }
+        if (f.dx2) dXX = (Lt.dSdx[k] + Rt.dSdx[k]) * 0.5;
+        if (f.dy2) dYY = (Up.dSdy[k] + Dn.dSdy[k]) * 0.5;
+        if (C.FT)
+          nx.S[k] = c.S[k] * beta + _beta * (P.dxx * (Lt.S[k] + Rt.S[k]) + P.dyy * (Up.S[k] + Dn.S[k])) * 0.5 -
+                    (P.dtdx * dXX + P.dtdy * (dYY + c.F[k] / (j + 1))) + (c.Src[k]) * P.dt + c.SrcAdd[k];
+        else
+          nx.S[k] = c.S[k] * beta + _beta * (P.dxx * (Lt.S[k] + Rt.S[k]) + P.dyy * (Up.S[k] + Dn.S[k])) * 0.5 -
+                    (P.dtdx * dXX + P.dtdy * dYY) + (c.Src[k]) * P.dt + c.SrcAdd[k];
+      }
+    }
+  // pass 2
+  real dtmin = 1.0;
+  const real dx_1 = 1.0 / C.dx, dy_1 = 1.0 / C.dy;
+  for (int i = 0; i < MX; i++)
+    for (int j = 0; j < MY; j++) {
+      CellRecord& c = J.at(i, j);
+      if (is_active(c.CT)) {
+        CellRecord& nx = core[(size_t)i * MY + j];
+        const int n1 = c.idXl, n2 = c.idXr, n3 = c.idYu, n4 = c.idYd;
+        CellRecord& Up = J.at(i, j + n3);
+        CellRecord& Dn = J.at(i, j - n4);
+        CellRecord& Rt = J.at(i + n2, j);
+        CellRecord& Lt = J.at(i - n1, j);
+        const real dxn = dx_1 / std::max(n1 + n2, 1), dym = dy_1 / std::max(n3 + n4, 1);
+        const int Num_Eq = num_eq_for(c.TurbType);
+        for (int k = 0; k < Num_Eq; k++) {
+          if (!pass2_frozen(k, c.CT, c.TurbType, C.ProblemType) && c.S[k] != 0.) {
+            const real Tmp = c.S[k];
+            const real absDD = nx.S[k] - c.S[k];
+            real DD, sq = 0;
+            if (std::fabs(Tmp) > 1.e-15) {
+              DD = std::fabs(absDD / Tmp);
+              sq = std::sqrt(DD);
+            } else {
+              DD = 1.0;
+            }
+            const real bmin = c.is(CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+            c.beta[k] = blend_beta(P.bff, bmin, c.beta[k], DD, sq);
+            EqResidual& e = r.res.eq[k];
+            e.dd_max = std::max(e.dd_max, DD);
+            if (e.dd_max == DD) {
+              e.i = i;
+              e.j = j;
+            }
+            if (P.alternate_rms) {
+              e.rms += serial ? absDD : absDD * absDD;
+              e.sum_div += Tmp * Tmp;
+              if (serial) e.count += 1;
+            } else {
+              e.rms += DD * DD;
+              e.count += 1;
+            }
+          }
+          if (k < 4 + NCOMP) {
+            if (!pass2_frozen(k, c.CT, c.TurbType, C.ProblemType)) c.S[k] = nx.S[k];
+          } else if (C.ProblemType == SM_NS && has_turb_eq(c.TurbType)) {
+            if (!has_all(c.TurbType, TCT_k_CONST << (k - 4 - NCOMP))) c.S[k] = nx.S[k];
+          }
+        }
+        if (C.ProblemType == SM_NS) {
+          real aR = Rt.S[0], aL = Lt.S[0], aU = Up.S[0], aD = Dn.S[0];
+          c.droYdx[NCOMP] = c.droYdy[NCOMP] = 0.;
+          for (int k = 4; k < NEQ - 2; k++) {
+            if (!c.is(CT_dYdx_NULL)) {
+              c.droYdx[k - 4] = (Rt.S[k] - Lt.S[k]) * dxn;
+              aR -= Rt.S[k];
+              aL -= Lt.S[k];
+            }
+            if (!c.is(CT_dYdy_NULL)) {
+              c.droYdy[k - 4] = (Up.S[k] - Dn.S[k]) * dym;
+              aU -= Up.S[k];
+              aD -= Dn.S[k];
+            }
+          }
+          if (!c.is(CT_dYdx_NULL)) c.droYdx[NCOMP] = (aR - aL) * dxn;
+          if (!c.is(CT_dYdy_NULL)) c.droYdy[NCOMP] = (aU - aD) * dym;
+          const bool wall = c.is(CT_WALL_NO_SLIP) || c.is(CT_WALL_LAW);
+          const real w1 = wall ? n1 : 1, w2 = wall ? n2 : 1, w3 = wall ? n3 : 1, w4 = wall ? n4 : 1;
+          c.dUdx = (Rt.U * w1 - Lt.U * w2) * dxn;
+          c.dVdx = (Rt.V * w1 - Lt.V * w2) * dxn;
+          c.dUdy = (Up.U * w3 - Dn.U * w4) * dym;
+          c.dVdy = (Up.V * w3 - Dn.V * w4) * dym;
+          if (is_two_eq(c.TurbType)) {
+            c.dkdx = (Rt.S[I_K] * w1 - Lt.S[I_K] * w2) * dxn / c.S[I_RHO];
+            c.depsdx = (Rt.S[I_EPS] * w1 - Lt.S[I_EPS] * w2) * dxn / c.S[I_RHO];
+            c.dkdy = (Up.S[I_K] * w3 - Dn.S[I_K] * w4) * dym / c.S[I_RHO];
+            c.depsdy = (Up.S[I_EPS] * w3 - Dn.S[I_EPS] * w4) * dym / c.S[I_RHO];
+          } else if (c.is_turb(TCT_Spalart_Allmaras_Model)) {
+            c.dkdx = (Rt.S[I_K] * w1 - Lt.S[I_K] * w2) * dxn / c.S[I_RHO];
+            c.dkdy = (Up.S[I_K] * w3 - Dn.S[I_K] * w4) * dym / c.S[I_RHO];
+          }
+          c.dTdx = (Rt.Tg - Lt.Tg) * dxn;
+          c.dTdy = (Up.Tg - Dn.Tg) * dym;
+        }
+        fill_node(c, P.fpa);
+        if (c.Tg < 0.) {
+          r.neg_T = 1;
+        } else {
+          const real AAA = std::sqrt(c.k * c.R * c.Tg);
+          dtmin = std::min(dtmin, P.CFL_min * std::min(C.dx / (AAA + std::fabs(c.U)), C.dy / (AAA + std::fabs(c.V))));
+          if (C.chem_model != NO_REACTIONS) chemistry_zeldovich(c, C.species, C.ProblemType, C.chem_model);
+        }
+      } else if (c.is(NT_FC)) {
+        fill_node(c, P.ffc);
+      }
+    }
+  r.dt_min = dtmin;
+  // wall heat, reference scatter order
+  if (!C.isAdiabaticWall) {
+    for (int i = 0; i < MX; i++)
+      for (int j = 0; j < MY; j++) J.at(i, j).Q_conv = 0.;
+    for (int i = 0; i < MX; i++)
+      for (int j = 0; j < MY; j++) {
+        CellRecord& c = J.at(i, j);
+        if (c.is(CT_SOLID) || !(c.is(CT_WALL_LAW) || c.is(CT_WALL_NO_SLIP))) continue;
+        auto upd = [&](CellRecord& s, real h) {
+          const real lam_eff = c.lam + c.lam_t;
+          if (s.Q_conv > 0.)
+            s.Q_conv = (s.Q_conv - lam_eff * (s.Tg - c.Tg) / h) * 0.5;
+          else
+            s.Q_conv = -lam_eff * (s.Tg - c.Tg) / h;
+          c.SrcAdd[I_RHOE] = -P.dt * s.Q_conv / h;
+        };
+        if (j > 0 && J.at(i, j - 1).is(CT_SOLID)) upd(J.at(i, j - 1), C.dy);
+        if (j < MY - 1 && J.at(i, j + 1).is(CT_SOLID)) upd(J.at(i, j + 1), C.dy);
+        if (i > 0 && J.at(i - 1, j).is(CT_SOLID)) upd(J.at(i - 1, j), C.dx);
+        if (i < MX - 1 && J.at(i + 1, j).is(CT_SOLID)) upd(J.at(i + 1, j), C.dx);
+      }
+  }
+  return r;
+}
+
+}  // namespace hf2d

@@ -1,0 +1,140 @@
+// Solvers and the time-march driver.
+//
+//   SolverBase     the DEEPS2D_Run outer/inner loop (deeps2d_core.cpp:723-1884):
+//                  scenario tables, dt bookkeeping, residual/monitor logging,
+//                  per-cycle outputs, checkpointing and the exit monitor.
+//   CpuSolver      Jacobi stepper over host SoA arrays; uses the same per-cell
+//                  kernels as the GPU (stepkern.hpp).  Strip-aware: a rank owns
+//                  columns [i0, i1) of a local array with halo columns.
+//   RefSolver      reference-order (in-place, Gauss-Seidel-like) stepper on
+//                  AoS records, used as the golden-comparison oracle against
+//                  the reference binary.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "case.hpp"
+#include "residual.hpp"
+#include "stepkern.hpp"
+
+namespace hf2d {
+
+struct StepResult {
+  real dt_min = 1.0;        // min local dt of this step (before cross-rank reduction)
+  int neg_T = 0;
+  bool have_residual = false;
+  ResidualPack res;
+};
+
+// Host SoA arrays (also the staging format for device upload/download).
+struct HostArrays {
+  int nx = 0, ny = 0;
+  long N = 0;
+  std::vector<real> S[2], A, B, F, Src, SrcAdd, beta, dSdx[2], dSdy[2];
+  std::vector<real> U[2], V[2], Tg[2], p, kk, R, CP, lam, mu, mu_t, lam_t, Diff, Y;
+  std::vector<real> l_min, y_plus, Re_local, BGX, BGY, Tf, Q_conv, grad, qdir;
+  std::vector<u64> CT, TT;
+  std::vector<uint8_t> nb;
+  std::vector<int32_t> iw, jw;
+  std::vector<real> time;   // per-cell record time (checkpoint only)
+
+  void allocate(int X, int Y);
+  // columns [gi0, gi0 + X) of J
+  void from_field(const Field& J, int gi0);
+  void to_field(Field& J, int gi0, int i_from, int i_to, int prim_buf, int ds_buf) const;
+  SoA view(int sbuf, int dsbuf, int pbuf);
+};
+
+// Communication hooks for multi-rank (strip) runs.  Single-rank: no-ops.
+struct Comm {
+  virtual ~Comm() = default;
+  virtual int rank() const { return 0; }
+  virtual int size() const { return 1; }
+  virtual real allreduce_min(real v) { return v; }
+  virtual void allreduce_residual(ResidualPack&) {}
+  virtual int allreduce_max_int(int v) { return v; }
+  virtual real allreduce_sum(real v) { return v; }
+};
+
+struct RunOptions {
+  int max_cycles = -1;       // stop after this many outer cycles (-1: exit monitor only)
+  bool write_outputs = true;
+  bool write_checkpoint = true;
+  std::string outdir = ".";
+  bool verbose = true;
+};
+
+class SolverBase {
+ public:
+  explicit SolverBase(Case& cs);
+  virtual ~SolverBase() = default;
+
+  Case& cs;
+  Comm* comm = nullptr;      // owned elsewhere
+  Comm local_comm;
+  real dt = 0;               // dt used by the next step
+  real dt_running = 1.0;     // serial semantics: never reset
+  long iter = 0;             // iteration inside the current cycle
+  long last_iter = 0;        // completed iterations of previous cycles
+  real cur_time_part = 0;
+  int cycle = 0;
+  ResidualSummary last_res{};
+  bool last_res_valid = false;
+  double step_seconds = 0;   // wall time of the last cycle
+
+  // One iteration (inner loop body).  want_res forces the residual pass.
+  StepResult advance(bool want_res);
+  // n iterations without outputs (benchmarks / tests).
+  void run_steps(long n, bool want_res_last = false);
+  // Full DEEPS2D_Run driver.  Returns the number of cycles run.
+  int run(const RunOptions& opt, std::ostream* log);
+
+  // Backend interface
+  virtual StepResult do_step(const StepParams& P, bool want_res) = 0;
+  virtual void download(Field& J) = 0;   // refresh host records (owned columns)
+  virtual void upload() = 0;             // host records -> backend
+  virtual void cycle_update() {}         // per-cycle y+ / sources (backend side)
+  virtual void sample_monitors(std::vector<MonitorPoint>& mp);
+  StepParams make_params(long it) const;
+
+ protected:
+  bool isSrcAdd = false;
+};
+
+class CpuSolver : public SolverBase {
+ public:
+  // Owns columns [gi0, gi1) of the global field; a halo column is added on
+  // each interior side.
+  CpuSolver(Case& cs, int gi0 = 0, int gi1 = -1);
+  StepResult do_step(const StepParams& P, bool want_res) override;
+  void download(Field& J) override;
+  void upload() override;
+  void cycle_update() override;
+
+  HostArrays h;
+  int gi0, gi1;     // owned global columns
+  int l_off;        // local index of global column gi0 (0 or 1)
+  int sbuf = 0, dsbuf = 0, pbuf = 0;
+  // halo access for distributed runs: pack/unpack columns of the exchanged fields
+  // groups: 0 = predicted state (N-S gradients), 1 = post-fill state,
+  // 2 = wall-heat per-direction fluxes
+  enum { HALO_MID = 0, HALO_STATE = 1, HALO_QDIR = 2 };
+  int halo_doubles(int group) const;
+  void pack_column(int group, int local_i, real* buf) const;
+  void unpack_column(int group, int local_i, const real* buf);
+  std::function<void(CpuSolver&, int)> halo_exchange;
+};
+
+class RefSolver : public SolverBase {
+ public:
+  explicit RefSolver(Case& cs);
+  StepResult do_step(const StepParams& P, bool want_res) override;
+  void download(Field&) override {}
+  void upload() override {}
+  std::vector<CellRecord> core;   // FlowNodeCore2D scratch (NextNode)
+};
+
+}  // namespace hf2d

@@ -1,0 +1,518 @@
+// Per-cell DEEPS step kernels over structure-of-arrays state, shared verbatim
+// by the CPU Jacobi stepper and the HIP kernels (hip/kernels.hip), so the two
+// agree to rounding.
+//
+// Jacobi semantics (the reference sweeps in place, Gauss-Seidel-like;
+// SURVEY H1): every phase reads only values produced by the previous phase.
+//   predict_cell   pass 1 + pass 2a of DEEPS2D_Run (deeps2d_core.cpp:853-1165):
+//                  blended LxF/central predictor, BC handling, residual,
+//                  blending-factor update, commit.  Reads S_in/A/B/F/dS*_in,
+//                  writes S_out/dS*_out/beta.
+//   fill_cell      pass 2b+2c (deeps2d_core.cpp:1169-1332): gradients from the
+//                  committed neighbours (primitives U,V,T lagged one step),
+//                  FillNode2D, negative-T check, local dt, chemistry.
+//   wall_heat_*    CalcHeatOnWallSources (deeps2d_core.cpp:2679-2833) in
+//                  owner-computes form (no scatter races).
+#pragma once
+
+#include "physics.hpp"
+#include "residual.hpp"
+
+namespace hf2d {
+
+// Neighbour-present bits packed per cell.
+enum : uint8_t { NB_XL = 1, NB_XR = 2, NB_YU = 4, NB_YD = 8 };
+
+// Raw SoA view.  Equation arrays are [k * N + idx], idx = i * ny + j
+// (x-major, matching the .hf2d file; a column is contiguous).
+struct SoA {
+  int nx = 0, ny = 0;
+  long N = 0;
+  // conserved state and fluxes (equation-major)
+  real* S = nullptr;
+  real* A = nullptr;
+  real* B = nullptr;
+  real* F = nullptr;
+  real* Src = nullptr;
+  real* SrcAdd = nullptr;
+  real* beta = nullptr;
+  real* dSdx = nullptr;
+  real* dSdy = nullptr;
+  // primitives / transport
+  real* U = nullptr;
+  real* V = nullptr;
+  real* Tg = nullptr;
+  real* p = nullptr;
+  real* kk = nullptr;   // Cp/Cv
+  real* R = nullptr;
+  real* CP = nullptr;
+  real* lam = nullptr;
+  real* mu = nullptr;
+  real* mu_t = nullptr;
+  real* lam_t = nullptr;
+  real* Diff = nullptr;
+  real* Y = nullptr;    // [NSPEC * N]
+  // turbulence / wall data
+  real* l_min = nullptr;
+  real* y_plus = nullptr;
+  real* Re_local = nullptr;
+  real* BGX = nullptr;
+  real* BGY = nullptr;
+  real* Tf = nullptr;
+  real* Q_conv = nullptr;
+  real* grad = nullptr; // [10 * N]: dUdx dUdy dVdx dVdy dTdx dTdy dkdx dkdy depsdx depsdy
+  u64* CT = nullptr;
+  u64* TT = nullptr;
+  uint8_t* nb = nullptr;
+  int32_t* iw = nullptr;
+  int32_t* jw = nullptr;
+};
+
+enum { G_DUDX = 0, G_DUDY, G_DVDX, G_DVDY, G_DTDX, G_DTDY, G_DKDX, G_DKDY, G_DEDX, G_DEDY, NGRAD };
+
+struct StepParams {
+  int nx, ny;        // local array extents (including halo columns)
+  int i0, i1;        // owned/computed column range [i0, i1)
+  int gx0;           // global column index of local column 0
+  real dx, dy, dt;
+  real dtdx, dtdy, dxx, dyy;  // dxx = dy/(dx+dy), dyy = dx/(dx+dy)
+  real beta_min;     // min(beta0, beta_Scenario(it))
+  real nrbc_beta0;
+  real CFL_min;      // min(CFL, CFL_Scenario(it))
+  int bff;
+  int alternate_rms;
+  int do_residual;
+  int sm;            // ProblemType
+  int chem_model;
+  FillParams fpa;    // for active cells (is_mu_t / is_init per TurbStartIter)
+  FillParams ffc;    // for NT_FC cells: FillNode2D(1, 0, ...)
+  const SpeciesProps* species;  // host or device pointer
+};
+
+// Register-resident cell used by fill_node / turb_model / chemistry.
+struct CellLocal {
+  real S[NEQ], A[NEQ], B[NEQ], F[NEQ], RX[NEQ], RY[NEQ], Src[NEQ], SrcAdd[NEQ];
+  real U, V, p, Tg, k, R, CP, lam, mu, Diff, mu_t, lam_t;
+  real l_min, y_plus, Re_local;
+  real dkdx, dkdy, depsdx, depsdy;
+  real dUdx, dUdy, dVdx, dVdy, dTdx, dTdy;
+  real droYdx[NSPEC], droYdy[NSPEC];
+  real Y[NSPEC];
+  real BGX, BGY, Uw, Vw, y, Tf;
+  u64 CT, TurbType;
+};
+
+// ---------------------------------------------------------------------------
+// Equation BC masks (deeps2d_core.cpp:903-991).  Returns false when the
+// equation is frozen (Dirichlet or not transported for this cell model).
+// ---------------------------------------------------------------------------
+struct EqFlags {
+  bool upd;   // not Dirichlet
+  bool dx, dy, dx2, dy2;   // dx/dy: flux difference used (no Neumann); dx2/dy2: Cauchy
+};
+
+HF_HD inline EqFlags eq_flags(int k, u64 CT, u64 TT, int sm) {
+  EqFlags f{false, true, true, false, false};
+  if (k < 4) {
+    f.upd = !has_all(CT, CT_Rho_CONST << k);
+    f.dx = !has_all(CT, CT_dRhodx_NULL << k);
+    f.dy = !has_all(CT, CT_dRhody_NULL << k);
+    f.dx2 = has_all(CT, CT_d2Rhodx2_NULL << k);
+    f.dy2 = has_all(CT, CT_d2Rhody2_NULL << k);
+  } else if (k < 4 + NCOMP) {
+    f.upd = !has_all(CT, CT_Y_CONST);
+    f.dx = !has_all(CT, CT_dYdx_NULL);
+    f.dy = !has_all(CT, CT_dYdy_NULL);
+    f.dx2 = has_all(CT, CT_d2Ydx2_NULL);
+    f.dy2 = has_all(CT, CT_d2Ydy2_NULL);
+  } else if (sm == SM_NS && has_turb_eq(TT)) {
+    // The reference shifts the eps masks by (k - 7) as well, so eps tests
+    // the *next* flag bit (quirk Q3, kept for parity).
+    const int sh = k - 4 - NCOMP;
+    f.upd = !has_all(TT, TCT_k_CONST << sh);
+    f.dx = !has_all(TT, TCT_dkdx_NULL << sh);
+    f.dy = !has_all(TT, TCT_dkdy_NULL << sh);
+    f.dx2 = has_all(TT, TCT_d2kdx2_NULL << sh);
+    f.dy2 = has_all(TT, TCT_d2kdy2_NULL << sh);
+  }
+  return f;
+}
+
+// Pass-2 "Dirichlet" test used to gate the residual/beta update: for the
+// turbulence equations the reference tests TCT bits against CT (quirk Q4).
+HF_HD inline bool pass2_frozen(int k, u64 CT, u64 TT, int sm) {
+  u64 c = 0;
+  if (k < 4)
+    c = CT_Rho_CONST << k;
+  else if (k < 4 + NCOMP)
+    c = CT_Y_CONST;
+  else if (sm == SM_NS && has_turb_eq(TT))
+    c = TCT_k_CONST << (k - 4 - NCOMP);
+  return has_all(CT, c);
+}
+
+HF_HD inline bool is_active(u64 CT) {
+  return has_all(CT, CT_NODE_IS_SET) && !has_all(CT, CT_SOLID) && !has_all(CT, NT_FC);
+}
+
+HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, real sqrt_res) {
+  const real b2 = beta_min * beta_min;
+  switch (bff) {
+    case BFF_L: return hf_min(beta_min, b2 / (beta_min + DD));
+    case BFF_LR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + DD));
+    case BFF_S: return hf_min(beta_min, b2 / (beta_min + DD * DD));
+    case BFF_SR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + DD * DD));
+    case BFF_SQR: return hf_min(beta_min, b2 / (beta_min + sqrt_res));
+    case BFF_SQRR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + sqrt_res));
+    default: return beta_old;   // declared but unimplemented variants (Q22)
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 1 + pass 2a for one cell.  `res` (may be null) accumulates residuals.
+// ---------------------------------------------------------------------------
+HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
+                               ResidualPack* res) {
+  const long N = in.N;
+  const long idx = (long)i * P.ny + j;
+  const u64 CT = in.CT[idx];
+  if (!is_active(CT)) {
+    for (int k = 0; k < NEQ; k++) {
+      out.S[k * N + idx] = in.S[k * N + idx];
+      out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
+      out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
+    }
+    return;
+  }
+  const u64 TT = in.TT[idx];
+  const uint8_t nbm = in.nb[idx];
+  const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+  const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+  const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j;
+  const long iU = idx + n3, iD = idx - n4;
+  const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
+  const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+  const int Num_Eq = num_eq_for(TT);
+  const bool axi = P.fpa.FT != 0;
+  for (int k = 0; k < NEQ; k++) {
+    const long o = k * N;
+    real s = in.S[o + idx];
+    const EqFlags f = eq_flags(k, CT, TT, P.sm);
+    if (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT)))) {
+      out.S[o + idx] = s;
+      out.dSdx[o + idx] = in.dSdx[o + idx];
+      out.dSdy[o + idx] = in.dSdy[o + idx];
+      continue;
+    }
+    real dXX, dYY, dsdx, dsdy;
+    if (f.dx) {
+      dXX = dsdx = (in.A[o + iR] - in.A[o + iL]) * n_n_1;
+    } else {
+      // a missing neighbour resolves to the cell itself
+      const real sL = n1 ? in.S[o + iL] : s, sR = n2 ? in.S[o + iR] : s;
+      s = (sL * n2 + sR * n1) * n_n_1;
+      dXX = dsdx = 0.;
+    }
+    if (f.dy) {
+      dYY = dsdy = (in.B[o + iU] - in.B[o + iD]) * m_m_1;
+    } else {
+      const real sU = n3 ? in.S[o + iU] : s, sD = n4 ? in.S[o + iD] : s;
+      s = (sU * n3 + sD * n4) * m_m_1;
+      dYY = dsdy = 0.;
+    }
+    if (f.dx2) dXX = (in.dSdx[o + iL] + in.dSdx[o + iR]) * 0.5;
+    if (f.dy2) dYY = (in.dSdy[o + iU] + in.dSdy[o + iD]) * 0.5;
+    const real SL = n1 ? in.S[o + iL] : s, SR = n2 ? in.S[o + iR] : s;
+    const real SU = n3 ? in.S[o + iU] : s, SD = n4 ? in.S[o + iD] : s;
+    const real beta = in.beta[o + idx];
+    const real _beta = 1. - beta;
+    real snew;
+    if (axi)
+      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 -
+             (P.dtdx * dXX + P.dtdy * (dYY + in.F[o + idx] / (j + 1))) + (in.Src[o + idx]) * P.dt +
+             in.SrcAdd[o + idx];
+    else
+      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 - (P.dtdx * dXX + P.dtdy * dYY) +
+             (in.Src[o + idx]) * P.dt + in.SrcAdd[o + idx];
+    out.dSdx[o + idx] = dsdx;
+    out.dSdy[o + idx] = dsdy;
+    // pass 2a: residual + blending factor
+    if (!pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
+      const real absDD = snew - s;
+      real DD, sqrt_res = 0;
+      if (std::fabs(s) > 1.e-15) {
+        DD = std::fabs(absDD / s);
+        sqrt_res = std::sqrt(DD);
+      } else {
+        DD = 1.0;
+      }
+      const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+      out.beta[o + idx] = blend_beta(P.bff, bmin, beta, DD, sqrt_res);
+      if (res) {
+        EqResidual& e = res->eq[k];
+        if (DD >= e.dd_max) {
+          e.dd_max = DD;
+          e.i = P.gx0 + i;
+          e.j = j;
+        }
+        if (P.alternate_rms) {
+          e.rms += absDD * absDD;
+          e.sum_div += s * s;
+        } else {
+          e.rms += DD * DD;
+          e.count += 1;
+        }
+      }
+    }
+    out.S[o + idx] = snew;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Gradients + FillNode2D + dt + chemistry for one cell.
+// `sin` holds the committed state (S after predict), prim_old the previous
+// step's U/V/Tg.  Results go to `out` (S, A, B, F, primitives).
+// Returns the local dt (1.0 when the cell does not limit dt); sets *neg_T.
+// ---------------------------------------------------------------------------
+HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
+                            int* neg_T, bool store_grad) {
+  const long N = sin.N;
+  const long idx = (long)i * P.ny + j;
+  const u64 CT = sin.CT[idx];
+  CellLocal c;
+  for (int k = 0; k < NEQ; k++) c.S[k] = sin.S[k * N + idx];
+  if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
+    for (int k = 0; k < NEQ; k++) out.S[k * N + idx] = c.S[k];
+    return 1.0;
+  }
+  const bool active = !has_all(CT, NT_FC);
+  c.CT = CT;
+  c.TurbType = sin.TT[idx];
+  for (int k = 0; k < NEQ; k++) {
+    c.A[k] = out.A[k * N + idx];
+    c.B[k] = out.B[k * N + idx];
+    c.F[k] = out.F[k * N + idx];
+    c.Src[k] = out.Src[k * N + idx];
+    c.SrcAdd[k] = out.SrcAdd[k * N + idx];
+    c.RX[k] = c.RY[k] = 0;
+  }
+  c.U = prim_old.U[idx];
+  c.V = prim_old.V[idx];
+  c.Tg = prim_old.Tg[idx];
+  c.p = out.p[idx];
+  c.k = out.kk[idx];
+  c.R = out.R[idx];
+  c.CP = out.CP[idx];
+  c.lam = out.lam[idx];
+  c.mu = out.mu[idx];
+  c.Diff = out.Diff[idx];
+  c.mu_t = out.mu_t[idx];
+  c.lam_t = out.lam_t[idx];
+  c.l_min = sin.l_min[idx];
+  c.y_plus = sin.y_plus[idx];
+  c.Re_local = out.Re_local[idx];
+  c.BGX = sin.BGX[idx];
+  c.BGY = sin.BGY[idx];
+  c.Tf = sin.Tf[idx];
+  c.Uw = c.Vw = 0;
+  c.y = (j + 0.5) * P.dy;
+  for (int s = 0; s < NSPEC; s++) {
+    c.Y[s] = out.Y[s * N + idx];
+    c.droYdx[s] = c.droYdy[s] = 0;
+  }
+  c.dUdx = out.grad[G_DUDX * N + idx];
+  c.dUdy = out.grad[G_DUDY * N + idx];
+  c.dVdx = out.grad[G_DVDX * N + idx];
+  c.dVdy = out.grad[G_DVDY * N + idx];
+  c.dTdx = out.grad[G_DTDX * N + idx];
+  c.dTdy = out.grad[G_DTDY * N + idx];
+  c.dkdx = out.grad[G_DKDX * N + idx];
+  c.dkdy = out.grad[G_DKDY * N + idx];
+  c.depsdx = out.grad[G_DEDX * N + idx];
+  c.depsdy = out.grad[G_DEDY * N + idx];
+
+  if (active && P.sm == SM_NS) {
+    const uint8_t nbm = sin.nb[idx];
+    const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+    const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+    const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j;
+    const long iU = idx + n3, iD = idx - n4;
+    const real dx_1_n = (1.0 / P.dx) / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
+    const real dy_1_m = (1.0 / P.dy) / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+    real aR = sin.S[iR], aL = sin.S[iL], aU = sin.S[iU], aD = sin.S[iD];
+    c.droYdx[NCOMP] = c.droYdy[NCOMP] = 0.;
+    const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
+    for (int k = 4; k < 4 + NCOMP; k++) {
+      const long o = k * N;
+      if (!nx0) {
+        c.droYdx[k - 4] = (sin.S[o + iR] - sin.S[o + iL]) * dx_1_n;
+        aR -= sin.S[o + iR];
+        aL -= sin.S[o + iL];
+      }
+      if (!ny0) {
+        c.droYdy[k - 4] = (sin.S[o + iU] - sin.S[o + iD]) * dy_1_m;
+        aU -= sin.S[o + iU];
+        aD -= sin.S[o + iD];
+      }
+    }
+    if (!nx0) c.droYdx[NCOMP] = (aR - aL) * dx_1_n;
+    if (!ny0) c.droYdy[NCOMP] = (aU - aD) * dy_1_m;
+    const real* Uo = prim_old.U;
+    const real* Vo = prim_old.V;
+    const real rho = c.S[I_RHO];
+    const long oK = (long)I_K * N, oE = (long)I_EPS * N;
+    if (has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW)) {
+      c.dUdx = (Uo[iR] * n1 - Uo[iL] * n2) * dx_1_n;
+      c.dVdx = (Vo[iR] * n1 - Vo[iL] * n2) * dx_1_n;
+      c.dUdy = (Uo[iU] * n3 - Uo[iD] * n4) * dy_1_m;
+      c.dVdy = (Vo[iU] * n3 - Vo[iD] * n4) * dy_1_m;
+      if (is_two_eq(c.TurbType)) {
+        c.dkdx = (sin.S[oK + iR] * n1 - sin.S[oK + iL] * n2) * dx_1_n / rho;
+        c.depsdx = (sin.S[oE + iR] * n1 - sin.S[oE + iL] * n2) * dx_1_n / rho;
+        c.dkdy = (sin.S[oK + iU] * n3 - sin.S[oK + iD] * n4) * dy_1_m / rho;
+        c.depsdy = (sin.S[oE + iU] * n3 - sin.S[oE + iD] * n4) * dy_1_m / rho;
+      } else if (has_all(c.TurbType, TCT_Spalart_Allmaras_Model)) {
+        c.dkdx = (sin.S[oK + iR] * n1 - sin.S[oK + iL] * n2) * dx_1_n / rho;
+        c.dkdy = (sin.S[oK + iU] * n3 - sin.S[oK + iD] * n4) * dy_1_m / rho;
+      }
+    } else {
+      c.dUdx = (Uo[iR] - Uo[iL]) * dx_1_n;
+      c.dVdx = (Vo[iR] - Vo[iL]) * dx_1_n;
+      c.dUdy = (Uo[iU] - Uo[iD]) * dy_1_m;
+      c.dVdy = (Vo[iU] - Vo[iD]) * dy_1_m;
+      if (is_two_eq(c.TurbType)) {
+        c.dkdx = (sin.S[oK + iR] - sin.S[oK + iL]) * dx_1_n / rho;
+        c.depsdx = (sin.S[oE + iR] - sin.S[oE + iL]) * dx_1_n / rho;
+        c.dkdy = (sin.S[oK + iU] - sin.S[oK + iD]) * dy_1_m / rho;
+        c.depsdy = (sin.S[oE + iU] - sin.S[oE + iD]) * dy_1_m / rho;
+      } else if (has_all(c.TurbType, TCT_Spalart_Allmaras_Model)) {
+        c.dkdx = (sin.S[oK + iR] - sin.S[oK + iL]) * dx_1_n / rho;
+        c.dkdy = (sin.S[oK + iU] - sin.S[oK + iD]) * dy_1_m / rho;
+      }
+    }
+    c.dTdx = (prim_old.Tg[iR] - prim_old.Tg[iL]) * dx_1_n;
+    c.dTdy = (prim_old.Tg[iU] - prim_old.Tg[iD]) * dy_1_m;
+  }
+
+  fill_node(c, active ? P.fpa : P.ffc);
+
+  real dt_local = 1.0;
+  if (active) {
+    if (c.Tg < 0.) {
+      if (neg_T) *neg_T = 1;
+    } else {
+      const real AAA = std::sqrt(c.k * c.R * c.Tg);
+      dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(c.U)), P.dy / (AAA + std::fabs(c.V)));
+      if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
+    }
+  }
+  for (int k = 0; k < NEQ; k++) {
+    out.S[k * N + idx] = c.S[k];
+    out.A[k * N + idx] = c.A[k];
+    out.B[k * N + idx] = c.B[k];
+    out.F[k * N + idx] = c.F[k];
+    out.Src[k * N + idx] = c.Src[k];
+    out.SrcAdd[k * N + idx] = c.SrcAdd[k];
+  }
+  out.U[idx] = c.U;
+  out.V[idx] = c.V;
+  out.Tg[idx] = c.Tg;
+  out.p[idx] = c.p;
+  out.kk[idx] = c.k;
+  out.R[idx] = c.R;
+  out.CP[idx] = c.CP;
+  out.lam[idx] = c.lam;
+  out.mu[idx] = c.mu;
+  out.Diff[idx] = c.Diff;
+  out.mu_t[idx] = c.mu_t;
+  out.lam_t[idx] = c.lam_t;
+  out.Re_local[idx] = c.Re_local;
+  for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
+  if (store_grad && active && P.sm == SM_NS) {
+    out.grad[G_DUDX * N + idx] = c.dUdx;
+    out.grad[G_DUDY * N + idx] = c.dUdy;
+    out.grad[G_DVDX * N + idx] = c.dVdx;
+    out.grad[G_DVDY * N + idx] = c.dVdy;
+    out.grad[G_DTDX * N + idx] = c.dTdx;
+    out.grad[G_DTDY * N + idx] = c.dTdy;
+    out.grad[G_DKDX * N + idx] = c.dkdx;
+    out.grad[G_DKDY * N + idx] = c.dkdy;
+    out.grad[G_DEDX * N + idx] = c.depsdx;
+    out.grad[G_DEDY * N + idx] = c.depsdy;
+  }
+  return dt_local;
+}
+
+}  // namespace hf2d
+
+namespace hf2d {
+
+// ---------------------------------------------------------------------------
+// Wall heat sources, owner-computes form of CalcHeatOnWallSources
+// (deeps2d_core.cpp:2679-2833).  The reference visits wall cells column by
+// column (i outer, j inner) and, per wall cell, its solid neighbours in the
+// order Down, Up, Left, Right, updating the solid's Q_conv in place.  A solid
+// cell therefore sees its wall neighbours in the order (i-1,j), (i,j-1),
+// (i,j+1), (i+1,j); we replay that sequence per solid cell and record the
+// Q value after each update in qdir[d] so that the wall cell can pick it up.
+// qdir slots: 0 = updated by the left wall cell, 1 = by the lower, 2 = by the
+// upper, 3 = by the right wall cell.
+// ---------------------------------------------------------------------------
+HF_HD inline bool is_wall_gas(u64 ct) {
+  return !has_all(ct, CT_SOLID) && (has_all(ct, CT_WALL_LAW) || has_all(ct, CT_WALL_NO_SLIP));
+}
+
+HF_HD inline void wall_heat_solid_cell(const StepParams& P, const SoA& s, real* qdir, int i, int j) {
+  const long N = s.N;
+  const long idx = (long)i * P.ny + j;
+  for (int d = 0; d < 4; d++) qdir[d * N + idx] = 0.;
+  if (!has_all(s.CT[idx], CT_SOLID)) return;
+  real Q = 0.;
+  const real Ts = s.Tg[idx];
+  const int di[4] = {-1, 0, 0, 1};
+  const int dj[4] = {0, -1, 1, 0};
+  for (int d = 0; d < 4; d++) {
+    const int wi = i + di[d], wj = j + dj[d];
+    if (wi < 0 || wj < 0 || wi >= P.nx || wj >= P.ny) continue;
+    const long w = (long)wi * P.ny + wj;
+    if (!is_wall_gas(s.CT[w])) continue;
+    const real h = (d == 0 || d == 3) ? P.dx : P.dy;
+    const real lam_eff = s.lam[w] + s.lam_t[w];
+    if (Q > 0.)
+      Q = (Q - lam_eff * (Ts - s.Tg[w]) / h) * 0.5;
+    else
+      Q = -lam_eff * (Ts - s.Tg[w]) / h;
+    qdir[d * N + idx] = Q;
+  }
+  s.Q_conv[idx] = Q;
+}
+
+HF_HD inline void wall_heat_wall_cell(const StepParams& P, const SoA& s, const real* qdir, int i, int j) {
+  const long N = s.N;
+  const long idx = (long)i * P.ny + j;
+  if (!is_wall_gas(s.CT[idx])) return;
+  real* srcE = s.SrcAdd + (long)I_RHOE * N;
+  // Down, Up, Left, Right: later assignments overwrite earlier ones.
+  if (j > 0 && has_all(s.CT[idx - 1], CT_SOLID)) srcE[idx] = -P.dt * qdir[2 * N + idx - 1] / P.dy;
+  if (j < P.ny - 1 && has_all(s.CT[idx + 1], CT_SOLID)) srcE[idx] = -P.dt * qdir[1 * N + idx + 1] / P.dy;
+  if (i > 0 && has_all(s.CT[idx - P.ny], CT_SOLID)) srcE[idx] = -P.dt * qdir[3 * N + idx - P.ny] / P.dx;
+  if (i < P.nx - 1 && has_all(s.CT[idx + P.ny], CT_SOLID)) srcE[idx] = -P.dt * qdir[0 * N + idx + P.ny] / P.dx;
+}
+
+// y+ from the friction velocity of the nearest wall node (the MPI build's
+// per-cycle ParallelRecalc_y_plus, deeps2d_core.cpp:2291-2322, in O(N) form).
+HF_HD inline void y_plus_cell(const StepParams& P, const SoA& s, int i, int j, int gx0) {
+  const long idx = (long)i * P.ny + j;
+  const u64 ct = s.CT[idx];
+  if (!has_all(ct, CT_NODE_IS_SET) || has_all(ct, CT_SOLID)) return;
+  const int iw = s.iw[idx] - gx0, jw = s.jw[idx];
+  if (iw < 0 || iw >= P.nx || jw < 0 || jw >= P.ny) return;
+  const long w = (long)iw * P.ny + jw;
+  if (!is_wall_gas(s.CT[w])) return;
+  const long N = s.N;
+  const real tau_w = (std::fabs(s.grad[G_DUDY * N + w]) + std::fabs(s.grad[G_DVDX * N + w])) * s.mu[w];
+  const real U_w = std::sqrt(tau_w / s.S[w] + 1e-30);
+  s.y_plus[idx] = std::fabs(U_w * s.l_min[idx] * s.S[idx] / s.mu[idx]);
+}
+
+}  // namespace hf2d
