@@ -1,0 +1,128 @@
+"""In-tree native build of the hf2d runtime (no JIT cache, no pip install).
+
+Produces, next to this file:
+  _hf2d.<ext-suffix>.so   pybind11 module: host core + gfx950 HIP kernels + RCCL
+  bin/hf2d                C++ CLI (argv-compatible with OpenHyperFLOW2D-<ver> <deck>)
+  bin/hf2d_cpu            host-only CLI (g++; CPU / reference-order steppers)
+
+Uses ninja for incremental builds; every HIP source is compiled with
+``hipcc --offload-arch=gfx950``.  Device code is built with
+``-ffp-contract=off`` so the GPU matches the CPU Jacobi stepper to rounding.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "..", "build", "native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("HF2D_OFFLOAD_ARCH", "gfx950")
+
+CORE_SRCS = ["deck.cpp", "gasdyn.cpp", "config.cpp", "preprocess.cpp", "checkpoint.cpp", "postproc.cpp", "solver.cpp"]
+HIP_SRCS = ["device_solver.hip"]
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(HERE, "_hf2d" + suffix)
+
+
+def _pybind_include() -> str:
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def _ninja_file() -> str:
+    py_inc = sysconfig.get_paths()["include"]
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    common = "-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable"
+    lines = [
+        "ninja_required_version = 1.5",
+        f"hipcc = {hipcc}",
+        f"cxxflags = {common} -x c++ -I{CSRC}",
+        f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC}",
+        f"pyflags = -I{_pybind_include()} -I{py_inc}",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl",
+        "rule cxx",
+        "  command = $hipcc $cxxflags $extra -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "rule hip",
+        "  command = $hipcc $hipflags -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "rule gxx",
+        "  command = g++ -O2 -std=c++17 -fPIC -I" + CSRC + " -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "rule link_so",
+        "  command = $hipcc -shared --offload-arch=" + ARCH + " $in -o $out $ldflags",
+        "rule link_exe",
+        "  command = $hipcc --offload-arch=" + ARCH + " $in -o $out $ldflags",
+        "rule link_gxx",
+        "  command = g++ $in -o $out",
+    ]
+    objs = []
+    for s in CORE_SRCS:
+        o = f"core_{s[:-4]}.o"
+        lines.append(f"build {o}: cxx {os.path.join(CSRC, 'core', s)}")
+        objs.append(o)
+    hobjs = []
+    for s in HIP_SRCS:
+        o = f"hip_{s[:-4]}.o"
+        lines.append(f"build {o}: hip {os.path.join(CSRC, 'hip', s)}")
+        hobjs.append(o)
+    lines.append(f"build bind_module.o: cxx {os.path.join(CSRC, 'bind', 'module.cpp')}")
+    lines.append("  extra = $pyflags")
+    lines.append(f"build main.o: cxx {os.path.join(CSRC, 'core', 'hf2d_main.cpp')}")
+    gobjs = []
+    for s in CORE_SRCS + ["hf2d_main.cpp"]:
+        o = f"gxx_{s[:-4]}.o"
+        lines.append(f"build {o}: gxx {os.path.join(CSRC, 'core', s)}")
+        gobjs.append(o)
+    lines.append(f"build {ext_path()}: link_so {' '.join(objs + hobjs)} bind_module.o")
+    lines.append(f"build {os.path.join(HERE, 'bin', 'hf2d')}: link_exe {' '.join(objs + hobjs)} main.o")
+    lines.append(f"build {os.path.join(HERE, 'bin', 'hf2d_cpu')}: link_gxx {' '.join(gobjs)}")
+    return "\n".join(lines) + "\n"
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
+    nf = os.path.join(BUILD, "build.ninja")
+    txt = _ninja_file()
+    old = open(nf).read() if os.path.exists(nf) else ""
+    if old != txt:
+        with open(nf, "w") as f:
+            f.write(txt)
+    ninja = shutil.which("ninja")
+    if ninja is None:
+        try:
+            import ninja as _n  # type: ignore
+
+            ninja = os.path.join(_n.BIN_DIR, "ninja")
+        except Exception as e:  # pragma: no cover
+            raise RuntimeError("ninja not found") from e
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    cmd = [ninja, "-C", BUILD, f"-j{jobs}"]
+    if verbose:
+        cmd.append("-v")
+    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        sys.stderr.write((r.stdout or "") + (r.stderr or ""))
+        raise RuntimeError("native build failed")
+    return ext_path()
+
+
+def is_built() -> bool:
+    return os.path.exists(ext_path())
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

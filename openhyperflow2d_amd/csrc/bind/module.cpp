@@ -1,0 +1,268 @@
+// Python bindings (pybind11) for the native hf2d runtime.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <sstream>
+
+#include "../core/case.hpp"
+#include "../core/checkpoint.hpp"
+#include "../core/postproc.hpp"
+#include "../core/solver.hpp"
+#include "../hip/device_solver.hpp"
+
+namespace py = pybind11;
+using namespace hf2d;
+
+namespace {
+
+// Comm whose reductions are delegated to Python callables (gloo tests).
+struct PyComm : Comm {
+  int r = 0, n = 1;
+  std::function<double(double)> f_min, f_sum;
+  std::function<int(int)> f_maxi;
+  std::function<py::bytes(py::bytes)> f_res;   // allgather-of-packs, returns concatenated bytes
+  int rank() const override { return r; }
+  int size() const override { return n; }
+  real allreduce_min(real v) override { return f_min ? f_min(v) : v; }
+  real allreduce_sum(real v) override { return f_sum ? f_sum(v) : v; }
+  int allreduce_max_int(int v) override { return f_maxi ? f_maxi(v) : v; }
+  void allreduce_residual(ResidualPack& p) override {
+    if (!f_res) return;
+    py::gil_scoped_acquire g;
+    py::bytes all = f_res(py::bytes((const char*)&p, sizeof(ResidualPack)));
+    std::string s = all;
+    const size_t m = s.size() / sizeof(ResidualPack);
+    ResidualPack a;
+    std::memcpy(&a, s.data(), sizeof(ResidualPack));
+    for (size_t q = 1; q < m; q++) {
+      ResidualPack b;
+      std::memcpy(&b, s.data() + q * sizeof(ResidualPack), sizeof(ResidualPack));
+      residual_merge_lex(a, b);
+    }
+    p = a;
+  }
+};
+
+py::array_t<double> field_scalar(const Field& J, const std::string& name) {
+  py::array_t<double> a({J.nx, J.ny});
+  auto m = a.mutable_unchecked<2>();
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& c = J.at(i, j);
+      double v = 0;
+      if (name.size() == 2 && name[0] == 'S') v = c.S[name[1] - '0'];
+      else if (name == "rho") v = c.S[0];
+      else if (name == "U") v = c.U;
+      else if (name == "V") v = c.V;
+      else if (name == "p") v = c.p;
+      else if (name == "T") v = c.Tg;
+      else if (name == "mu_t") v = c.mu_t;
+      else if (name == "k") v = c.k;
+      else if (name == "R") v = c.R;
+      else if (name == "CP") v = c.CP;
+      else if (name == "l_min") v = c.l_min;
+      else if (name == "y_plus") v = c.y_plus;
+      else if (name == "mach") {
+        const double A = std::sqrt(c.k * c.R * c.Tg + 1e-30);
+        v = std::sqrt(c.U * c.U + c.V * c.V + 1e-30) / A;
+      } else if (name == "solid") v = c.is(CT_SOLID) ? 1.0 : 0.0;
+      else if (name == "CT") v = (double)c.CT;
+      else throw std::runtime_error("unknown field " + name);
+      m(i, j) = v;
+    }
+  return a;
+}
+
+py::dict summary_dict(const SolverBase& s) {
+  py::dict d;
+  d["iteration"] = s.last_iter + s.iter;
+  d["dt"] = s.dt;
+  d["time"] = s.cs.global_time + s.cur_time_part;
+  py::list rms;
+  for (int k = 0; k < NEQ; k++) rms.append(s.last_res.rms[k]);
+  d["rms"] = rms;
+  d["max_rms"] = s.last_res.max_rms;
+  d["k_max"] = s.last_res.k_max;
+  return d;
+}
+
+template <class T>
+void bind_solver_common(py::class_<T, SolverBase>& c) {}
+
+}  // namespace
+
+PYBIND11_MODULE(_hf2d, m) {
+  m.doc() = "hf2d native runtime: OpenHyperFLOW2D-compatible DEEPS solver for AMD MI355X";
+  m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
+  m.attr("NEQ") = NEQ;
+  m.def("gpu_available", &gpu_available);
+
+  py::register_exception<DeckError>(m, "DeckError");
+
+  py::class_<InputDeck>(m, "InputDeck")
+      .def_static("from_file", &InputDeck::from_file)
+      .def_static("from_string", &InputDeck::from_string, py::arg("text"), py::arg("origin") = "<string>")
+      .def("name", &InputDeck::name)
+      .def("has", &InputDeck::has)
+      .def("get_int", &InputDeck::get_int)
+      .def("get_float", &InputDeck::get_float)
+      .def("get_string", &InputDeck::get_string)
+      .def("get_table", [](InputDeck& d, const std::string& k) {
+        const Table& t = d.get_table(k);
+        return py::make_tuple(t.x, t.y);
+      })
+      .def("table_eval", [](InputDeck& d, const std::string& k, double x) { return d.get_table(k).eval(x); })
+      .def("set", &InputDeck::set)
+      .def("keys", &InputDeck::keys)
+      .def("table_names", &InputDeck::table_names)
+      .def("to_text", &InputDeck::to_text);
+
+  py::class_<GasFlow>(m, "GasFlow")
+      .def(py::init<real, real, real, real, real, real>(), py::arg("Cp"), py::arg("T0"), py::arg("P0"), py::arg("R"),
+           py::arg("lam") = 0.01, py::arg("mu") = 5e-5)
+      .def_static("make2d", &GasFlow::make2d)
+      .def("kg", &GasFlow::kg)
+      .def("Tg", py::overload_cast<>(&GasFlow::Tg, py::const_))
+      .def("Pg", &GasFlow::Pg)
+      .def("ROG", &GasFlow::ROG)
+      .def("T0", &GasFlow::T0)
+      .def("P0", &GasFlow::P0)
+      .def("LAM", &GasFlow::LAM)
+      .def("TAU", &GasFlow::TAU)
+      .def("PF", &GasFlow::PF)
+      .def("EPS", &GasFlow::EPS)
+      .def("QF", &GasFlow::QF)
+      .def("Asound", &GasFlow::Asound)
+      .def("Akr", &GasFlow::Akr)
+      .def("mach", py::overload_cast<>(&GasFlow::flow_MACH, py::const_))
+      .def("set_mach", py::overload_cast<real>(&GasFlow::flow_MACH))
+      .def("wg", py::overload_cast<>(&GasFlow::flow_Wg, py::const_))
+      .def("set_wg", py::overload_cast<real>(&GasFlow::flow_Wg))
+      .def("set_lam", &GasFlow::flow_LAM)
+      .def("correct_flow", &GasFlow::CorrectFlow)
+      .def("U", &GasFlow::U)
+      .def("V", &GasFlow::V)
+      .def("Wg2d", &GasFlow::Wg2d)
+      .def("mach2d", &GasFlow::MACH2d)
+      .def("set_uv", &GasFlow::set_UV);
+
+  py::class_<Case, std::shared_ptr<Case>>(m, "Case")
+      .def_static(
+          "from_deck",
+          [](const std::string& text, const std::string& workdir, bool use_checkpoint, bool verbose) {
+            InputDeck d = InputDeck::from_string(text);
+            std::ostringstream* os = nullptr;
+            auto cs = std::make_shared<Case>(Case::from_deck(d, workdir, use_checkpoint, nullptr));
+            (void)os;
+            (void)verbose;
+            return cs;
+          },
+          py::arg("text"), py::arg("workdir") = ".", py::arg("use_checkpoint") = false, py::arg("verbose") = false)
+      .def_property_readonly("nx", [](const Case& c) { return c.J.nx; })
+      .def_property_readonly("ny", [](const Case& c) { return c.J.ny; })
+      .def_property_readonly("dt0", [](const Case& c) { return c.dt0; })
+      .def_property_readonly("dx", [](const Case& c) { return c.cfg.dx; })
+      .def_property_readonly("dy", [](const Case& c) { return c.cfg.dy; })
+      .def_property_readonly("problem_type", [](const Case& c) { return c.cfg.ProblemType; })
+      .def_property_readonly("flow_type", [](const Case& c) { return c.cfg.FT; })
+      .def_property_readonly("nmax", [](const Case& c) { return c.cfg.Nmax; })
+      .def_property_readonly("project", [](const Case& c) { return c.cfg.project; })
+      .def_property_readonly("global_time", [](const Case& c) { return c.global_time; })
+      .def_property_readonly("wall_nodes", [](const Case& c) { return c.wall_nodes; })
+      .def("set_semantics", [](Case& c, const std::string& s) {
+        c.cfg.semantics = (s == "serial") ? Semantics::SERIAL : Semantics::MPI;
+      })
+      .def("set_chem_model", [](Case& c, int m) { c.cfg.chem_model = m; })
+      .def("partition", &Case::partition_columns)
+      .def("field", [](const Case& c, const std::string& n) { return field_scalar(c.J, n); })
+      .def("records", [](const Case& c) {
+        return py::bytes((const char*)c.J.c.data(), c.J.c.size() * sizeof(CellRecord));
+      })
+      .def("set_records", [](Case& c, py::bytes b) {
+        std::string s = b;
+        if (s.size() != c.J.c.size() * sizeof(CellRecord)) throw std::runtime_error("record size mismatch");
+        std::memcpy((void*)c.J.c.data(), s.data(), s.size());
+      })
+      .def("write_checkpoint", [](const Case& c, const std::string& p) { write_hf2d(p, c.J); })
+      .def("read_checkpoint", [](Case& c, const std::string& p) { return read_hf2d(p, c.J); })
+      .def("save_plt", [](const Case& c, const std::string& p, bool rewrite) {
+        save_field_plt(p, c, c.J, c.global_time, rewrite);
+      })
+      .def("mass_flow_x", [](const Case& c, double x0, double y0, double dy) {
+        return mass_flow_rate_x(c, c.J, x0, y0, dy);
+      });
+
+  py::class_<SolverBase>(m, "SolverBase")
+      .def("run_steps", &SolverBase::run_steps, py::arg("n"), py::arg("want_residual_last") = false,
+           py::call_guard<py::gil_scoped_release>())
+      .def("advance", [](SolverBase& s, bool want) { s.advance(want); }, py::arg("want_residual") = false)
+      .def("run",
+           [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose) {
+             RunOptions o;
+             o.max_cycles = max_cycles;
+             o.outdir = outdir;
+             o.write_outputs = outputs;
+             o.write_checkpoint = checkpoint;
+             std::ostringstream log;
+             int n = s.run(o, verbose ? &log : nullptr);
+             return py::make_tuple(n, log.str());
+           },
+           py::arg("max_cycles") = 1, py::arg("outdir") = ".", py::arg("outputs") = true,
+           py::arg("checkpoint") = true, py::arg("verbose") = true)
+      .def("download", [](SolverBase& s) { s.download(s.cs.J); })
+      .def("upload", &SolverBase::upload)
+      .def("sync", &SolverBase::sync_scalars)
+      .def("summary", &summary_dict)
+      .def_readwrite("dt", &SolverBase::dt)
+      .def_readonly("iter", &SolverBase::iter)
+      .def_readonly("last_iter", &SolverBase::last_iter);
+
+  py::class_<CpuSolver, SolverBase>(m, "CpuSolver")
+      .def(py::init<Case&, int, int>(), py::arg("case"), py::arg("gi0") = 0, py::arg("gi1") = -1,
+           py::keep_alive<1, 2>())
+      .def_readonly("gi0", &CpuSolver::gi0)
+      .def_readonly("gi1", &CpuSolver::gi1)
+      .def_readonly("l_off", &CpuSolver::l_off)
+      .def_property_readonly("local_nx", [](const CpuSolver& s) { return s.h.nx; })
+      .def("halo_doubles", &CpuSolver::halo_doubles)
+      .def("pack_column",
+           [](const CpuSolver& s, int g, int li) {
+             py::array_t<double> a(s.halo_doubles(g) * s.h.ny);
+             s.pack_column(g, li, a.mutable_data());
+             return a;
+           })
+      .def("unpack_column",
+           [](CpuSolver& s, int g, int li, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+             if (a.size() != s.halo_doubles(g) * s.h.ny) throw std::runtime_error("halo size mismatch");
+             s.unpack_column(g, li, a.data());
+           })
+      .def("set_exchange", [](CpuSolver& s, std::function<void(CpuSolver&, int)> f) { s.halo_exchange = f; })
+      .def("set_comm",
+           [](CpuSolver& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
+              std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres) {
+             auto* c = new PyComm();
+             c->r = rank;
+             c->n = size;
+             c->f_min = fmin;
+             c->f_sum = fsum;
+             c->f_maxi = fmaxi;
+             c->f_res = fres;
+             s.comm = c;   // leaked intentionally: lives as long as the solver
+           });
+
+  py::class_<RefSolver, SolverBase>(m, "RefSolver").def(py::init<Case&>(), py::keep_alive<1, 2>());
+
+  py::class_<DeviceSolver, SolverBase>(m, "DeviceSolver")
+      .def(py::init<Case&, int, int, int>(), py::arg("case"), py::arg("device") = 0, py::arg("gi0") = 0,
+           py::arg("gi1") = -1, py::keep_alive<1, 2>())
+      .def_static("nccl_unique_id", []() { return py::bytes(DeviceSolver::nccl_unique_id()); })
+      .def("init_comm", [](DeviceSolver& s, py::bytes uid, int r, int n) { s.init_comm(std::string(uid), r, n); })
+      .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_readwrite("fused", &DeviceSolver::fused)
+      .def_readonly("gi0", &DeviceSolver::gi0)
+      .def_readonly("gi1", &DeviceSolver::gi1)
+      .def_property_readonly("stream", [](const DeviceSolver& s) { return (uintptr_t)s.stream(); });
+}

@@ -50,6 +50,26 @@ HF_HD inline void residual_merge(ResidualPack& a, const ResidualPack& b) {
   }
 }
 
+// Deterministic, associative merge used by tree reductions: the argmax keeps
+// the larger residual and, on ties, the cell that comes later in the
+// reference's sweep order (x outer, y inner), matching its "last equal wins".
+HF_HD inline void residual_merge_lex(ResidualPack& a, const ResidualPack& b) {
+  a.dt_min = a.dt_min < b.dt_min ? a.dt_min : b.dt_min;
+  for (int k = 0; k < NEQ; k++) {
+    const EqResidual& e = b.eq[k];
+    EqResidual& f = a.eq[k];
+    const bool later = (e.i > f.i) || (e.i == f.i && e.j > f.j);
+    if (e.dd_max > f.dd_max || (e.dd_max == f.dd_max && later)) {
+      f.dd_max = e.dd_max;
+      f.i = e.i;
+      f.j = e.j;
+    }
+    f.rms += e.rms;
+    f.sum_div += e.sum_div;
+    f.count += e.count;
+  }
+}
+
 // Final RMS per equation (MPI definition, deeps2d_core.cpp:1506-1518) and the
 // maximum used by the exit monitor.
 struct ResidualSummary {

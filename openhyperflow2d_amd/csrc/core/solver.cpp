@@ -243,6 +243,17 @@ StepResult SolverBase::advance(bool want_res) {
   const long it = last_iter + iter;
   StepParams P = make_params(it);
   StepResult r = do_step(P, want_res);
+  if (r.async) {
+    if (r.have_residual) {
+      comm->allreduce_residual(r.res);
+      last_res = residual_finalize(r.res, cs.cfg.isAlternateRMS, cs.cfg.MonitorIndex,
+                                   cs.cfg.semantics == Semantics::SERIAL, cs.cfg.ExitMonitorValue);
+      last_res_valid = true;
+    }
+    iter++;
+    if (want_res) sync_scalars();
+    return r;
+  }
   if (comm->allreduce_max_int(r.neg_T)) {
     char b[256];
     std::snprintf(b, sizeof b, "ERROR: Computational unstability (Tg < 0) on iteration %ld, dt=%g", it, P.dt);
@@ -269,15 +280,18 @@ StepResult SolverBase::advance(bool want_res) {
 void SolverBase::run_steps(long n, bool want_res_last) {
   for (long s = 0; s < n; s++) {
     if (iter >= cs.cfg.Nmax) {   // roll the inner counter like an outer cycle
+      sync_scalars();
       last_iter += iter;
       iter = 0;
       cs.global_time += cur_time_part;
       cur_time_part = 0;
+      on_cycle_roll();
       isSrcAdd = true;
       cycle++;
     }
     advance(want_res_last && s == n - 1);
   }
+  sync_scalars();
 }
 
 void SolverBase::sample_monitors(std::vector<MonitorPoint>& mp) {
@@ -340,6 +354,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
         }
       }
     }
+    sync_scalars();
     cycle_update();
     if (cs.cfg.sources.size() && comm->size() == 1) {
       // sources are re-applied every cycle in the MPI build (deeps2d_core.cpp:1716-1722)
@@ -370,6 +385,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
     iter = 0;
     cs.global_time += cur_time_part;
     cur_time_part = 0.;
+    on_cycle_roll();
     cycle++;
     cycles++;
     if (root) {

@@ -26,6 +26,7 @@ struct StepResult {
   real dt_min = 1.0;        // min local dt of this step (before cross-rank reduction)
   int neg_T = 0;
   bool have_residual = false;
+  bool async = false;       // device backend: dt / time / neg_T stay on the device
   ResidualPack res;
 };
 
@@ -98,6 +99,10 @@ class SolverBase {
   virtual void upload() = 0;             // host records -> backend
   virtual void cycle_update() {}         // per-cycle y+ / sources (backend side)
   virtual void sample_monitors(std::vector<MonitorPoint>& mp);
+  // device backends: pull dt, accumulated time and the error flag to the host
+  virtual void sync_scalars() {}
+  // called after an outer-cycle roll-over (cur_time_part folded into global_time)
+  virtual void on_cycle_roll() {}
   StepParams make_params(long it) const;
 
  protected:

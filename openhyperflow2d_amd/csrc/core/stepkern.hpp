@@ -129,11 +129,12 @@ HF_HD inline EqFlags eq_flags(int k, u64 CT, u64 TT, int sm) {
     // The reference shifts the eps masks by (k - 7) as well, so eps tests
     // the *next* flag bit (quirk Q3, kept for parity).
     const int sh = k - 4 - NCOMP;
-    f.upd = !has_all(TT, TCT_k_CONST << sh);
-    f.dx = !has_all(TT, TCT_dkdx_NULL << sh);
-    f.dy = !has_all(TT, TCT_dkdy_NULL << sh);
-    f.dx2 = has_all(TT, TCT_d2kdx2_NULL << sh);
-    f.dy2 = has_all(TT, TCT_d2kdy2_NULL << sh);
+    const bool e = (k == I_EPS);
+    f.upd = !has_all(TT, (e ? TCT_eps_CONST : TCT_k_CONST) << sh);
+    f.dx = !has_all(TT, (e ? TCT_depsdx_NULL : TCT_dkdx_NULL) << sh);
+    f.dy = !has_all(TT, (e ? TCT_depsdy_NULL : TCT_dkdy_NULL) << sh);
+    f.dx2 = has_all(TT, (e ? TCT_d2epsdx2_NULL : TCT_d2kdx2_NULL) << sh);
+    f.dy2 = has_all(TT, (e ? TCT_d2epsdy2_NULL : TCT_d2kdy2_NULL) << sh);
   }
   return f;
 }
@@ -199,6 +200,31 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
     real s = in.S[o + idx];
     const EqFlags f = eq_flags(k, CT, TT, P.sm);
     if (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT)))) {
+      // A TCT-frozen turbulence equation whose CT-based pass-2 test says
+      // "not frozen" (quirk Q4) is scored against the never-written
+      // predictor scratch (0) in the reference: DD = 1, dS = -S.
+      if (k < Num_Eq && !f.upd && k >= 4 + NCOMP && P.sm == SM_NS && has_turb_eq(TT) &&
+          !pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
+        const real beta = in.beta[o + idx];
+        const real DD = std::fabs(s) > 1.e-15 ? 1.0 : 1.0;
+        const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+        out.beta[o + idx] = blend_beta(P.bff, bmin, beta, DD, 1.0);
+        if (res) {
+          EqResidual& e = res->eq[k];
+          if (DD >= e.dd_max) {
+            e.dd_max = DD;
+            e.i = P.gx0 + i;
+            e.j = j;
+          }
+          if (P.alternate_rms) {
+            e.rms += s * s;
+            e.sum_div += s * s;
+          } else {
+            e.rms += DD * DD;
+            e.count += 1;
+          }
+        }
+      }
       out.S[o + idx] = s;
       out.dSdx[o + idx] = in.dSdx[o + idx];
       out.dSdy[o + idx] = in.dSdy[o + idx];
@@ -271,7 +297,8 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
 // ---------------------------------------------------------------------------
 // Gradients + FillNode2D + dt + chemistry for one cell.
 // `sin` holds the committed state (S after predict), prim_old the previous
-// step's U/V/Tg.  Results go to `out` (S, A, B, F, primitives).
+// step's U/V/Tg.  Non-double-buffered per-cell fields are read from `sin`
+// and written to `out` (the same arrays except A/B in the fused Euler path).
 // Returns the local dt (1.0 when the cell does not limit dt); sets *neg_T.
 // ---------------------------------------------------------------------------
 HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
@@ -289,47 +316,47 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   c.CT = CT;
   c.TurbType = sin.TT[idx];
   for (int k = 0; k < NEQ; k++) {
-    c.A[k] = out.A[k * N + idx];
-    c.B[k] = out.B[k * N + idx];
-    c.F[k] = out.F[k * N + idx];
-    c.Src[k] = out.Src[k * N + idx];
-    c.SrcAdd[k] = out.SrcAdd[k * N + idx];
+    c.A[k] = sin.A[k * N + idx];
+    c.B[k] = sin.B[k * N + idx];
+    c.F[k] = sin.F[k * N + idx];
+    c.Src[k] = sin.Src[k * N + idx];
+    c.SrcAdd[k] = sin.SrcAdd[k * N + idx];
     c.RX[k] = c.RY[k] = 0;
   }
   c.U = prim_old.U[idx];
   c.V = prim_old.V[idx];
   c.Tg = prim_old.Tg[idx];
-  c.p = out.p[idx];
-  c.k = out.kk[idx];
-  c.R = out.R[idx];
-  c.CP = out.CP[idx];
-  c.lam = out.lam[idx];
-  c.mu = out.mu[idx];
-  c.Diff = out.Diff[idx];
-  c.mu_t = out.mu_t[idx];
-  c.lam_t = out.lam_t[idx];
+  c.p = sin.p[idx];
+  c.k = sin.kk[idx];
+  c.R = sin.R[idx];
+  c.CP = sin.CP[idx];
+  c.lam = sin.lam[idx];
+  c.mu = sin.mu[idx];
+  c.Diff = sin.Diff[idx];
+  c.mu_t = sin.mu_t[idx];
+  c.lam_t = sin.lam_t[idx];
   c.l_min = sin.l_min[idx];
   c.y_plus = sin.y_plus[idx];
-  c.Re_local = out.Re_local[idx];
+  c.Re_local = sin.Re_local[idx];
   c.BGX = sin.BGX[idx];
   c.BGY = sin.BGY[idx];
   c.Tf = sin.Tf[idx];
   c.Uw = c.Vw = 0;
   c.y = (j + 0.5) * P.dy;
   for (int s = 0; s < NSPEC; s++) {
-    c.Y[s] = out.Y[s * N + idx];
+    c.Y[s] = sin.Y[s * N + idx];
     c.droYdx[s] = c.droYdy[s] = 0;
   }
-  c.dUdx = out.grad[G_DUDX * N + idx];
-  c.dUdy = out.grad[G_DUDY * N + idx];
-  c.dVdx = out.grad[G_DVDX * N + idx];
-  c.dVdy = out.grad[G_DVDY * N + idx];
-  c.dTdx = out.grad[G_DTDX * N + idx];
-  c.dTdy = out.grad[G_DTDY * N + idx];
-  c.dkdx = out.grad[G_DKDX * N + idx];
-  c.dkdy = out.grad[G_DKDY * N + idx];
-  c.depsdx = out.grad[G_DEDX * N + idx];
-  c.depsdy = out.grad[G_DEDY * N + idx];
+  c.dUdx = sin.grad[G_DUDX * N + idx];
+  c.dUdy = sin.grad[G_DUDY * N + idx];
+  c.dVdx = sin.grad[G_DVDX * N + idx];
+  c.dVdy = sin.grad[G_DVDY * N + idx];
+  c.dTdx = sin.grad[G_DTDX * N + idx];
+  c.dTdy = sin.grad[G_DTDY * N + idx];
+  c.dkdx = sin.grad[G_DKDX * N + idx];
+  c.dkdy = sin.grad[G_DKDY * N + idx];
+  c.depsdx = sin.grad[G_DEDX * N + idx];
+  c.depsdy = sin.grad[G_DEDY * N + idx];
 
   if (active && P.sm == SM_NS) {
     const uint8_t nbm = sin.nb[idx];

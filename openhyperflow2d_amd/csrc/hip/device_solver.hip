@@ -1,0 +1,736 @@
+// GPU backend for MI355X (gfx950): device-resident SoA state, one HIP
+// kernel per DEEPS phase, RCCL halo exchange / reductions for strip-
+// decomposed multi-GPU runs.
+//
+// Kernels (rocprof names):
+//   hf2d_predict<RES>     pass 1 + 2a (predictor, BC, residual, blending factor)
+//   hf2d_fill             pass 2b/2c (gradients, FillNode2D, dt, chemistry)
+//   hf2d_fused_euler      predict + fill in one sweep for Euler problems
+//   hf2d_wall_solid/_wall owner-computes wall heat sources (K5)
+//   hf2d_reduce_residual  deterministic tree over per-wave residual partials (K6)
+//   hf2d_pack/unpack      halo column packing (K7)
+//   hf2d_yplus            per-cycle y+ (K10)
+// dt never leaves the device inside the inner loop: hf2d_fill folds the
+// local CFL limit into a device slot with an integer atomicMin on the IEEE
+// bits (valid for positive doubles, order independent => deterministic) and
+// the next step's kernels read it from there.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../core/solver.hpp"
+#include "device_solver.hpp"
+
+#define HIP_CHECK(x)                                                                             \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess)                                                                        \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " +      \
+                               __FILE__ + ":" + std::to_string(__LINE__));                       \
+  } while (0)
+#define NCCL_CHECK(x)                                                                            \
+  do {                                                                                           \
+    ncclResult_t r_ = (x);                                                                       \
+    if (r_ != ncclSuccess)                                                                       \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r_) + " at " +    \
+                               __FILE__ + ":" + std::to_string(__LINE__));                       \
+  } while (0)
+
+namespace hf2d {
+
+constexpr int BLOCK = 256;
+constexpr int WAVE = 64;
+
+// Per-step scalars living on the device.
+struct DevScalars {
+  unsigned long long dt_bits[3];   // rotating dt slots (IEEE bits of positive doubles)
+  double time_part;                // accumulated dt since the cycle start
+  int neg_T;
+  int pad;
+};
+
+__device__ inline double bits_to_d(unsigned long long b) { return __longlong_as_double((long long)b); }
+__device__ inline unsigned long long d_to_bits(double d) { return (unsigned long long)__double_as_longlong(d); }
+
+__device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
+  const double dt = bits_to_d(sc->dt_bits[slot]);
+  P.dt = dt;
+  P.dtdx = dt / P.dx;
+  P.dtdy = dt / P.dy;
+}
+
+// ---------------------------------------------------------------------------
+// Wave-level residual reduction helpers
+// ---------------------------------------------------------------------------
+__device__ inline void shfl_merge(ResidualPack& r, int off) {
+  for (int k = 0; k < NEQ; k++) {
+    EqResidual o;
+    o.dd_max = __shfl_xor(r.eq[k].dd_max, off, WAVE);
+    o.i = __shfl_xor(r.eq[k].i, off, WAVE);
+    o.j = __shfl_xor(r.eq[k].j, off, WAVE);
+    o.rms = __shfl_xor(r.eq[k].rms, off, WAVE);
+    o.sum_div = __shfl_xor(r.eq[k].sum_div, off, WAVE);
+    o.count = __shfl_xor(r.eq[k].count, off, WAVE);
+    EqResidual& f = r.eq[k];
+    const bool later = (o.i > f.i) || (o.i == f.i && o.j > f.j);
+    if (o.dd_max > f.dd_max || (o.dd_max == f.dd_max && later)) {
+      f.dd_max = o.dd_max;
+      f.i = o.i;
+      f.j = o.j;
+    }
+    f.rms += o.rms;
+    f.sum_div += o.sum_div;
+    f.count += o.count;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+template <bool RES>
+__global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA out, long c0, long c1,
+                                                       DevScalars* sc, int slot, int slot_next, int serial,
+                                                       ResidualPack* partials) {
+  apply_dt(P, sc, slot);
+  const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (g == 0) {
+    // reset the next dt slot and accumulate physical time
+    sc->dt_bits[slot_next] = serial ? sc->dt_bits[slot] : d_to_bits(1.0);
+    sc->time_part += P.dt;
+  }
+  const long c = c0 + g;
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  if (c < c1) {
+    const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+    predict_cell(P, in, out, i, j, RES ? &r : nullptr);
+  }
+  if (RES) {
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack* partials, long n,
+                                                               ResidualPack* outp) {
+  __shared__ ResidualPack sh[32];
+  ResidualPack acc;
+  residual_reset(acc);
+  for (int k = 0; k < NEQ; k++) acc.eq[k].i = acc.eq[k].j = -1;
+  for (long t = threadIdx.x; t < n; t += BLOCK) residual_merge_lex(acc, partials[t]);
+  for (int off = 1; off < WAVE; off <<= 1) shfl_merge(acc, off);
+  const int w = threadIdx.x / WAVE;
+  if ((threadIdx.x & (WAVE - 1)) == 0) sh[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ResidualPack a = sh[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) residual_merge_lex(a, sh[q]);
+    *outp = a;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
+                                                    DevScalars* sc, int slot, int slot_next) {
+  apply_dt(P, sc, slot);
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  double dtl = 1.0;
+  int neg = 0;
+  if (c < c1) {
+    const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+    dtl = fill_cell(P, sin, pold, out, i, j, &neg, true);
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+// Euler: no gradients, so the fill of a cell depends only on its own
+// predicted state and the predictor and fill run in one sweep.  A and B are
+// ping-ponged (neighbours read the old fluxes).
+template <bool RES>
+__global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, SoA mid, SoA out, long c0, long c1,
+                                                           DevScalars* sc, int slot, int slot_next, int serial,
+                                                           ResidualPack* partials) {
+  apply_dt(P, sc, slot);
+  const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (g == 0) {
+    sc->dt_bits[slot_next] = serial ? sc->dt_bits[slot] : d_to_bits(1.0);
+    sc->time_part += P.dt;
+  }
+  const long c = c0 + g;
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  if (c < c1) {
+    const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+    predict_cell(P, in, mid, i, j, RES ? &r : nullptr);
+    dtl = fill_cell(P, mid, mid, out, i, j, &neg, false);
+  }
+  if (RES) {
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= c1) return;
+  const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+  wall_heat_solid_cell(P, s, qdir, i, j);
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_wall_wall(StepParams P, SoA s, const real* qdir, long c0, long c1,
+                                                         const DevScalars* sc, int slot) {
+  apply_dt(P, sc, slot);
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= c1) return;
+  const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+  wall_heat_wall_cell(P, s, qdir, i, j);
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_yplus(StepParams P, SoA s, long c0, long c1, int gx0) {
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= c1) return;
+  const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+  y_plus_cell(P, s, i, j, gx0);
+}
+
+// Halo pack: nf field columns (each ny contiguous doubles at src[f] + col*ny)
+struct ColList {
+  real* f[48];
+  int nf;
+};
+__global__ void hf2d_pack(ColList L, int col, int ny, real* buf) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L.nf * ny) return;
+  const int f = t / ny, j = t - f * ny;
+  buf[t] = L.f[f][(long)col * ny + j];
+}
+__global__ void hf2d_unpack(ColList L, int col, int ny, const real* buf) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L.nf * ny) return;
+  const int f = t / ny, j = t - f * ny;
+  L.f[f][(long)col * ny + j] = buf[t];
+}
+
+// ---------------------------------------------------------------------------
+// DeviceSolver
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  std::vector<void*> ptrs;
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    HIP_CHECK(hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(T)));
+    ptrs.push_back(p);
+    return (T*)p;
+  }
+  ~DevBuf() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+struct DeviceSolver::Impl {
+  DevBuf mem;
+  hipStream_t stream = nullptr;
+  // device arrays (same roles as HostArrays)
+  real *S[2], *A[2], *B[2], *F, *Src, *SrcAdd, *beta, *dSdx[2], *dSdy[2];
+  real *U[2], *V[2], *Tg[2], *p, *kk, *R, *CP, *lam, *mu, *mu_t, *lam_t, *Diff, *Y;
+  real *l_min, *y_plus, *Re_local, *BGX, *BGY, *Tf, *Q_conv, *grad, *qdir;
+  u64 *CT, *TT;
+  uint8_t* nb;
+  int32_t *iw, *jw;
+  SpeciesProps* species = nullptr;
+  DevScalars* sc = nullptr;
+  DevScalars* sc_host = nullptr;   // pinned
+  ResidualPack* partials = nullptr;
+  ResidualPack* res_out = nullptr;
+  ResidualPack* res_host = nullptr;   // pinned
+  long max_partials = 0;
+  real* halo_send[2] = {nullptr, nullptr};
+  real* halo_recv[2] = {nullptr, nullptr};
+  long halo_cap = 0;
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1;
+
+  SoA view(const HostArrays& h, int sb, int ab, int db, int pb) const {
+    SoA s;
+    s.nx = h.nx;
+    s.ny = h.ny;
+    s.N = h.N;
+    s.S = S[sb];
+    s.A = A[ab];
+    s.B = B[ab];
+    s.F = F;
+    s.Src = Src;
+    s.SrcAdd = SrcAdd;
+    s.beta = beta;
+    s.dSdx = dSdx[db];
+    s.dSdy = dSdy[db];
+    s.U = U[pb];
+    s.V = V[pb];
+    s.Tg = Tg[pb];
+    s.p = p;
+    s.kk = kk;
+    s.R = R;
+    s.CP = CP;
+    s.lam = lam;
+    s.mu = mu;
+    s.mu_t = mu_t;
+    s.lam_t = lam_t;
+    s.Diff = Diff;
+    s.Y = Y;
+    s.l_min = l_min;
+    s.y_plus = y_plus;
+    s.Re_local = Re_local;
+    s.BGX = BGX;
+    s.BGY = BGY;
+    s.Tf = Tf;
+    s.Q_conv = Q_conv;
+    s.grad = grad;
+    s.CT = CT;
+    s.TT = TT;
+    s.nb = nb;
+    s.iw = iw;
+    s.jw = jw;
+    return s;
+  }
+};
+
+static int g_device_count_cache = -1;
+
+bool gpu_available() {
+  if (g_device_count_cache < 0) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    g_device_count_cache = n;
+  }
+  return g_device_count_cache > 0;
+}
+
+DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase(c), impl(new Impl) {
+  if (!gpu_available()) throw std::runtime_error("no HIP device available");
+  dev = device;
+  HIP_CHECK(hipSetDevice(dev));
+  HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
+  gi0 = gi0_;
+  gi1 = gi1_ < 0 ? c.J.nx : gi1_;
+  const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
+  l_off = lh;
+  h.allocate((gi1 - gi0) + lh + rh, c.J.ny);
+  const long N = h.N;
+  Impl& m = *impl;
+  for (int b = 0; b < 2; b++) {
+    m.S[b] = m.mem.alloc<real>(NEQ * N);
+    m.A[b] = m.mem.alloc<real>(NEQ * N);
+    m.B[b] = m.mem.alloc<real>(NEQ * N);
+    m.dSdx[b] = m.mem.alloc<real>(NEQ * N);
+    m.dSdy[b] = m.mem.alloc<real>(NEQ * N);
+    m.U[b] = m.mem.alloc<real>(N);
+    m.V[b] = m.mem.alloc<real>(N);
+    m.Tg[b] = m.mem.alloc<real>(N);
+  }
+  m.F = m.mem.alloc<real>(NEQ * N);
+  m.Src = m.mem.alloc<real>(NEQ * N);
+  m.SrcAdd = m.mem.alloc<real>(NEQ * N);
+  m.beta = m.mem.alloc<real>(NEQ * N);
+  m.p = m.mem.alloc<real>(N);
+  m.kk = m.mem.alloc<real>(N);
+  m.R = m.mem.alloc<real>(N);
+  m.CP = m.mem.alloc<real>(N);
+  m.lam = m.mem.alloc<real>(N);
+  m.mu = m.mem.alloc<real>(N);
+  m.mu_t = m.mem.alloc<real>(N);
+  m.lam_t = m.mem.alloc<real>(N);
+  m.Diff = m.mem.alloc<real>(N);
+  m.Y = m.mem.alloc<real>(NSPEC * N);
+  m.l_min = m.mem.alloc<real>(N);
+  m.y_plus = m.mem.alloc<real>(N);
+  m.Re_local = m.mem.alloc<real>(N);
+  m.BGX = m.mem.alloc<real>(N);
+  m.BGY = m.mem.alloc<real>(N);
+  m.Tf = m.mem.alloc<real>(N);
+  m.Q_conv = m.mem.alloc<real>(N);
+  m.grad = m.mem.alloc<real>(NGRAD * N);
+  m.qdir = m.mem.alloc<real>(4 * N);
+  m.CT = m.mem.alloc<u64>(N);
+  m.TT = m.mem.alloc<u64>(N);
+  m.nb = m.mem.alloc<uint8_t>(N);
+  m.iw = m.mem.alloc<int32_t>(N);
+  m.jw = m.mem.alloc<int32_t>(N);
+  m.species = m.mem.alloc<SpeciesProps>(1);
+  m.sc = m.mem.alloc<DevScalars>(1);
+  HIP_CHECK(hipHostMalloc((void**)&m.sc_host, sizeof(DevScalars), hipHostMallocDefault));
+  m.max_partials = (N + BLOCK - 1) / BLOCK * (BLOCK / WAVE);
+  m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
+  m.res_out = m.mem.alloc<ResidualPack>(1);
+  HIP_CHECK(hipHostMalloc((void**)&m.res_host, sizeof(ResidualPack), hipHostMallocDefault));
+  m.halo_cap = (long)48 * h.ny;
+  for (int d = 0; d < 2; d++) {
+    m.halo_send[d] = m.mem.alloc<real>(m.halo_cap);
+    m.halo_recv[d] = m.mem.alloc<real>(m.halo_cap);
+  }
+  upload();
+}
+
+DeviceSolver::~DeviceSolver() {
+  host_comm.reset();
+  if (impl) {
+    if (impl->comm) ncclCommDestroy(impl->comm);
+    if (impl->sc_host) (void)hipHostFree(impl->sc_host);
+    if (impl->res_host) (void)hipHostFree(impl->res_host);
+    if (impl->stream) (void)hipStreamDestroy(impl->stream);
+  }
+}
+
+void* DeviceSolver::stream() const { return (void*)impl->stream; }
+
+void DeviceSolver::upload() {
+  HIP_CHECK(hipSetDevice(dev));
+  h.from_field(cs.J, gi0 - l_off);
+  Impl& m = *impl;
+  hipStream_t st = m.stream;
+  const long N = h.N;
+  auto cp = [&](void* d, const void* s, size_t bytes) { HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st)); };
+  const size_t EQB = NEQ * N * sizeof(real), SB = N * sizeof(real);
+  for (int b = 0; b < 2; b++) {
+    cp(m.S[b], h.S[0].data(), EQB);
+    cp(m.A[b], h.A.data(), EQB);
+    cp(m.B[b], h.B.data(), EQB);
+    cp(m.dSdx[b], h.dSdx[0].data(), EQB);
+    cp(m.dSdy[b], h.dSdy[0].data(), EQB);
+    cp(m.U[b], h.U[0].data(), SB);
+    cp(m.V[b], h.V[0].data(), SB);
+    cp(m.Tg[b], h.Tg[0].data(), SB);
+  }
+  cp(m.F, h.F.data(), EQB);
+  cp(m.Src, h.Src.data(), EQB);
+  cp(m.SrcAdd, h.SrcAdd.data(), EQB);
+  cp(m.beta, h.beta.data(), EQB);
+  cp(m.p, h.p.data(), SB);
+  cp(m.kk, h.kk.data(), SB);
+  cp(m.R, h.R.data(), SB);
+  cp(m.CP, h.CP.data(), SB);
+  cp(m.lam, h.lam.data(), SB);
+  cp(m.mu, h.mu.data(), SB);
+  cp(m.mu_t, h.mu_t.data(), SB);
+  cp(m.lam_t, h.lam_t.data(), SB);
+  cp(m.Diff, h.Diff.data(), SB);
+  cp(m.Y, h.Y.data(), NSPEC * SB);
+  cp(m.l_min, h.l_min.data(), SB);
+  cp(m.y_plus, h.y_plus.data(), SB);
+  cp(m.Re_local, h.Re_local.data(), SB);
+  cp(m.BGX, h.BGX.data(), SB);
+  cp(m.BGY, h.BGY.data(), SB);
+  cp(m.Tf, h.Tf.data(), SB);
+  cp(m.Q_conv, h.Q_conv.data(), SB);
+  cp(m.grad, h.grad.data(), NGRAD * SB);
+  cp(m.CT, h.CT.data(), N * sizeof(u64));
+  cp(m.TT, h.TT.data(), N * sizeof(u64));
+  cp(m.nb, h.nb.data(), N);
+  cp(m.iw, h.iw.data(), N * sizeof(int32_t));
+  cp(m.jw, h.jw.data(), N * sizeof(int32_t));
+  cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
+  DevScalars s0{};
+  const double d0 = dt;
+  std::memcpy(&s0.dt_bits[0], &d0, 8);
+  s0.dt_bits[1] = s0.dt_bits[2] = s0.dt_bits[0];
+  s0.time_part = 0.0;
+  time_offset = -cur_time_part;
+  last_dev_time = 0.0;
+  *m.sc_host = s0;
+  cp(m.sc, m.sc_host, sizeof(DevScalars));
+  HIP_CHECK(hipStreamSynchronize(st));
+  nstep = 0;
+  abuf = 0;
+  dsbuf = 0;
+  pbuf = 0;
+}
+
+void DeviceSolver::download(Field& J) {
+  HIP_CHECK(hipSetDevice(dev));
+  Impl& m = *impl;
+  hipStream_t st = m.stream;
+  const long N = h.N;
+  auto cp = [&](void* d, const void* s, size_t bytes) { HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st)); };
+  const size_t EQB = NEQ * N * sizeof(real), SB = N * sizeof(real);
+  cp(h.S[0].data(), m.S[0], EQB);
+  cp(h.A.data(), m.A[abuf], EQB);
+  cp(h.B.data(), m.B[abuf], EQB);
+  cp(h.dSdx[0].data(), m.dSdx[dsbuf], EQB);
+  cp(h.dSdy[0].data(), m.dSdy[dsbuf], EQB);
+  cp(h.U[0].data(), m.U[pbuf], SB);
+  cp(h.V[0].data(), m.V[pbuf], SB);
+  cp(h.Tg[0].data(), m.Tg[pbuf], SB);
+  cp(h.F.data(), m.F, EQB);
+  cp(h.Src.data(), m.Src, EQB);
+  cp(h.SrcAdd.data(), m.SrcAdd, EQB);
+  cp(h.beta.data(), m.beta, EQB);
+  cp(h.p.data(), m.p, SB);
+  cp(h.kk.data(), m.kk, SB);
+  cp(h.R.data(), m.R, SB);
+  cp(h.CP.data(), m.CP, SB);
+  cp(h.lam.data(), m.lam, SB);
+  cp(h.mu.data(), m.mu, SB);
+  cp(h.mu_t.data(), m.mu_t, SB);
+  cp(h.lam_t.data(), m.lam_t, SB);
+  cp(h.Diff.data(), m.Diff, SB);
+  cp(h.Y.data(), m.Y, NSPEC * SB);
+  cp(h.y_plus.data(), m.y_plus, SB);
+  cp(h.Re_local.data(), m.Re_local, SB);
+  cp(h.Q_conv.data(), m.Q_conv, SB);
+  cp(h.grad.data(), m.grad, NGRAD * SB);
+  cp(h.CT.data(), m.CT, N * sizeof(u64));
+  HIP_CHECK(hipStreamSynchronize(st));
+  h.to_field(J, gi0 - l_off, l_off, l_off + (gi1 - gi0), 0, 0);
+}
+
+void DeviceSolver::on_cycle_roll() { time_offset = last_dev_time; }
+
+void DeviceSolver::sync_scalars() {
+  Impl& m = *impl;
+  HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  const int slot = nstep % 3;
+  std::memcpy(&dt, &m.sc_host->dt_bits[slot], 8);
+  cur_time_part = m.sc_host->time_part - time_offset;
+  last_dev_time = m.sc_host->time_part;
+  if (comm->allreduce_max_int(m.sc_host->neg_T)) {
+    char b[256];
+    std::snprintf(b, sizeof b, "ERROR: Computational unstability (Tg < 0) before iteration %ld", last_iter + iter);
+    throw std::runtime_error(b);
+  }
+}
+
+// Called at each outer-cycle boundary by the driver (time_part restarts).
+void DeviceSolver::cycle_update() {
+  Impl& m = *impl;
+  if (cs.cfg.ProblemType == SM_NS && cs.cfg.semantics != Semantics::SERIAL) {
+    StepParams P = make_params(last_iter);
+    P.nx = h.nx;
+    P.ny = h.ny;
+    SoA s = m.view(h, 0, abuf, dsbuf, pbuf);
+    const long c0 = (long)l_off * h.ny, c1 = (long)(l_off + (gi1 - gi0)) * h.ny;
+    const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(hf2d_yplus, dim3(nb), dim3(BLOCK), 0, m.stream, P, s, c0, c1, gi0 - l_off);
+    HIP_CHECK(hipGetLastError());
+  }
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+}
+
+// Host-side reductions of the driver over RCCL (output steps only).
+struct RcclHostComm : Comm {
+  ncclComm_t c;
+  hipStream_t st;
+  int r, n;
+  double* buf = nullptr;
+  RcclHostComm(ncclComm_t c_, hipStream_t s_, int r_, int n_) : c(c_), st(s_), r(r_), n(n_) {
+    HIP_CHECK(hipMalloc((void**)&buf, sizeof(ResidualPack) * (n + 1) + 64));
+  }
+  ~RcclHostComm() override { (void)hipFree(buf); }
+  int rank() const override { return r; }
+  int size() const override { return n; }
+  double reduce1(double v, ncclRedOp_t op) {
+    HIP_CHECK(hipMemcpyAsync(buf, &v, 8, hipMemcpyHostToDevice, st));
+    NCCL_CHECK(ncclAllReduce(buf, buf, 1, ncclDouble, op, c, st));
+    HIP_CHECK(hipMemcpyAsync(&v, buf, 8, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return v;
+  }
+  real allreduce_min(real v) override { return reduce1(v, ncclMin); }
+  real allreduce_sum(real v) override { return reduce1(v, ncclSum); }
+  int allreduce_max_int(int v) override { return (int)reduce1((double)v, ncclMax); }
+  void allreduce_residual(ResidualPack& p) override {
+    std::vector<ResidualPack> all(n);
+    char* dbuf = (char*)buf;
+    HIP_CHECK(hipMemcpyAsync(dbuf, &p, sizeof(ResidualPack), hipMemcpyHostToDevice, st));
+    NCCL_CHECK(ncclAllGather(dbuf, dbuf + sizeof(ResidualPack), sizeof(ResidualPack), ncclChar, c, st));
+    HIP_CHECK(hipMemcpyAsync(all.data(), dbuf + sizeof(ResidualPack), sizeof(ResidualPack) * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    ResidualPack a = all[0];
+    for (int q = 1; q < n; q++) residual_merge_lex(a, all[q]);
+    p = a;
+  }
+};
+
+std::string DeviceSolver::nccl_unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+void DeviceSolver::init_comm(const std::string& uid, int rank, int nranks) {
+  HIP_CHECK(hipSetDevice(dev));
+  ncclUniqueId id;
+  if (uid.size() != sizeof(id.internal)) throw std::runtime_error("bad RCCL unique id size");
+  std::memcpy(id.internal, uid.data(), sizeof(id.internal));
+  NCCL_CHECK(ncclCommInitRank(&impl->comm, nranks, id, rank));
+  impl->rank = rank;
+  impl->nranks = nranks;
+  host_comm.reset(new RcclHostComm(impl->comm, impl->stream, rank, nranks));
+  comm = host_comm.get();
+}
+
+int DeviceSolver::comm_rank() const { return impl->rank; }
+int DeviceSolver::comm_size() const { return impl->nranks; }
+
+// Halo exchange of one field group with RCCL send/recv to the strip
+// neighbours (rank-1 owns the columns to the left).
+void DeviceSolver::exchange(int group) {
+  Impl& m = *impl;
+  if (!m.comm || m.nranks == 1) return;
+  const int ny = h.ny;
+  const long N = h.N;
+  ColList L;
+  L.nf = 0;
+  auto add_eq = [&](real* base) {
+    for (int k = 0; k < NEQ; k++) L.f[L.nf++] = base + (long)k * N;
+  };
+  if (group == CpuSolver::HALO_MID) {
+    add_eq(m.S[1]);
+  } else if (group == CpuSolver::HALO_QDIR) {
+    for (int d = 0; d < 4; d++) L.f[L.nf++] = m.qdir + (long)d * N;
+  } else {
+    add_eq(m.S[0]);
+    add_eq(m.A[abuf]);
+    add_eq(m.B[abuf]);
+    add_eq(m.dSdx[dsbuf]);
+    L.f[L.nf++] = m.U[pbuf];
+    L.f[L.nf++] = m.V[pbuf];
+    L.f[L.nf++] = m.Tg[pbuf];
+    L.f[L.nf++] = m.lam;
+    L.f[L.nf++] = m.lam_t;
+  }
+  const int cnt = L.nf * ny;
+  const unsigned nb = (unsigned)((cnt + BLOCK - 1) / BLOCK);
+  const int first = l_off, last = l_off + (gi1 - gi0) - 1;
+  const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
+  if (has_left) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, first, ny, m.halo_send[0]);
+  if (has_right) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, last, ny, m.halo_send[1]);
+  NCCL_CHECK(ncclGroupStart());
+  if (has_left) {
+    NCCL_CHECK(ncclSend(m.halo_send[0], cnt, ncclDouble, m.rank - 1, m.comm, m.stream));
+    NCCL_CHECK(ncclRecv(m.halo_recv[0], cnt, ncclDouble, m.rank - 1, m.comm, m.stream));
+  }
+  if (has_right) {
+    NCCL_CHECK(ncclSend(m.halo_send[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
+    NCCL_CHECK(ncclRecv(m.halo_recv[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
+  }
+  NCCL_CHECK(ncclGroupEnd());
+  if (has_left) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, 0, ny, m.halo_recv[0]);
+  if (has_right) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, h.nx - 1, ny, m.halo_recv[1]);
+}
+
+StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
+  Impl& m = *impl;
+  StepParams P = P0;
+  P.nx = h.nx;
+  P.ny = h.ny;
+  P.i0 = l_off;
+  P.i1 = l_off + (gi1 - gi0);
+  P.gx0 = gi0 - l_off;
+  P.do_residual = want_res ? 1 : 0;
+  P.species = m.species;
+  const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
+  const unsigned nblk = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+  const int slot = nstep % 3, slot_next = (nstep + 1) % 3;
+  const int serial = cs.cfg.semantics == Semantics::SERIAL ? 1 : 0;
+  const bool euler = P.sm != SM_NS;
+  hipStream_t st = m.stream;
+  if (euler && fused) {
+    SoA in = m.view(h, 0, abuf, dsbuf, pbuf);
+    SoA mid = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
+    SoA out = m.view(h, 0, 1 - abuf, 1 - dsbuf, pbuf);
+    if (want_res)
+      hipLaunchKernelGGL(hf2d_fused_euler<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, out, c0, c1, m.sc, slot,
+                         slot_next, serial, m.partials);
+    else
+      hipLaunchKernelGGL(hf2d_fused_euler<false>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, out, c0, c1, m.sc, slot,
+                         slot_next, serial, m.partials);
+    HIP_CHECK(hipGetLastError());
+    abuf = 1 - abuf;
+    dsbuf = 1 - dsbuf;
+  } else {
+    SoA in = m.view(h, 0, abuf, dsbuf, pbuf);
+    SoA mid = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
+    if (want_res)
+      hipLaunchKernelGGL(hf2d_predict<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next,
+                         serial, m.partials);
+    else
+      hipLaunchKernelGGL(hf2d_predict<false>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next,
+                         serial, m.partials);
+    HIP_CHECK(hipGetLastError());
+    if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
+    SoA sin = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
+    SoA out = m.view(h, 0, abuf, 1 - dsbuf, 1 - pbuf);
+    hipLaunchKernelGGL(hf2d_fill, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot, slot_next);
+    HIP_CHECK(hipGetLastError());
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+  }
+  if (m.comm && m.nranks > 1) {
+    // global dt: MIN over ranks, in place on the next slot
+    real* dslot = (real*)&m.sc->dt_bits[slot_next];
+    NCCL_CHECK(ncclAllReduce(dslot, dslot, 1, ncclDouble, ncclMin, m.comm, st));
+    exchange(CpuSolver::HALO_STATE);
+  }
+  if (!cs.cfg.isAdiabaticWall) {
+    SoA s = m.view(h, 0, abuf, dsbuf, pbuf);
+    hipLaunchKernelGGL(hf2d_wall_solid, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1);
+    exchange(CpuSolver::HALO_QDIR);
+    hipLaunchKernelGGL(hf2d_wall_wall, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1, m.sc, slot);
+    HIP_CHECK(hipGetLastError());
+  }
+  nstep++;
+  StepResult r;
+  r.async = true;
+  if (want_res) {
+    hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials, (long)nblk * (BLOCK / WAVE),
+                       m.res_out);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(m.res_host, m.res_out, sizeof(ResidualPack), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    r.res = *m.res_host;
+    r.have_residual = true;
+  }
+  return r;
+}
+
+void DeviceSolver::synchronize() { HIP_CHECK(hipStreamSynchronize(impl->stream)); }
+
+std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device) {
+  return std::unique_ptr<SolverBase>(new DeviceSolver(cs, device < 0 ? 0 : device));
+}
+
+}  // namespace hf2d

@@ -1,0 +1,49 @@
+// DeviceSolver: MI355X backend of the DEEPS time march (see device_solver.hip).
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "../core/solver.hpp"
+
+namespace hf2d {
+
+bool gpu_available();
+
+class DeviceSolver : public SolverBase {
+ public:
+  DeviceSolver(Case& cs, int device = 0, int gi0 = 0, int gi1 = -1);
+  ~DeviceSolver() override;
+  StepResult do_step(const StepParams& P, bool want_res) override;
+  void download(Field& J) override;
+  void upload() override;
+  void cycle_update() override;
+  void sync_scalars() override;
+  void on_cycle_roll() override;
+  double time_offset = 0.0, last_dev_time = 0.0;
+  void synchronize();
+  void* stream() const;
+
+  // Multi-GPU: RCCL communicator over the strip ranks.
+  static std::string nccl_unique_id();
+  void init_comm(const std::string& uid, int rank, int nranks);
+  int comm_rank() const;
+  int comm_size() const;
+  void exchange(int group);
+
+  HostArrays h;           // host staging copy
+  int dev = 0;
+  int gi0 = 0, gi1 = 0, l_off = 0;
+  long nstep = 0;
+  int abuf = 0, dsbuf = 0, pbuf = 0;
+  bool fused = true;      // Euler: single fused predict+fill kernel
+  std::unique_ptr<Comm> host_comm;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl;
+};
+
+std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device);
+
+}  // namespace hf2d

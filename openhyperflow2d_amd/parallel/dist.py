@@ -1,0 +1,146 @@
+"""Distributed runner: one process per GPU (or per CPU rank), torchrun-style env.
+
+GPU ranks: torch.distributed only bootstraps — rank 0 creates an RCCL unique
+id which is broadcast over the default process group; afterwards every
+per-step exchange (halo send/recv to the strip neighbours, MIN all-reduce of
+dt) is issued by the native DeviceSolver with RCCL on its own HIP stream, so
+the inner loop never returns to Python.
+
+CPU ranks (tests, gloo): the native CpuSolver calls back into Python for the
+halo columns and the scalar reductions, which go over torch.distributed.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from .strips import balanced_columns
+
+
+def init_from_env(backend: Optional[str] = None):
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* env vars."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group(backend=backend or "gloo", rank=rank, world_size=world)
+    return rank, world
+
+
+class DistributedSimulation:
+    """A strip of a deck run on this rank."""
+
+    def __init__(self, deck_text: str, backend: str = "gpu", *, rank: int = 0, world: int = 1,
+                 device: int = 0, semantics: str = "mpi", fused: bool = True, parts=None):
+        from .. import native
+
+        hf = native()
+        self.hf = hf
+        self.rank, self.world = rank, world
+        self.case = hf.Case.from_deck(deck_text, ".", False)
+        self.case.set_semantics(semantics)
+        solid = np.asarray(self.case.field("solid"))
+        self.parts = parts or balanced_columns(solid, world)
+        gi0, gi1 = self.parts[rank]
+        self.backend = backend
+        if backend == "gpu":
+            self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
+            self.solver.fused = fused
+            if world > 1:
+                import torch.distributed as dist
+
+                obj = [hf.DeviceSolver.nccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                self.solver.init_comm(obj[0], rank, world)
+        elif backend == "cpu":
+            self.solver = hf.CpuSolver(self.case, gi0, gi1)
+            if world > 1:
+                self._wire_cpu()
+        else:
+            raise ValueError(backend)
+
+    # -- gloo wiring for the CPU stepper ------------------------------------
+    def _wire_cpu(self):
+        import torch
+        import torch.distributed as dist
+
+        s = self.solver
+        rank, world = self.rank, self.world
+        left, right = rank - 1, rank + 1
+
+        def exchange(solver, group):
+            n_loc = solver.local_nx
+            first = solver.l_off
+            last = solver.l_off + (solver.gi1 - solver.gi0) - 1
+            ops = []
+            bufs = {}
+            if left >= 0:
+                snd = torch.from_numpy(np.ascontiguousarray(solver.pack_column(group, first)))
+                rcv = torch.empty_like(snd)
+                ops += [dist.P2POp(dist.isend, snd, left), dist.P2POp(dist.irecv, rcv, left)]
+                bufs["l"] = rcv
+            if right < world:
+                snd = torch.from_numpy(np.ascontiguousarray(solver.pack_column(group, last)))
+                rcv = torch.empty_like(snd)
+                ops += [dist.P2POp(dist.isend, snd, right), dist.P2POp(dist.irecv, rcv, right)]
+                bufs["r"] = rcv
+            if ops:
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+            if "l" in bufs:
+                solver.unpack_column(group, 0, bufs["l"].numpy())
+            if "r" in bufs:
+                solver.unpack_column(group, n_loc - 1, bufs["r"].numpy())
+
+        def fmin(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return float(t.item())
+
+        def fsum(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return float(t.item())
+
+        def fmaxi(v):
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return int(t.item())
+
+        def fres(b):
+            arr = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            out = [torch.empty_like(arr) for _ in range(world)]
+            dist.all_gather(out, arr)
+            return b"".join(bytes(o.numpy().tobytes()) for o in out)
+
+        s.set_exchange(exchange)
+        s.set_comm(rank, world, fmin, fsum, fmaxi, fres)
+
+    def step(self, n: int, residual: bool = False):
+        self.solver.run_steps(int(n), bool(residual))
+
+    def summary(self):
+        return dict(self.solver.summary())
+
+    def gather_field(self, name: str) -> np.ndarray:
+        """Full (nx, ny) field on every rank (for tests/outputs)."""
+        self.solver.download()
+        f = np.asarray(self.case.field(name))
+        if self.world == 1:
+            return f
+        import torch
+        import torch.distributed as dist
+
+        gi0, gi1 = self.parts[self.rank]
+        mine = np.zeros_like(f)
+        mine[gi0:gi1] = f[gi0:gi1]
+        t = torch.from_numpy(mine)
+        if self.backend == "gpu" and dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t)
+        return t.cpu().numpy()
