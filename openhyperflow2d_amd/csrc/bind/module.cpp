@@ -221,6 +221,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("last_iter", &SolverBase::last_iter);
 
   py::class_<CpuSolver, SolverBase>(m, "CpuSolver")
+      .def_readwrite("lean", &CpuSolver::lean)
+      .def_readonly("lean_ok", &CpuSolver::lean_ok)
+      .def_readonly("lean_why", &CpuSolver::lean_why)
       .def(py::init<Case&, int, int>(), py::arg("case"), py::arg("gi0") = 0, py::arg("gi1") = -1,
            py::keep_alive<1, 2>())
       .def_readonly("gi0", &CpuSolver::gi0)
@@ -262,6 +265,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("init_comm", [](DeviceSolver& s, py::bytes uid, int r, int n) { s.init_comm(std::string(uid), r, n); })
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("fused", &DeviceSolver::fused)
+      .def_readwrite("lean", &DeviceSolver::lean)
+      .def_readonly("lean_ok", &DeviceSolver::lean_ok)
+      .def_readonly("lean_why", &DeviceSolver::lean_why)
       .def_readonly("gi0", &DeviceSolver::gi0)
       .def_readonly("gi1", &DeviceSolver::gi1)
       .def_property_readonly("stream", [](const DeviceSolver& s) { return (uintptr_t)s.stream(); });

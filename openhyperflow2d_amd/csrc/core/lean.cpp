@@ -1,0 +1,68 @@
+// Host side of the lean inviscid path (lean_euler.hpp): eligibility and the
+// per-cell neighbour/publish byte.
+#include <string>
+#include <vector>
+
+#include "lean_euler.hpp"
+#include "solver.hpp"
+
+namespace hf2d {
+
+bool lean_eligible(const Case& cs, std::string* why) {
+  auto no = [&](const char* w) {
+    if (why) *why = w;
+    return false;
+  };
+  const Config& C = cs.cfg;
+  if (C.ProblemType == SM_NS) return no("viscous problem");
+  if (!C.sources.empty()) return no("gas sources");
+  if (!C.isAdiabaticWall) return no("wall heat transfer");
+  for (const CellRecord& c : cs.J.c) {
+    if (c.is(CT_SOLID)) continue;
+    if (!c.is(CT_NODE_IS_SET)) return no("unset non-solid node");
+    // equations >= 4 + NCOMP are frozen for inviscid nodes: their Src/SrcAdd
+    // (e.g. left by a k-eps initialisation) are never read
+    for (int k = 0; k < 4 + NCOMP; k++)
+      if (c.Src[k] != 0.) return no("non-zero Src");
+    if (!c.is(CT_WALL_NO_SLIP))
+      for (int k = 0; k < 4 + NCOMP; k++)
+        if (c.SrcAdd[k] != 0.) return no("non-zero SrcAdd off no-slip walls");
+  }
+  if (why) why->clear();
+  return true;
+}
+
+std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {
+  const long N = h.N;
+  const int ny = h.ny;
+  std::vector<uint8_t> lb(N);
+  for (long idx = 0; idx < N; idx++) lb[idx] = h.nb[idx] & (NB_XL | NB_XR | NB_YU | NB_YD);
+  // a node whose predictor applies d2S/dx2 = 0 reads dS/dx of its x
+  // neighbours (likewise y): those neighbours must keep publishing dS/dx.
+  for (int i = 0; i < h.nx; i++)
+    for (int j = 0; j < ny; j++) {
+      const long idx = (long)i * ny + j;
+      const u64 CT = h.CT[idx];
+      if (!is_active(CT)) continue;
+      bool dx2 = false, dy2 = false;
+      for (int k = 0; k < NEQ; k++) {
+        const EqFlags f = eq_flags(k, CT, h.TT[idx], sm);
+        dx2 = dx2 || f.dx2;
+        dy2 = dy2 || f.dy2;
+      }
+      const uint8_t nbm = h.nb[idx];
+      const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+      const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+      if (dx2) {
+        if (i - n1 >= 0) lb[(long)(i - n1) * ny + j] |= LB_DX_OUT;
+        if (i + n2 < h.nx) lb[(long)(i + n2) * ny + j] |= LB_DX_OUT;
+      }
+      if (dy2) {
+        lb[idx + n3] |= LB_DY_OUT;
+        lb[idx - n4] |= LB_DY_OUT;
+      }
+    }
+  return lb;
+}
+
+}  // namespace hf2d

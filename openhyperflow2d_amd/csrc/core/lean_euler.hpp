@@ -1,0 +1,326 @@
+// Lean inviscid step: predictor + FillNode2D + chemistry of one cell in a
+// single pass, with the neighbour fluxes recomputed from their state instead
+// of loaded.
+//
+// The generic Jacobi stepper (stepkern.hpp) keeps the reference's per-node
+// record alive in SoA form: A, B, F, Src, SrcAdd, p, k, R, CP, Tg, ... are
+// re-read and re-written every step (~2 KB of HBM traffic per cell-step).
+// For an inviscid case without gas sources the inviscid fluxes of a node
+// (FillNode2D flux block, reference libFlow FlowNode2D.hpp FillNode2D) are a
+// pure function of
+//   S[0..3] (committed), the pre-chemistry species S[4..6] and U, V, p
+// of that node's last fill, so the persistent per-cell state shrinks to
+//   S (7), Spre (3), beta (7), U, V, p, CP, R  (+ Y, Tg, k written for output)
+// plus dS/dx, dS/dy on the few nodes a Cauchy (d2/dx2 = 0) neighbour reads.
+// Every value is produced by the same expressions as fill_node(),
+// chemistry_zeldovich() and predict_core(), so the lean path equals the
+// generic stepper bit for bit.  The device solver switches freely between
+// the two: the first lean step after a generic one reads the generic A/B/F
+// (FROM_GENERIC), and lean_materialize_cell() rebuilds A/B/F/p before any
+// generic step.
+//
+// Eligibility (lean_eligible() on the host): inviscid, no gas sources,
+// adiabatic walls, Src == 0 everywhere, SrcAdd == 0 except on no-slip nodes
+// (whose SrcAdd lives in its array), every non-solid node set.
+#pragma once
+
+#include "stepkern.hpp"
+
+namespace hf2d {
+
+// per-cell lean byte: neighbour bits (NB_*) | who must publish dS/dx, dS/dy
+enum : uint8_t { LB_DX_OUT = 16, LB_DY_OUT = 32 };
+
+struct LeanSoA {
+  long N = 0;
+  const real* Sin;     // [NEQ*N] committed state (equations 0..6 used)
+  real* Sout;
+  const real* Pin_s;   // [NCOMP*N] pre-chemistry species of the last fill
+  real* Pout_s;
+  real* beta;          // in place
+  const real* Uin;
+  const real* Vin;
+  const real* Pin;     // pressure (FROM_GENERIC: the generic p array)
+  real* Uout;
+  real* Vout;
+  real* Pout;
+  real* Tout;          // Tg of this fill (output only for Euler)
+  const real* dSdx_in;
+  const real* dSdy_in;
+  real* dSdx_out;
+  real* dSdy_out;
+  const u64* CT;
+  const uint8_t* lb;
+  real* CP;            // in place (chemistry)
+  real* R;             // in place (chemistry)
+  real* kk;            // written (output)
+  real* Y;             // [NSPEC*N] in place
+  const real* Tf;
+  const real* BGX;
+  const real* BGY;
+  real* SrcAdd;        // no-slip nodes only
+  // FROM_GENERIC: the previous step was generic; use its flux arrays
+  const real* gA;
+  const real* gB;
+  const real* gF;
+};
+
+// Inviscid fluxes of equation k at node `at` (fill_node's A/B assembly);
+// species use the pre-chemistry partial densities.
+HF_HD inline real lean_flux_A(const LeanSoA& L, int k, long at, real u, real p) {
+  const long N = L.N;
+  switch (k) {
+    case I_RHO: return L.Sin[N + at];
+    case I_RHOU: return p + L.Sin[N + at] * u;
+    case I_RHOV: return L.Sin[2 * N + at] * u;
+    case I_RHOE: return (L.Sin[3 * N + at] + p) * u;
+    default: return L.Pin_s[(k - 4) * N + at] * u;
+  }
+}
+HF_HD inline real lean_flux_B(const LeanSoA& L, int k, long at, real u, real v, real p) {
+  const long N = L.N;
+  switch (k) {
+    case I_RHO: return L.Sin[2 * N + at];
+    case I_RHOU: return L.Sin[2 * N + at] * u;
+    case I_RHOV: return p + L.Sin[2 * N + at] * v;
+    case I_RHOE: return (L.Sin[3 * N + at] + p) * v;
+    default: return L.Pin_s[(k - 4) * N + at] * v;
+  }
+}
+
+template <bool FROMG>
+struct LeanIO {
+  static constexpr int NE = 4 + NCOMP;
+  const LeanSoA& L;
+  long N, idx, iL, iR, iU, iD;
+  uint8_t lb;
+  bool noslip;
+  real FT;
+  real uL, pL, uR, pR, uU, vU, pU, uD, vD, pD, u0, v0, p0;
+  real sm[NEQ];
+
+  HF_HD real S(int k) const { return L.Sin[k * N + idx]; }
+  HF_HD real SL(int k) const { return L.Sin[k * N + iL]; }
+  HF_HD real SR(int k) const { return L.Sin[k * N + iR]; }
+  HF_HD real SU(int k) const { return L.Sin[k * N + iU]; }
+  HF_HD real SD(int k) const { return L.Sin[k * N + iD]; }
+  HF_HD real AL(int k) const { return FROMG ? L.gA[k * N + iL] : lean_flux_A(L, k, iL, uL, pL); }
+  HF_HD real AR(int k) const { return FROMG ? L.gA[k * N + iR] : lean_flux_A(L, k, iR, uR, pR); }
+  HF_HD real BU(int k) const { return FROMG ? L.gB[k * N + iU] : lean_flux_B(L, k, iU, uU, vU, pU); }
+  HF_HD real BD(int k) const { return FROMG ? L.gB[k * N + iD] : lean_flux_B(L, k, iD, uD, vD, pD); }
+  HF_HD real dxL(int k) const { return L.dSdx_in[k * N + iL]; }
+  HF_HD real dxR(int k) const { return L.dSdx_in[k * N + iR]; }
+  HF_HD real dyU(int k) const { return L.dSdy_in[k * N + iU]; }
+  HF_HD real dyD(int k) const { return L.dSdy_in[k * N + iD]; }
+  HF_HD real beta(int k) const { return L.beta[k * N + idx]; }
+  // axisymmetric source of the node's own previous fill (fill_node F block)
+  HF_HD real F(int k) const {
+    if (FROMG) return L.gF[k * N + idx];
+    switch (k) {
+      case I_RHO: return FT * L.Sin[2 * N + idx];
+      case I_RHOU: return FT * (L.Sin[2 * N + idx] * u0);
+      case I_RHOV: return FT * (FT * L.Sin[2 * N + idx]) * v0;
+      case I_RHOE: return FT * ((L.Sin[3 * N + idx] + p0) * v0);
+      default: return FT * (L.Pin_s[(k - 4) * N + idx] * v0);
+    }
+  }
+  HF_HD real Src(int) const { return 0.0; }
+  HF_HD real SrcAdd(int k) const { return noslip ? L.SrcAdd[k * N + idx] : 0.0; }
+  HF_HD void put_S(int k, real v) { sm[k] = v; }
+  HF_HD void put_beta(int k, real v) const { L.beta[k * N + idx] = v; }
+  HF_HD void put_dS(int k, real a, real b) const {
+    if (lb & LB_DX_OUT) L.dSdx_out[k * N + idx] = a;
+    if (lb & LB_DY_OUT) L.dSdy_out[k * N + idx] = b;
+  }
+  HF_HD void keep_dS(int k) const {
+    if (lb & LB_DX_OUT) L.dSdx_out[k * N + idx] = L.dSdx_in[k * N + idx];
+    if (lb & LB_DY_OUT) L.dSdy_out[k * N + idx] = L.dSdy_in[k * N + idx];
+  }
+};
+
+// Node as seen by chemistry_zeldovich().
+struct LeanChemNode {
+  real S[NEQ];
+  real Tg, Tf, R, CP, lam, mu;
+  real Y[NSPEC];
+  u64 CT;
+};
+
+// One lean step of cell (i, j).  Returns the local dt limit (1.0 if none).
+template <bool FROMG>
+HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, int j, ResidualPack* res,
+                                  int* neg_T) {
+  const long N = L.N;
+  const long idx = (long)i * P.ny + j;
+  const u64 CT = L.CT[idx];
+  const uint8_t lb = L.lb[idx];
+  constexpr int NE = 4 + NCOMP;
+  if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
+    // neither transported nor filled: carry the state into the other buffers
+    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = L.Sin[k * N + idx];
+    if (lb & LB_DX_OUT)
+      for (int k = 0; k < NEQ; k++) L.dSdx_out[k * N + idx] = L.dSdx_in[k * N + idx];
+    if (lb & LB_DY_OUT)
+      for (int k = 0; k < NEQ; k++) L.dSdy_out[k * N + idx] = L.dSdy_in[k * N + idx];
+    return 1.0;
+  }
+  const bool active = !has_all(CT, NT_FC);
+  const bool noslip = has_all(CT, CT_WALL_NO_SLIP);
+  const real u_old = L.Uin[idx], v_old = L.Vin[idx];
+  LeanIO<FROMG> io{L, N, idx, idx, idx, idx, idx, lb, noslip, (real)P.fpa.FT};
+  io.u0 = u_old;
+  io.v0 = v_old;
+  io.p0 = L.Pin[idx];
+  if (active) {
+    const int n1 = (lb & NB_XL) ? 1 : 0, n2 = (lb & NB_XR) ? 1 : 0;
+    const int n3 = (lb & NB_YU) ? 1 : 0, n4 = (lb & NB_YD) ? 1 : 0;
+    io.iL = (long)(i - n1) * P.ny + j;
+    io.iR = (long)(i + n2) * P.ny + j;
+    io.iU = idx + n3;
+    io.iD = idx - n4;
+    if (!FROMG) {
+      io.uL = L.Uin[io.iL];
+      io.pL = L.Pin[io.iL];
+      io.uR = L.Uin[io.iR];
+      io.pR = L.Pin[io.iR];
+      io.uU = L.Uin[io.iU];
+      io.vU = L.Vin[io.iU];
+      io.pU = L.Pin[io.iU];
+      io.uD = L.Uin[io.iD];
+      io.vD = L.Vin[io.iD];
+      io.pD = L.Pin[io.iD];
+    }
+    // Equations >= NE are frozen for inviscid cells: TurbType only matters
+    // through num_eq_for(), which is >= NE for every model.
+    predict_core(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
+    if (lb & (LB_DX_OUT | LB_DY_OUT))
+      for (int k = NE; k < NEQ; k++) io.keep_dS(k);
+  } else {
+    for (int k = 0; k < NE; k++) io.sm[k] = L.Sin[k * N + idx];
+    for (int k = 0; k < NEQ; k++) io.keep_dS(k);
+  }
+
+  // ---- FillNode2D, inviscid subset (fill_node) ----
+  LeanChemNode c;
+  for (int k = 0; k < NE; k++) c.S[k] = io.sm[k];
+  c.S[NE] = c.S[NE + 1] = 0.;
+  real* s = c.S;
+  const FillParams& F = active ? P.fpa : P.ffc;
+  c.R = L.R[idx];
+  c.CP = L.CP[idx];
+  const real k_old = L.kk[idx];
+  if (s[I_RHO] == 0 || k_old < 1) {
+    // fill_node() skipped the node: keep the previous primitives
+    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = s[k];
+    for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
+    L.Uout[idx] = u_old;
+    L.Vout[idx] = v_old;
+    L.Pout[idx] = io.p0;
+    return 1.0;
+  }
+  const real kk = c.CP / (c.CP - c.R);
+  real U, V;
+  if (has_all(CT, CT_U_CONST)) {
+    U = u_old;
+    s[I_RHOU] = U * s[I_RHO];
+  } else {
+    U = s[I_RHOU] / s[I_RHO];
+  }
+  if (has_all(CT, CT_V_CONST)) {
+    V = v_old;
+    s[I_RHOV] = V * s[I_RHO];
+  } else {
+    V = s[I_RHOV] / s[I_RHO];
+  }
+  real Tmp1 = s[I_RHO], Tmp3 = 0.;
+  for (int q = 0; q < NCOMP; q++) {
+    Tmp3 += F.Hu[q] * s[q + 4];
+    Tmp1 -= s[q + 4];
+  }
+  Tmp3 += F.Hu[NCOMP] * Tmp1;
+  if (has_all(CT, CT_WALL_LAW)) {
+    Tmp1 = std::sqrt(U * U + V * V + 1.e-30);
+    s[I_RHOU] = Tmp1 * L.BGX[idx];
+    s[I_RHOV] = Tmp1 * L.BGY[idx];
+    U = s[I_RHOU] / s[I_RHO];
+    V = s[I_RHOV] / s[I_RHO];
+  } else if (noslip) {
+    U = s[I_RHOU] / s[I_RHO];
+    V = s[I_RHOV] / s[I_RHO];
+    real* sa = L.SrcAdd;
+    const real Uw = 0.0, Vw = 0.0;
+    if (F.isSrcAdd) {
+      const real bgx = L.BGX[idx], bgy = L.BGY[idx];
+      sa[I_RHO * N + idx] = bgx * (U - Uw) * s[I_RHO] / F.dx + bgy * (V - Vw) * s[I_RHO] / F.dy;
+      sa[I_RHOU * N + idx] = bgx * (U - Uw) * s[I_RHO];
+      sa[I_RHOV * N + idx] = bgy * (V - Vw) * s[I_RHO];
+      sa[I_RHOE * N + idx] = 0.;
+    } else {
+      sa[I_RHOU * N + idx] = sa[I_RHOV * N + idx] = sa[I_RHOE * N + idx] = 0.;
+    }
+    U = Uw;
+    V = Vw;
+    for (int q = 0; q < NCOMP; q++)
+      sa[(4 + q) * N + idx] = F.isSrcAdd ? sa[I_RHO * N + idx] * L.Y[q * N + idx] : 0.;
+    s[I_RHOU] = U * s[I_RHO];
+    s[I_RHOV] = V * s[I_RHO];
+  }
+  const real p = (kk - 1.) * (s[I_RHOE] - s[I_RHO] * (U * U + V * V) * 0.5 - Tmp3);
+  const real Tg = p / c.R / s[I_RHO];
+  // fluxes of this fill are built from the pre-chemistry species
+  for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
+  real dt_local = 1.0;
+  if (active) {
+    if (Tg < 0.) {
+      if (neg_T) *neg_T = 1;
+    } else {
+      const real AAA = std::sqrt(kk * c.R * Tg);
+      dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(U)), P.dy / (AAA + std::fabs(V)));
+      if (P.chem_model != NO_REACTIONS) {
+        c.Tg = Tg;
+        c.Tf = L.Tf[idx];
+        c.CT = CT;
+        c.lam = c.mu = 0.;
+        chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
+        L.R[idx] = c.R;
+        L.CP[idx] = c.CP;
+        for (int q = 0; q < NSPEC; q++) L.Y[q * N + idx] = c.Y[q];
+      }
+    }
+  }
+  for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = s[k];
+  L.Uout[idx] = U;
+  L.Vout[idx] = V;
+  L.Pout[idx] = p;
+  L.Tout[idx] = Tg;
+  L.kk[idx] = kk;
+  return dt_local;
+}
+
+// Rebuild the generic per-node fluxes (A, B, F) and p from the lean state,
+// exactly as the last fill produced them.
+HF_HD inline void lean_materialize_cell(const StepParams& P, const LeanSoA& L, const SoA& g, int i, int j) {
+  const long N = L.N;
+  const long idx = (long)i * P.ny + j;
+  const u64 CT = L.CT[idx];
+  if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) return;
+  const real U = L.Uin[idx], V = L.Vin[idx], p = L.Pin[idx];
+  g.p[idx] = p;
+  if (L.Sin[idx] == 0) return;
+  constexpr int NE = 4 + NCOMP;
+  for (int k = 0; k < NE; k++) {
+    g.A[k * N + idx] = lean_flux_A(L, k, idx, U, p);
+    g.B[k * N + idx] = lean_flux_B(L, k, idx, U, V, p);
+  }
+  if (P.fpa.FT == FT_AXISYMMETRIC) {
+    const real FT = (real)P.fpa.FT;
+    const real F0 = FT * L.Sin[2 * N + idx];
+    g.F[idx] = F0;
+    g.F[N + idx] = FT * (L.Sin[2 * N + idx] * U);
+    g.F[2 * N + idx] = FT * F0 * V;
+    g.F[3 * N + idx] = FT * ((L.Sin[3 * N + idx] + p) * V);
+    for (int k = 4; k < NE; k++) g.F[k * N + idx] = FT * (L.Pin_s[(k - 4) * N + idx] * V);
+  }
+}
+
+}  // namespace hf2d

@@ -428,15 +428,72 @@ void CpuSolver::upload() {
   sbuf = 0;
   dsbuf = 0;
   pbuf = 0;
+  lean_ok = lean_eligible(cs, &lean_why);
+  lean_state = 0;
+  if (lean_ok) {
+    lb = lean_flags(h, cs.cfg.ProblemType);
+    for (int b = 0; b < 2; b++) {
+      Spre[b].assign(NCOMP * h.N, 0.0);
+      P2[b].assign(h.N, 0.0);
+    }
+  }
 }
 
 void CpuSolver::download(Field& J) {
+  if (lean_state) lean_materialize();
   h.to_field(J, gi0 - l_off, l_off, l_off + (gi1 - gi0), pbuf, dsbuf);
+}
+
+LeanSoA CpuSolver::lean_view(bool fromg) {
+  LeanSoA L;
+  L.N = h.N;
+  L.Sin = h.S[0].data();
+  L.Sout = h.S[1].data();
+  L.Pin_s = Spre[pbuf].data();
+  L.Pout_s = Spre[1 - pbuf].data();
+  L.beta = h.beta.data();
+  L.Uin = h.U[pbuf].data();
+  L.Vin = h.V[pbuf].data();
+  L.Pin = fromg ? h.p.data() : P2[pbuf].data();
+  L.Uout = h.U[1 - pbuf].data();
+  L.Vout = h.V[1 - pbuf].data();
+  L.Pout = P2[1 - pbuf].data();
+  L.Tout = h.Tg[1 - pbuf].data();
+  L.dSdx_in = h.dSdx[dsbuf].data();
+  L.dSdy_in = h.dSdy[dsbuf].data();
+  L.dSdx_out = h.dSdx[1 - dsbuf].data();
+  L.dSdy_out = h.dSdy[1 - dsbuf].data();
+  L.CT = h.CT.data();
+  L.lb = lb.data();
+  L.CP = h.CP.data();
+  L.R = h.R.data();
+  L.kk = h.kk.data();
+  L.Y = h.Y.data();
+  L.Tf = h.Tf.data();
+  L.BGX = h.BGX.data();
+  L.BGY = h.BGY.data();
+  L.SrcAdd = h.SrcAdd.data();
+  L.gA = h.A.data();
+  L.gB = h.B.data();
+  L.gF = h.F.data();
+  return L;
+}
+
+void CpuSolver::lean_materialize() {
+  StepParams P = make_params(last_iter + iter);
+  P.nx = h.nx;
+  P.ny = h.ny;
+  LeanSoA L = lean_view(false);
+  SoA g = h.view(0, dsbuf, pbuf);
+  for (int i = 0; i < h.nx; i++)
+    for (int j = 0; j < h.ny; j++) lean_materialize_cell(P, L, g, i, j);
+  lean_state = 0;
 }
 
 int CpuSolver::halo_doubles(int g) const {
   if (g == HALO_MID) return NEQ;
   if (g == HALO_QDIR) return 4;
+  if (g == HALO_LEAN) return 4 + 2 * NCOMP + 3 + NEQ;
   return 4 * NEQ + 5;
 }
 
@@ -449,6 +506,13 @@ void CpuSolver::pack_column(int g, int li, real* o) const {
       for (int k = 0; k < NEQ; k++) *o++ = h.S[1][k * N + idx];
     } else if (g == HALO_QDIR) {
       for (int d = 0; d < 4; d++) *o++ = h.qdir[d * N + idx];
+    } else if (g == HALO_LEAN) {
+      for (int k = 0; k < 4 + NCOMP; k++) *o++ = h.S[0][k * N + idx];
+      for (int k = 0; k < NCOMP; k++) *o++ = Spre[pbuf][k * N + idx];
+      *o++ = h.U[pbuf][idx];
+      *o++ = h.V[pbuf][idx];
+      *o++ = P2[pbuf][idx];
+      for (int k = 0; k < NEQ; k++) *o++ = h.dSdx[dsbuf][k * N + idx];
     } else {
       for (int k = 0; k < NEQ; k++) {
         *o++ = h.S[0][k * N + idx];
@@ -474,6 +538,13 @@ void CpuSolver::unpack_column(int g, int li, const real* o) {
       for (int k = 0; k < NEQ; k++) h.S[1][k * N + idx] = *o++;
     } else if (g == HALO_QDIR) {
       for (int d = 0; d < 4; d++) h.qdir[d * N + idx] = *o++;
+    } else if (g == HALO_LEAN) {
+      for (int k = 0; k < 4 + NCOMP; k++) h.S[0][k * N + idx] = *o++;
+      for (int k = 0; k < NCOMP; k++) Spre[pbuf][k * N + idx] = *o++;
+      h.U[pbuf][idx] = *o++;
+      h.V[pbuf][idx] = *o++;
+      P2[pbuf][idx] = *o++;
+      for (int k = 0; k < NEQ; k++) h.dSdx[dsbuf][k * N + idx] = *o++;
     } else {
       for (int k = 0; k < NEQ; k++) {
         h.S[0][k * N + idx] = *o++;
@@ -500,6 +571,36 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
   P.do_residual = want_res ? 1 : 0;
   StepResult r;
   residual_reset(r.res);
+  if (lean && lean_ok) {
+    // lean inviscid step: S[0] -> S[1] (swapped back), prims/dS ping-pong
+    const bool fromg = lean_state == 0;
+    if (fromg) h.S[1] = h.S[0];
+    LeanSoA L = lean_view(fromg);
+    int negT = 0;
+    real dtmin = 1.0;
+    ResidualPack* rp = want_res ? &r.res : nullptr;
+    for (int i = P.i0; i < P.i1; i++)
+      for (int j = 0; j < P.ny; j++) {
+        const real d = fromg ? lean_euler_cell<true>(P, L, i, j, rp, &negT) : lean_euler_cell<false>(P, L, i, j, rp, &negT);
+        dtmin = std::min(dtmin, d);
+      }
+    // halo columns keep their exchanged values
+    for (int i = 0; i < h.nx; i++) {
+      if (i >= P.i0 && i < P.i1) continue;
+      for (int k = 0; k < 4 + NCOMP; k++)
+        for (int j = 0; j < P.ny; j++) h.S[1][k * h.N + (long)i * P.ny + j] = h.S[0][k * h.N + (long)i * P.ny + j];
+    }
+    h.S[0].swap(h.S[1]);
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+    lean_state = 1;
+    r.have_residual = want_res;
+    r.dt_min = dtmin;
+    r.neg_T = negT;
+    if (halo_exchange) halo_exchange(*this, HALO_LEAN);
+    return r;
+  }
+  if (lean_state) lean_materialize();
   // predict: S[0] -> S[1], dS[dsbuf] -> dS[1-dsbuf]
   SoA in = h.view(0, dsbuf, pbuf);
   SoA mid = h.view(1, 1 - dsbuf, pbuf);

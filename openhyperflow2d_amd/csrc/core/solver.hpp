@@ -18,7 +18,7 @@
 
 #include "case.hpp"
 #include "residual.hpp"
-#include "stepkern.hpp"
+#include "lean_euler.hpp"
 
 namespace hf2d {
 
@@ -109,6 +109,10 @@ class SolverBase {
   bool isSrcAdd = false;
 };
 
+// lean inviscid path (lean.cpp)
+bool lean_eligible(const Case& cs, std::string* why);
+std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);
+
 class CpuSolver : public SolverBase {
  public:
   // Owns columns [gi0, gi1) of the global field; a halo column is added on
@@ -126,11 +130,23 @@ class CpuSolver : public SolverBase {
   // halo access for distributed runs: pack/unpack columns of the exchanged fields
   // groups: 0 = predicted state (N-S gradients), 1 = post-fill state,
   // 2 = wall-heat per-direction fluxes
-  enum { HALO_MID = 0, HALO_STATE = 1, HALO_QDIR = 2 };
+  // 3 = lean inviscid state (lean_euler.hpp)
+  enum { HALO_MID = 0, HALO_STATE = 1, HALO_QDIR = 2, HALO_LEAN = 3 };
   int halo_doubles(int group) const;
   void pack_column(int group, int local_i, real* buf) const;
   void unpack_column(int group, int local_i, const real* buf);
   std::function<void(CpuSolver&, int)> halo_exchange;
+
+  // lean inviscid path (off by default on the CPU: the generic stepper is the
+  // oracle the device kernels are checked against)
+  bool lean = false;
+  bool lean_ok = false;
+  std::string lean_why;
+  int lean_state = 0;   // 1: lean arrays authoritative, A/B/F/p stale
+  std::vector<real> Spre[2], P2[2];
+  std::vector<uint8_t> lb;
+  LeanSoA lean_view(bool fromg);
+  void lean_materialize();
 };
 
 class RefSolver : public SolverBase {

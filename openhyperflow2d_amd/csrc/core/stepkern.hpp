@@ -170,8 +170,156 @@ HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, rea
 }
 
 // ---------------------------------------------------------------------------
-// Pass 1 + pass 2a for one cell.  `res` (may be null) accumulates residuals.
+// Pass 1 + pass 2a for one active cell, written once against an accessor so
+// the generic SoA stepper and the lean Euler kernel (fluxes recomputed from
+// the neighbours' state instead of loaded) share the exact arithmetic.
+//
+// IO must provide (k = equation; L/R/U/D are the neighbour slots iL/iR/iU/iD,
+// which resolve to the cell itself when the neighbour is absent):
+//   S(k)  SL(k) SR(k) SU(k) SD(k)      conserved state
+//   AL(k) AR(k) BU(k) BD(k)            fluxes at the neighbour slots
+//   dxL(k) dxR(k) dyU(k) dyD(k)        previous dS/dx, dS/dy (Cauchy BCs)
+//   beta(k) F(k) Src(k) SrcAdd(k)
+//   put_S(k, v) put_beta(k, v) put_dS(k, dsdx, dsdy) keep_dS(k)
 // ---------------------------------------------------------------------------
+template <class IO>
+HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int n1, int n2, int n3, int n4, int gi,
+                               int j, ResidualPack* res) {
+  const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
+  const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+  const int Num_Eq = num_eq_for(TT);
+  const bool axi = P.fpa.FT != 0;
+#pragma unroll
+  for (int k = 0; k < IO::NE; k++) {
+    real s = io.S(k);
+    const EqFlags f = eq_flags(k, CT, TT, P.sm);
+    if (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT)))) {
+      // A TCT-frozen turbulence equation whose CT-based pass-2 test says
+      // "not frozen" (quirk Q4) is scored against the never-written
+      // predictor scratch (0) in the reference: DD = 1, dS = -S.
+      if (k < Num_Eq && !f.upd && k >= 4 + NCOMP && P.sm == SM_NS && has_turb_eq(TT) &&
+          !pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
+        const real beta = io.beta(k);
+        const real DD = 1.0;
+        const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+        io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, 1.0));
+        if (res) {
+          EqResidual& e = res->eq[k];
+          if (DD >= e.dd_max) {
+            e.dd_max = DD;
+            e.i = gi;
+            e.j = j;
+          }
+          if (P.alternate_rms) {
+            e.rms += s * s;
+            e.sum_div += s * s;
+          } else {
+            e.rms += DD * DD;
+            e.count += 1;
+          }
+        }
+      }
+      io.put_S(k, s);
+      io.keep_dS(k);
+      continue;
+    }
+    real dXX, dYY, dsdx, dsdy;
+    if (f.dx) {
+      dXX = dsdx = (io.AR(k) - io.AL(k)) * n_n_1;
+    } else {
+      // a missing neighbour resolves to the cell itself
+      const real sL = n1 ? io.SL(k) : s, sR = n2 ? io.SR(k) : s;
+      s = (sL * n2 + sR * n1) * n_n_1;
+      dXX = dsdx = 0.;
+    }
+    if (f.dy) {
+      dYY = dsdy = (io.BU(k) - io.BD(k)) * m_m_1;
+    } else {
+      const real sU = n3 ? io.SU(k) : s, sD = n4 ? io.SD(k) : s;
+      s = (sU * n3 + sD * n4) * m_m_1;
+      dYY = dsdy = 0.;
+    }
+    if (f.dx2) dXX = (io.dxL(k) + io.dxR(k)) * 0.5;
+    if (f.dy2) dYY = (io.dyU(k) + io.dyD(k)) * 0.5;
+    const real SL = n1 ? io.SL(k) : s, SR = n2 ? io.SR(k) : s;
+    const real SU = n3 ? io.SU(k) : s, SD = n4 ? io.SD(k) : s;
+    const real beta = io.beta(k);
+    const real _beta = 1. - beta;
+    real snew;
+    if (axi)
+      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 -
+             (P.dtdx * dXX + P.dtdy * (dYY + io.F(k) / (j + 1))) + (io.Src(k)) * P.dt + io.SrcAdd(k);
+    else
+      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 - (P.dtdx * dXX + P.dtdy * dYY) +
+             (io.Src(k)) * P.dt + io.SrcAdd(k);
+    io.put_dS(k, dsdx, dsdy);
+    // pass 2a: residual + blending factor
+    if (!pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
+      const real absDD = snew - s;
+      real DD, sqrt_res = 0;
+      if (std::fabs(s) > 1.e-15) {
+        DD = std::fabs(absDD / s);
+        sqrt_res = std::sqrt(DD);
+      } else {
+        DD = 1.0;
+      }
+      const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+      io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, sqrt_res));
+      if (res) {
+        EqResidual& e = res->eq[k];
+        if (DD >= e.dd_max) {
+          e.dd_max = DD;
+          e.i = gi;
+          e.j = j;
+        }
+        if (P.alternate_rms) {
+          e.rms += absDD * absDD;
+          e.sum_div += s * s;
+        } else {
+          e.rms += DD * DD;
+          e.count += 1;
+        }
+      }
+    }
+    io.put_S(k, snew);
+  }
+}
+
+// Accessor over the full SoA arrays (fluxes loaded).
+struct SoAPredictIO {
+  static constexpr int NE = NEQ;
+  const SoA& in;
+  const SoA& out;
+  long N, idx, iL, iR, iU, iD;
+  HF_HD real S(int k) const { return in.S[k * N + idx]; }
+  HF_HD real SL(int k) const { return in.S[k * N + iL]; }
+  HF_HD real SR(int k) const { return in.S[k * N + iR]; }
+  HF_HD real SU(int k) const { return in.S[k * N + iU]; }
+  HF_HD real SD(int k) const { return in.S[k * N + iD]; }
+  HF_HD real AL(int k) const { return in.A[k * N + iL]; }
+  HF_HD real AR(int k) const { return in.A[k * N + iR]; }
+  HF_HD real BU(int k) const { return in.B[k * N + iU]; }
+  HF_HD real BD(int k) const { return in.B[k * N + iD]; }
+  HF_HD real dxL(int k) const { return in.dSdx[k * N + iL]; }
+  HF_HD real dxR(int k) const { return in.dSdx[k * N + iR]; }
+  HF_HD real dyU(int k) const { return in.dSdy[k * N + iU]; }
+  HF_HD real dyD(int k) const { return in.dSdy[k * N + iD]; }
+  HF_HD real beta(int k) const { return in.beta[k * N + idx]; }
+  HF_HD real F(int k) const { return in.F[k * N + idx]; }
+  HF_HD real Src(int k) const { return in.Src[k * N + idx]; }
+  HF_HD real SrcAdd(int k) const { return in.SrcAdd[k * N + idx]; }
+  HF_HD void put_S(int k, real v) const { out.S[k * N + idx] = v; }
+  HF_HD void put_beta(int k, real v) const { out.beta[k * N + idx] = v; }
+  HF_HD void put_dS(int k, real a, real b) const {
+    out.dSdx[k * N + idx] = a;
+    out.dSdy[k * N + idx] = b;
+  }
+  HF_HD void keep_dS(int k) const {
+    out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
+    out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
+  }
+};
+
 HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
                                ResidualPack* res) {
   const long N = in.N;
@@ -189,109 +337,9 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
   const uint8_t nbm = in.nb[idx];
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-  const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j;
-  const long iU = idx + n3, iD = idx - n4;
-  const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
-  const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
-  const int Num_Eq = num_eq_for(TT);
-  const bool axi = P.fpa.FT != 0;
-  for (int k = 0; k < NEQ; k++) {
-    const long o = k * N;
-    real s = in.S[o + idx];
-    const EqFlags f = eq_flags(k, CT, TT, P.sm);
-    if (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT)))) {
-      // A TCT-frozen turbulence equation whose CT-based pass-2 test says
-      // "not frozen" (quirk Q4) is scored against the never-written
-      // predictor scratch (0) in the reference: DD = 1, dS = -S.
-      if (k < Num_Eq && !f.upd && k >= 4 + NCOMP && P.sm == SM_NS && has_turb_eq(TT) &&
-          !pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
-        const real beta = in.beta[o + idx];
-        const real DD = std::fabs(s) > 1.e-15 ? 1.0 : 1.0;
-        const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
-        out.beta[o + idx] = blend_beta(P.bff, bmin, beta, DD, 1.0);
-        if (res) {
-          EqResidual& e = res->eq[k];
-          if (DD >= e.dd_max) {
-            e.dd_max = DD;
-            e.i = P.gx0 + i;
-            e.j = j;
-          }
-          if (P.alternate_rms) {
-            e.rms += s * s;
-            e.sum_div += s * s;
-          } else {
-            e.rms += DD * DD;
-            e.count += 1;
-          }
-        }
-      }
-      out.S[o + idx] = s;
-      out.dSdx[o + idx] = in.dSdx[o + idx];
-      out.dSdy[o + idx] = in.dSdy[o + idx];
-      continue;
-    }
-    real dXX, dYY, dsdx, dsdy;
-    if (f.dx) {
-      dXX = dsdx = (in.A[o + iR] - in.A[o + iL]) * n_n_1;
-    } else {
-      // a missing neighbour resolves to the cell itself
-      const real sL = n1 ? in.S[o + iL] : s, sR = n2 ? in.S[o + iR] : s;
-      s = (sL * n2 + sR * n1) * n_n_1;
-      dXX = dsdx = 0.;
-    }
-    if (f.dy) {
-      dYY = dsdy = (in.B[o + iU] - in.B[o + iD]) * m_m_1;
-    } else {
-      const real sU = n3 ? in.S[o + iU] : s, sD = n4 ? in.S[o + iD] : s;
-      s = (sU * n3 + sD * n4) * m_m_1;
-      dYY = dsdy = 0.;
-    }
-    if (f.dx2) dXX = (in.dSdx[o + iL] + in.dSdx[o + iR]) * 0.5;
-    if (f.dy2) dYY = (in.dSdy[o + iU] + in.dSdy[o + iD]) * 0.5;
-    const real SL = n1 ? in.S[o + iL] : s, SR = n2 ? in.S[o + iR] : s;
-    const real SU = n3 ? in.S[o + iU] : s, SD = n4 ? in.S[o + iD] : s;
-    const real beta = in.beta[o + idx];
-    const real _beta = 1. - beta;
-    real snew;
-    if (axi)
-      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 -
-             (P.dtdx * dXX + P.dtdy * (dYY + in.F[o + idx] / (j + 1))) + (in.Src[o + idx]) * P.dt +
-             in.SrcAdd[o + idx];
-    else
-      snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 - (P.dtdx * dXX + P.dtdy * dYY) +
-             (in.Src[o + idx]) * P.dt + in.SrcAdd[o + idx];
-    out.dSdx[o + idx] = dsdx;
-    out.dSdy[o + idx] = dsdy;
-    // pass 2a: residual + blending factor
-    if (!pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
-      const real absDD = snew - s;
-      real DD, sqrt_res = 0;
-      if (std::fabs(s) > 1.e-15) {
-        DD = std::fabs(absDD / s);
-        sqrt_res = std::sqrt(DD);
-      } else {
-        DD = 1.0;
-      }
-      const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
-      out.beta[o + idx] = blend_beta(P.bff, bmin, beta, DD, sqrt_res);
-      if (res) {
-        EqResidual& e = res->eq[k];
-        if (DD >= e.dd_max) {
-          e.dd_max = DD;
-          e.i = P.gx0 + i;
-          e.j = j;
-        }
-        if (P.alternate_rms) {
-          e.rms += absDD * absDD;
-          e.sum_div += s * s;
-        } else {
-          e.rms += DD * DD;
-          e.count += 1;
-        }
-      }
-    }
-    out.S[o + idx] = snew;
-  }
+  SoAPredictIO io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4};
+  predict_core(P, io, CT, in.TT[idx], n1, n2, n3, n4, P.gx0 + i, j, res);
+  (void)TT;
 }
 
 // ---------------------------------------------------------------------------

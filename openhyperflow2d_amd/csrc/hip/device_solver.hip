@@ -6,6 +6,10 @@
 //   hf2d_predict<RES>     pass 1 + 2a (predictor, BC, residual, blending factor)
 //   hf2d_fill             pass 2b/2c (gradients, FillNode2D, dt, chemistry)
 //   hf2d_fused_euler      predict + fill in one sweep for Euler problems
+//   hf2d_lean_euler       inviscid step on the reduced state (lean_euler.hpp):
+//                         fluxes recomputed from neighbour state, ~1/5 the
+//                         HBM traffic of predict+fill
+//   hf2d_lean_materialize rebuild A/B/F/p from the lean state
 //   hf2d_wall_solid/_wall owner-computes wall heat sources (K5)
 //   hf2d_reduce_residual  deterministic tree over per-wave residual partials (K6)
 //   hf2d_pack/unpack      halo column packing (K7)
@@ -24,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "../core/lean_euler.hpp"
 #include "../core/solver.hpp"
 #include "device_solver.hpp"
 
@@ -57,6 +62,9 @@ struct DevScalars {
 
 __device__ inline double bits_to_d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ inline unsigned long long d_to_bits(double d) { return (unsigned long long)__double_as_longlong(d); }
+
+// Step n reads slot n%3, min-reduces into (n+1)%3 and resets (n+2)%3.
+__host__ __device__ inline int slot_reset(int slot) { return (slot + 2) % 3; }
 
 __device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
   const double dt = bits_to_d(sc->dt_bits[slot]);
@@ -100,8 +108,10 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
   apply_dt(P, sc, slot);
   const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
   if (g == 0) {
-    // reset the next dt slot and accumulate physical time
-    sc->dt_bits[slot_next] = serial ? sc->dt_bits[slot] : d_to_bits(1.0);
+    // Reset the slot the NEXT step will accumulate into (never the one this
+    // step's fill is min-reducing, which other blocks may already be
+    // writing) and accumulate physical time.
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
   }
   const long c = c0 + g;
@@ -139,7 +149,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
 }
 
 __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
-                                                    DevScalars* sc, int slot, int slot_next) {
+                                                    DevScalars* sc, int slot, int slot_next, int serial) {
   apply_dt(P, sc, slot);
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   double dtl = 1.0;
@@ -156,6 +166,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA po
   if (threadIdx.x == 0) {
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
   }
 }
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   apply_dt(P, sc, slot);
   const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
   if (g == 0) {
-    sc->dt_bits[slot_next] = serial ? sc->dt_bits[slot] : d_to_bits(1.0);
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
   }
   const long c = c0 + g;
@@ -198,8 +209,66 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   if (threadIdx.x == 0) {
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
   }
+}
+
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2).  Remap so XCD x owns a contiguous run of tiles: the i+-1 neighbour
+// columns a tile reads then sit in the same L2.  Bijective on [0, n).
+constexpr unsigned NUM_XCD = 8;
+__device__ inline unsigned xcd_remap(unsigned b, unsigned n) {
+  const unsigned q = n / NUM_XCD;
+  if (b >= q * NUM_XCD) return b;
+  return (b % NUM_XCD) * q + b / NUM_XCD;
+}
+
+template <bool RES, bool FROMG>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L, long c0, long c1, DevScalars* sc,
+                                                          int slot, int slot_next, int serial,
+                                                          ResidualPack* partials) {
+  apply_dt(P, sc, slot);
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  const long g = (long)b * BLOCK + threadIdx.x;
+  if (g == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += P.dt;
+  }
+  const long c = c0 + g;
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  if (c < c1) {
+    const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+    dtl = lean_euler_cell<FROMG>(P, L, i, j, RES ? &r : nullptr, &neg);
+  }
+  if (RES) {
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, LeanSoA L, SoA g, long c0, long c1) {
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= c1) return;
+  const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+  lean_materialize_cell(P, L, g, i, j);
 }
 
 __global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
@@ -270,6 +339,10 @@ struct DeviceSolver::Impl {
   real *l_min, *y_plus, *Re_local, *BGX, *BGY, *Tf, *Q_conv, *grad, *qdir;
   u64 *CT, *TT;
   uint8_t* nb;
+  // lean inviscid state: pre-chemistry species and pressure (ping-pong with
+  // U/V on pbuf), per-cell neighbour/publish byte
+  real *Spre[2], *P2[2];
+  uint8_t* lb;
   int32_t *iw, *jw;
   SpeciesProps* species = nullptr;
   DevScalars* sc = nullptr;
@@ -283,6 +356,41 @@ struct DeviceSolver::Impl {
   long halo_cap = 0;
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+
+  LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
+    LeanSoA L;
+    L.N = h.N;
+    L.Sin = S[sb];
+    L.Sout = S[1 - sb];
+    L.Pin_s = Spre[pb];
+    L.Pout_s = Spre[1 - pb];
+    L.beta = beta;
+    L.Uin = U[pb];
+    L.Vin = V[pb];
+    L.Pin = fromg ? p : P2[pb];
+    L.Uout = U[1 - pb];
+    L.Vout = V[1 - pb];
+    L.Pout = P2[1 - pb];
+    L.Tout = Tg[1 - pb];
+    L.dSdx_in = dSdx[db];
+    L.dSdy_in = dSdy[db];
+    L.dSdx_out = dSdx[1 - db];
+    L.dSdy_out = dSdy[1 - db];
+    L.CT = CT;
+    L.lb = lb;
+    L.CP = CP;
+    L.R = R;
+    L.kk = kk;
+    L.Y = Y;
+    L.Tf = Tf;
+    L.BGX = BGX;
+    L.BGY = BGY;
+    L.SrcAdd = SrcAdd;
+    L.gA = A[ab];
+    L.gB = B[ab];
+    L.gF = F;
+    return L;
+  }
 
   SoA view(const HostArrays& h, int sb, int ab, int db, int pb) const {
     SoA s;
@@ -360,7 +468,10 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     m.U[b] = m.mem.alloc<real>(N);
     m.V[b] = m.mem.alloc<real>(N);
     m.Tg[b] = m.mem.alloc<real>(N);
+    m.Spre[b] = m.mem.alloc<real>(NCOMP * N);
+    m.P2[b] = m.mem.alloc<real>(N);
   }
+  m.lb = m.mem.alloc<uint8_t>(N);
   m.F = m.mem.alloc<real>(NEQ * N);
   m.Src = m.mem.alloc<real>(NEQ * N);
   m.SrcAdd = m.mem.alloc<real>(NEQ * N);
@@ -459,13 +570,21 @@ void DeviceSolver::upload() {
   cp(m.CT, h.CT.data(), N * sizeof(u64));
   cp(m.TT, h.TT.data(), N * sizeof(u64));
   cp(m.nb, h.nb.data(), N);
+  lean_ok = lean_eligible(cs, &lean_why);
+  if (lean_ok) {
+    lean_bytes = lean_flags(h, cs.cfg.ProblemType);
+    cp(m.lb, lean_bytes.data(), N);
+  }
+  lean_state = 0;
   cp(m.iw, h.iw.data(), N * sizeof(int32_t));
   cp(m.jw, h.jw.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
   DevScalars s0{};
   const double d0 = dt;
   std::memcpy(&s0.dt_bits[0], &d0, 8);
-  s0.dt_bits[1] = s0.dt_bits[2] = s0.dt_bits[0];
+  const double one = 1.0;  // slot 1 accumulates step 0's min; slot 2 is reset by step 0
+  std::memcpy(&s0.dt_bits[1], &one, 8);
+  s0.dt_bits[2] = s0.dt_bits[1];
   s0.time_part = 0.0;
   time_offset = -cur_time_part;
   last_dev_time = 0.0;
@@ -474,18 +593,33 @@ void DeviceSolver::upload() {
   HIP_CHECK(hipStreamSynchronize(st));
   nstep = 0;
   abuf = 0;
+  sbuf = 0;
   dsbuf = 0;
   pbuf = 0;
+}
+
+void DeviceSolver::lean_materialize() {
+  Impl& m = *impl;
+  StepParams P = make_params(last_iter + iter);
+  P.nx = h.nx;
+  P.ny = h.ny;
+  LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+  SoA g = m.view(h, sbuf, abuf, dsbuf, pbuf);
+  const unsigned nb = (unsigned)((h.N + BLOCK - 1) / BLOCK);
+  hipLaunchKernelGGL(hf2d_lean_materialize, dim3(nb), dim3(BLOCK), 0, m.stream, P, L, g, 0L, h.N);
+  HIP_CHECK(hipGetLastError());
+  lean_state = 0;
 }
 
 void DeviceSolver::download(Field& J) {
   HIP_CHECK(hipSetDevice(dev));
   Impl& m = *impl;
+  if (lean_state) lean_materialize();
   hipStream_t st = m.stream;
   const long N = h.N;
   auto cp = [&](void* d, const void* s, size_t bytes) { HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st)); };
   const size_t EQB = NEQ * N * sizeof(real), SB = N * sizeof(real);
-  cp(h.S[0].data(), m.S[0], EQB);
+  cp(h.S[0].data(), m.S[sbuf], EQB);
   cp(h.A.data(), m.A[abuf], EQB);
   cp(h.B.data(), m.B[abuf], EQB);
   cp(h.dSdx[0].data(), m.dSdx[dsbuf], EQB);
@@ -540,7 +674,7 @@ void DeviceSolver::cycle_update() {
     StepParams P = make_params(last_iter);
     P.nx = h.nx;
     P.ny = h.ny;
-    SoA s = m.view(h, 0, abuf, dsbuf, pbuf);
+    SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     const long c0 = (long)l_off * h.ny, c1 = (long)(l_off + (gi1 - gi0)) * h.ny;
     const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(hf2d_yplus, dim3(nb), dim3(BLOCK), 0, m.stream, P, s, c0, c1, gi0 - l_off);
@@ -617,12 +751,19 @@ void DeviceSolver::exchange(int group) {
   auto add_eq = [&](real* base) {
     for (int k = 0; k < NEQ; k++) L.f[L.nf++] = base + (long)k * N;
   };
-  if (group == CpuSolver::HALO_MID) {
-    add_eq(m.S[1]);
+  if (group == CpuSolver::HALO_LEAN) {
+    for (int k = 0; k < 4 + NCOMP; k++) L.f[L.nf++] = m.S[sbuf] + (long)k * N;
+    for (int k = 0; k < NCOMP; k++) L.f[L.nf++] = m.Spre[pbuf] + (long)k * N;
+    L.f[L.nf++] = m.U[pbuf];
+    L.f[L.nf++] = m.V[pbuf];
+    L.f[L.nf++] = m.P2[pbuf];
+    add_eq(m.dSdx[dsbuf]);
+  } else if (group == CpuSolver::HALO_MID) {
+    add_eq(m.S[1 - sbuf]);
   } else if (group == CpuSolver::HALO_QDIR) {
     for (int d = 0; d < 4; d++) L.f[L.nf++] = m.qdir + (long)d * N;
   } else {
-    add_eq(m.S[0]);
+    add_eq(m.S[sbuf]);
     add_eq(m.A[abuf]);
     add_eq(m.B[abuf]);
     add_eq(m.dSdx[dsbuf]);
@@ -668,10 +809,37 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   const int serial = cs.cfg.semantics == Semantics::SERIAL ? 1 : 0;
   const bool euler = P.sm != SM_NS;
   hipStream_t st = m.stream;
-  if (euler && fused) {
-    SoA in = m.view(h, 0, abuf, dsbuf, pbuf);
-    SoA mid = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
-    SoA out = m.view(h, 0, 1 - abuf, 1 - dsbuf, pbuf);
+  if (euler && lean && lean_ok) {
+    const bool fromg = lean_state == 0;
+    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, fromg);
+    if (want_res) {
+      if (fromg)
+        hipLaunchKernelGGL((hf2d_lean_euler<true, true>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+      else
+        hipLaunchKernelGGL((hf2d_lean_euler<true, false>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+    } else {
+      if (fromg)
+        hipLaunchKernelGGL((hf2d_lean_euler<false, true>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+      else
+        hipLaunchKernelGGL((hf2d_lean_euler<false, false>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc,
+                           slot, slot_next, serial, m.partials);
+    }
+    HIP_CHECK(hipGetLastError());
+    sbuf = 1 - sbuf;
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+    lean_state = 1;
+  } else if (euler && fused) {
+    if (lean_state) lean_materialize();
+    // Predictor and fill of a cell run back to back in one thread, so the
+    // new state goes to the other S buffer (neighbours still read the old
+    // one) and the current-state index flips.
+    SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
+    SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
+    SoA out = m.view(h, 1 - sbuf, 1 - abuf, 1 - dsbuf, pbuf);
     if (want_res)
       hipLaunchKernelGGL(hf2d_fused_euler<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, out, c0, c1, m.sc, slot,
                          slot_next, serial, m.partials);
@@ -681,9 +849,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
     HIP_CHECK(hipGetLastError());
     abuf = 1 - abuf;
     dsbuf = 1 - dsbuf;
+    sbuf = 1 - sbuf;
   } else {
-    SoA in = m.view(h, 0, abuf, dsbuf, pbuf);
-    SoA mid = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
+    if (lean_state) lean_materialize();
+    SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
+    SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     if (want_res)
       hipLaunchKernelGGL(hf2d_predict<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next,
                          serial, m.partials);
@@ -692,9 +862,10 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
                          serial, m.partials);
     HIP_CHECK(hipGetLastError());
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
-    SoA sin = m.view(h, 1, abuf, 1 - dsbuf, pbuf);
-    SoA out = m.view(h, 0, abuf, 1 - dsbuf, 1 - pbuf);
-    hipLaunchKernelGGL(hf2d_fill, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot, slot_next);
+    SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
+    SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
+    hipLaunchKernelGGL(hf2d_fill, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot, slot_next,
+                       serial);
     HIP_CHECK(hipGetLastError());
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
@@ -703,10 +874,10 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
     // global dt: MIN over ranks, in place on the next slot
     real* dslot = (real*)&m.sc->dt_bits[slot_next];
     NCCL_CHECK(ncclAllReduce(dslot, dslot, 1, ncclDouble, ncclMin, m.comm, st));
-    exchange(CpuSolver::HALO_STATE);
+    exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE);
   }
   if (!cs.cfg.isAdiabaticWall) {
-    SoA s = m.view(h, 0, abuf, dsbuf, pbuf);
+    SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     hipLaunchKernelGGL(hf2d_wall_solid, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1);
     exchange(CpuSolver::HALO_QDIR);
     hipLaunchKernelGGL(hf2d_wall_wall, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1, m.sc, slot);

@@ -35,8 +35,16 @@ class DeviceSolver : public SolverBase {
   int dev = 0;
   int gi0 = 0, gi1 = 0, l_off = 0;
   long nstep = 0;
-  int abuf = 0, dsbuf = 0, pbuf = 0;
+  int abuf = 0, dsbuf = 0, pbuf = 0, sbuf = 0;  // ping-pong indices (sbuf: current state)
   bool fused = true;      // Euler: single fused predict+fill kernel
+  // Inviscid: lean kernel on the reduced state (lean_euler.hpp) when the case
+  // is eligible; takes precedence over `fused`.
+  bool lean = true;
+  bool lean_ok = false;
+  std::string lean_why;
+  int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
+  std::vector<uint8_t> lean_bytes;
+  void lean_materialize();
   std::unique_ptr<Comm> host_comm;
 
  private:

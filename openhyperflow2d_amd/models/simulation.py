@@ -16,7 +16,7 @@ import numpy as np
 class Simulation:
     def __init__(self, deck_text: str, backend: Optional[str] = None, *, workdir: str = ".",
                  use_checkpoint: bool = False, device: int = 0, semantics: str = "mpi",
-                 gi0: int = 0, gi1: int = -1, fused: bool = True):
+                 gi0: int = 0, gi1: int = -1, fused: bool = True, lean: Optional[bool] = None):
         from .. import native
 
         hf = native()
@@ -29,8 +29,10 @@ class Simulation:
         if backend == "gpu":
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
+            self.solver.lean = True if lean is None else bool(lean)
         elif backend == "cpu":
             self.solver = hf.CpuSolver(self.case, gi0, gi1)
+            self.solver.lean = False if lean is None else bool(lean)
         elif backend == "ref":
             self.solver = hf.RefSolver(self.case)
         else:

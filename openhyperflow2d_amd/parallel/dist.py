@@ -36,7 +36,7 @@ class DistributedSimulation:
     """A strip of a deck run on this rank."""
 
     def __init__(self, deck_text: str, backend: str = "gpu", *, rank: int = 0, world: int = 1,
-                 device: int = 0, semantics: str = "mpi", fused: bool = True, parts=None):
+                 device: int = 0, semantics: str = "mpi", fused: bool = True, lean: bool = True, parts=None):
         from .. import native
 
         hf = native()
@@ -51,6 +51,7 @@ class DistributedSimulation:
         if backend == "gpu":
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
+            self.solver.lean = lean
             if world > 1:
                 import torch.distributed as dist
 
@@ -59,6 +60,7 @@ class DistributedSimulation:
                 self.solver.init_comm(obj[0], rank, world)
         elif backend == "cpu":
             self.solver = hf.CpuSolver(self.case, gi0, gi1)
+            self.solver.lean = lean
             if world > 1:
                 self._wire_cpu()
         else:
