@@ -222,6 +222,7 @@ PYBIND11_MODULE(_hf2d, m) {
 
   py::class_<CpuSolver, SolverBase>(m, "CpuSolver")
       .def_readwrite("lean", &CpuSolver::lean)
+      .def_readwrite("lean_tile", &CpuSolver::lean_tile)
       .def_readonly("lean_ok", &CpuSolver::lean_ok)
       .def_readonly("lean_why", &CpuSolver::lean_why)
       .def(py::init<Case&, int, int>(), py::arg("case"), py::arg("gi0") = 0, py::arg("gi1") = -1,
@@ -266,6 +267,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("fused", &DeviceSolver::fused)
       .def_readwrite("lean", &DeviceSolver::lean)
+      .def_readwrite("lean_tile", &DeviceSolver::lean_tile)
       .def_readonly("lean_ok", &DeviceSolver::lean_ok)
       .def_readonly("lean_why", &DeviceSolver::lean_why)
       .def_readonly("gi0", &DeviceSolver::gi0)

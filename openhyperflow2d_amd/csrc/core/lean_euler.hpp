@@ -88,42 +88,30 @@ HF_HD inline real lean_flux_B(const LeanSoA& L, int k, long at, real u, real v, 
   }
 }
 
-template <bool FROMG>
-struct LeanIO {
+// Accessor members shared by the global-memory and the LDS-tile IO: the
+// node's own persistent arrays (beta, dS/dx, dS/dy, SrcAdd) stay in global
+// memory, addressed by the global indices idx / iL / iR / iU / iD.
+struct LeanIOCommon {
   static constexpr int NE = 4 + NCOMP;
   const LeanSoA& L;
   long N, idx, iL, iR, iU, iD;
-  uint8_t lb;
-  bool noslip;
-  real FT;
-  real uL, pL, uR, pR, uU, vU, pU, uD, vD, pD, u0, v0, p0;
+  uint8_t lb = 0;
+  bool noslip = false;
+  real FT = 0;
   real sm[NEQ];
 
-  HF_HD real S(int k) const { return L.Sin[k * N + idx]; }
-  HF_HD real SL(int k) const { return L.Sin[k * N + iL]; }
-  HF_HD real SR(int k) const { return L.Sin[k * N + iR]; }
-  HF_HD real SU(int k) const { return L.Sin[k * N + iU]; }
-  HF_HD real SD(int k) const { return L.Sin[k * N + iD]; }
-  HF_HD real AL(int k) const { return FROMG ? L.gA[k * N + iL] : lean_flux_A(L, k, iL, uL, pL); }
-  HF_HD real AR(int k) const { return FROMG ? L.gA[k * N + iR] : lean_flux_A(L, k, iR, uR, pR); }
-  HF_HD real BU(int k) const { return FROMG ? L.gB[k * N + iU] : lean_flux_B(L, k, iU, uU, vU, pU); }
-  HF_HD real BD(int k) const { return FROMG ? L.gB[k * N + iD] : lean_flux_B(L, k, iD, uD, vD, pD); }
+  HF_HD LeanIOCommon(const LeanSoA& l, long i) : L(l), N(l.N), idx(i), iL(i), iR(i), iU(i), iD(i) {}
+  HF_HD void set_nb_global(int i, int j, int ny, int n1, int n2, int n3, int n4) {
+    iL = (long)(i - n1) * ny + j;
+    iR = (long)(i + n2) * ny + j;
+    iU = idx + n3;
+    iD = idx - n4;
+  }
   HF_HD real dxL(int k) const { return L.dSdx_in[k * N + iL]; }
   HF_HD real dxR(int k) const { return L.dSdx_in[k * N + iR]; }
   HF_HD real dyU(int k) const { return L.dSdy_in[k * N + iU]; }
   HF_HD real dyD(int k) const { return L.dSdy_in[k * N + iD]; }
   HF_HD real beta(int k) const { return L.beta[k * N + idx]; }
-  // axisymmetric source of the node's own previous fill (fill_node F block)
-  HF_HD real F(int k) const {
-    if (FROMG) return L.gF[k * N + idx];
-    switch (k) {
-      case I_RHO: return FT * L.Sin[2 * N + idx];
-      case I_RHOU: return FT * (L.Sin[2 * N + idx] * u0);
-      case I_RHOV: return FT * (FT * L.Sin[2 * N + idx]) * v0;
-      case I_RHOE: return FT * ((L.Sin[3 * N + idx] + p0) * v0);
-      default: return FT * (L.Pin_s[(k - 4) * N + idx] * v0);
-    }
-  }
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int k) const { return noslip ? L.SrcAdd[k * N + idx] : 0.0; }
   HF_HD void put_S(int k, real v) { sm[k] = v; }
@@ -138,6 +126,56 @@ struct LeanIO {
   }
 };
 
+// Global-memory IO.  FROMG: the previous step was generic, read its A/B/F.
+template <bool FROMG>
+struct LeanIO : LeanIOCommon {
+  real uL, pL, uR, pR, uU, vU, pU, uD, vD, pD, u0, v0, p0;
+
+  HF_HD LeanIO(const LeanSoA& l, long i) : LeanIOCommon(l, i) {
+    u0 = L.Uin[idx];
+    v0 = L.Vin[idx];
+    p0 = L.Pin[idx];
+  }
+  HF_HD real U0() const { return u0; }
+  HF_HD real V0() const { return v0; }
+  HF_HD real P0() const { return p0; }
+  HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
+    set_nb_global(i, j, ny, n1, n2, n3, n4);
+    if (!FROMG) {
+      uL = L.Uin[iL];
+      pL = L.Pin[iL];
+      uR = L.Uin[iR];
+      pR = L.Pin[iR];
+      uU = L.Uin[iU];
+      vU = L.Vin[iU];
+      pU = L.Pin[iU];
+      uD = L.Uin[iD];
+      vD = L.Vin[iD];
+      pD = L.Pin[iD];
+    }
+  }
+  HF_HD real S(int k) const { return L.Sin[k * N + idx]; }
+  HF_HD real SL(int k) const { return L.Sin[k * N + iL]; }
+  HF_HD real SR(int k) const { return L.Sin[k * N + iR]; }
+  HF_HD real SU(int k) const { return L.Sin[k * N + iU]; }
+  HF_HD real SD(int k) const { return L.Sin[k * N + iD]; }
+  HF_HD real AL(int k) const { return FROMG ? L.gA[k * N + iL] : lean_flux_A(L, k, iL, uL, pL); }
+  HF_HD real AR(int k) const { return FROMG ? L.gA[k * N + iR] : lean_flux_A(L, k, iR, uR, pR); }
+  HF_HD real BU(int k) const { return FROMG ? L.gB[k * N + iU] : lean_flux_B(L, k, iU, uU, vU, pU); }
+  HF_HD real BD(int k) const { return FROMG ? L.gB[k * N + iD] : lean_flux_B(L, k, iD, uD, vD, pD); }
+  // axisymmetric source of the node's own previous fill (fill_node F block)
+  HF_HD real F(int k) const {
+    if (FROMG) return L.gF[k * N + idx];
+    switch (k) {
+      case I_RHO: return FT * L.Sin[2 * N + idx];
+      case I_RHOU: return FT * (L.Sin[2 * N + idx] * u0);
+      case I_RHOV: return FT * (FT * L.Sin[2 * N + idx]) * v0;
+      case I_RHOE: return FT * ((L.Sin[3 * N + idx] + p0) * v0);
+      default: return FT * (L.Pin_s[(k - 4) * N + idx] * v0);
+    }
+  }
+};
+
 // Node as seen by chemistry_zeldovich().
 struct LeanChemNode {
   real S[NEQ];
@@ -146,18 +184,20 @@ struct LeanChemNode {
   u64 CT;
 };
 
-// One lean step of cell (i, j).  Returns the local dt limit (1.0 if none).
-template <bool FROMG>
-HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, int j, ResidualPack* res,
-                                  int* neg_T) {
+// One lean step of cell (i, j) through accessor `io` (constructed on idx).
+// Returns the local dt limit (1.0 if none).
+template <bool RES, class IO>
+HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i, int j, ResidualPack& res,
+                            int* neg_T) {
   const long N = L.N;
-  const long idx = (long)i * P.ny + j;
+  const long idx = io.idx;
   const u64 CT = L.CT[idx];
   const uint8_t lb = L.lb[idx];
   constexpr int NE = 4 + NCOMP;
+  io.lb = lb;
   if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
     // neither transported nor filled: carry the state into the other buffers
-    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = L.Sin[k * N + idx];
+    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = io.S(k);
     if (lb & LB_DX_OUT)
       for (int k = 0; k < NEQ; k++) L.dSdx_out[k * N + idx] = L.dSdx_in[k * N + idx];
     if (lb & LB_DY_OUT)
@@ -166,38 +206,22 @@ HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, 
   }
   const bool active = !has_all(CT, NT_FC);
   const bool noslip = has_all(CT, CT_WALL_NO_SLIP);
-  const real u_old = L.Uin[idx], v_old = L.Vin[idx];
-  LeanIO<FROMG> io{L, N, idx, idx, idx, idx, idx, lb, noslip, (real)P.fpa.FT};
-  io.u0 = u_old;
-  io.v0 = v_old;
-  io.p0 = L.Pin[idx];
+  io.noslip = noslip;
+  io.FT = (real)P.fpa.FT;
+  const real u_old = io.U0(), v_old = io.V0();
   if (active) {
     const int n1 = (lb & NB_XL) ? 1 : 0, n2 = (lb & NB_XR) ? 1 : 0;
     const int n3 = (lb & NB_YU) ? 1 : 0, n4 = (lb & NB_YD) ? 1 : 0;
-    io.iL = (long)(i - n1) * P.ny + j;
-    io.iR = (long)(i + n2) * P.ny + j;
-    io.iU = idx + n3;
-    io.iD = idx - n4;
-    if (!FROMG) {
-      io.uL = L.Uin[io.iL];
-      io.pL = L.Pin[io.iL];
-      io.uR = L.Uin[io.iR];
-      io.pR = L.Pin[io.iR];
-      io.uU = L.Uin[io.iU];
-      io.vU = L.Vin[io.iU];
-      io.pU = L.Pin[io.iU];
-      io.uD = L.Uin[io.iD];
-      io.vD = L.Vin[io.iD];
-      io.pD = L.Pin[io.iD];
-    }
+    io.set_nb(i, j, P.ny, n1, n2, n3, n4);
     // Equations >= NE are frozen for inviscid cells: TurbType only matters
     // through num_eq_for(), which is >= NE for every model.
-    predict_core(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
+    predict_core<RES>(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
     if (lb & (LB_DX_OUT | LB_DY_OUT))
       for (int k = NE; k < NEQ; k++) io.keep_dS(k);
   } else {
-    for (int k = 0; k < NE; k++) io.sm[k] = L.Sin[k * N + idx];
-    for (int k = 0; k < NEQ; k++) io.keep_dS(k);
+    for (int k = 0; k < NE; k++) io.sm[k] = io.S(k);
+    if (lb & (LB_DX_OUT | LB_DY_OUT))
+      for (int k = 0; k < NEQ; k++) io.keep_dS(k);
   }
 
   // ---- FillNode2D, inviscid subset (fill_node) ----
@@ -205,7 +229,11 @@ HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, 
   for (int k = 0; k < NE; k++) c.S[k] = io.sm[k];
   c.S[NE] = c.S[NE + 1] = 0.;
   real* s = c.S;
-  const FillParams& F = active ? P.fpa : P.ffc;
+  // NT_FC nodes are filled with FillNode2D(1, 0, ...) (P.ffc): it differs
+  // from P.fpa only in is_mu_t / is_init, which the inviscid fill never reads.
+  // (A runtime-selected reference into the kernel-argument block would force
+  // a scratch copy of StepParams.)
+  const FillParams& F = P.fpa;
   c.R = L.R[idx];
   c.CP = L.CP[idx];
   const real k_old = L.kk[idx];
@@ -215,7 +243,7 @@ HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, 
     for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
     L.Uout[idx] = u_old;
     L.Vout[idx] = v_old;
-    L.Pout[idx] = io.p0;
+    L.Pout[idx] = io.P0();
     return 1.0;
   }
   const real kk = c.CP / (c.CP - c.R);
@@ -295,6 +323,142 @@ HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, 
   L.Tout[idx] = Tg;
   L.kk[idx] = kk;
   return dt_local;
+}
+
+// ---------------------------------------------------------------------------
+// LDS-tiled form.  A workgroup owns a TI x TJ tile of cells (TJ along the
+// contiguous j axis, sized so ny splits into equal tiles of <= 64) and first
+// stages the tile plus its one-cell cross-shaped halo -- S (7), pre-chemistry
+// species (3), U, V, p -- into LDS with independent coalesced loads; every
+// neighbour flux is then evaluated from LDS.  The node's own beta / CP / R /
+// k / flags come straight from global memory (read once).
+// ---------------------------------------------------------------------------
+constexpr int LEAN_TILE_FIELDS = 13;   // S[0..6], Spre[0..2], U, V, p
+constexpr int LEAN_TILE_MIN_TJ = 8;
+
+struct LeanTile {
+  int TI, TJ, W, NC, nbi, nbj;
+};
+
+inline LeanTile lean_tile_geom(int ncols, int ny, int block) {
+  LeanTile T;
+  const int nj = (ny + 63) / 64;
+  T.TJ = (ny + nj - 1) / nj;
+  T.TI = block / T.TJ;
+  T.W = T.TJ + 2;
+  T.NC = (T.TI + 2) * T.W;
+  T.nbi = (ncols + T.TI - 1) / T.TI;
+  T.nbj = (ny + T.TJ - 1) / T.TJ;
+  return T;
+}
+
+// Thread t of nthreads stages its share of tile (i0, j0).  LDS layout:
+// lds[f * NC + c], c = (ii + 1) * W + (jj + 1), ii in [-1, TI], jj in [-1, TJ].
+HF_HD inline void lean_tile_stage(const StepParams& P, const LeanSoA& L, const LeanTile& T, int i0, int j0,
+                                  real* lds, int t, int nthreads) {
+  const long N = L.N;
+  const int NC = T.NC;
+  for (int c = t; c < NC; c += nthreads) {
+    const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
+    const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
+    const int gi = i0 + ii, gj = j0 + jj;
+    if ((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
+    const long g = (long)gi * P.ny + gj;
+#pragma unroll
+    for (int f = 0; f < 4 + NCOMP; f++) lds[f * NC + c] = L.Sin[f * N + g];
+#pragma unroll
+    for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + c] = L.Pin_s[f * N + g];
+    lds[10 * NC + c] = L.Uin[g];
+    lds[11 * NC + c] = L.Vin[g];
+    lds[12 * NC + c] = L.Pin[g];
+  }
+}
+
+struct TileIO : LeanIOCommon {
+  const real* lds;
+  int NC, W, c, cL, cR, cU, cD;
+
+  HF_HD TileIO(const LeanSoA& l, long i, const real* s, int nc, int w, int cc)
+      : LeanIOCommon(l, i), lds(s), NC(nc), W(w), c(cc), cL(cc), cR(cc), cU(cc), cD(cc) {}
+  HF_HD real at(int f, int cc) const { return lds[f * NC + cc]; }
+  HF_HD real U0() const { return at(10, c); }
+  HF_HD real V0() const { return at(11, c); }
+  HF_HD real P0() const { return at(12, c); }
+  HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
+    set_nb_global(i, j, ny, n1, n2, n3, n4);
+    cL = c - n1 * W;
+    cR = c + n2 * W;
+    cU = c + n3;
+    cD = c - n4;
+  }
+  HF_HD real S(int k) const { return at(k, c); }
+  HF_HD real SL(int k) const { return at(k, cL); }
+  HF_HD real SR(int k) const { return at(k, cR); }
+  HF_HD real SU(int k) const { return at(k, cU); }
+  HF_HD real SD(int k) const { return at(k, cD); }
+  HF_HD real fA(int k, int cc) const {
+    const real u = at(10, cc), p = at(12, cc);
+    switch (k) {
+      case I_RHO: return at(1, cc);
+      case I_RHOU: return p + at(1, cc) * u;
+      case I_RHOV: return at(2, cc) * u;
+      case I_RHOE: return (at(3, cc) + p) * u;
+      default: return at(k + 3, cc) * u;
+    }
+  }
+  HF_HD real fB(int k, int cc) const {
+    const real u = at(10, cc), v = at(11, cc), p = at(12, cc);
+    switch (k) {
+      case I_RHO: return at(2, cc);
+      case I_RHOU: return at(2, cc) * u;
+      case I_RHOV: return p + at(2, cc) * v;
+      case I_RHOE: return (at(3, cc) + p) * v;
+      default: return at(k + 3, cc) * v;
+    }
+  }
+  HF_HD real AL(int k) const { return fA(k, cL); }
+  HF_HD real AR(int k) const { return fA(k, cR); }
+  HF_HD real BU(int k) const { return fB(k, cU); }
+  HF_HD real BD(int k) const { return fB(k, cD); }
+  HF_HD real F(int k) const {
+    const real u0 = U0(), v0 = V0(), p0 = P0();
+    switch (k) {
+      case I_RHO: return FT * at(2, c);
+      case I_RHOU: return FT * (at(2, c) * u0);
+      case I_RHOV: return FT * (FT * at(2, c)) * v0;
+      case I_RHOE: return FT * ((at(3, c) + p0) * v0);
+      default: return FT * (at(k + 3, c) * v0);
+    }
+  }
+};
+
+// Logical tile b -> its cell for thread t; returns false for idle threads.
+HF_HD inline bool lean_tile_cell(const StepParams& P, const LeanTile& T, int b, int t, int* i, int* j, int* c,
+                                 int* i0, int* j0) {
+  const int bi = b / T.nbj, bj = b - bi * T.nbj;
+  *i0 = P.i0 + bi * T.TI;
+  *j0 = bj * T.TJ;
+  const int ii = t / T.TJ, jj = t - ii * T.TJ;
+  *i = *i0 + ii;
+  *j = *j0 + jj;
+  *c = (ii + 1) * T.W + jj + 1;
+  return ii < T.TI && *i < P.i1 && *j < P.ny;
+}
+
+template <bool RES, bool FROMG>
+HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, int j, ResidualPack& res,
+                                  int* neg_T) {
+  LeanIO<FROMG> io(L, (long)i * P.ny + j);
+  return lean_cell<RES>(P, L, io, i, j, res, neg_T);
+}
+
+// host convenience: nullable residual pack
+template <class IO>
+inline real lean_cell_host(const StepParams& P, const LeanSoA& L, IO& io, int i, int j, ResidualPack* res,
+                           int* neg_T) {
+  if (res) return lean_cell<true>(P, L, io, i, j, *res, neg_T);
+  ResidualPack d;
+  return lean_cell<false>(P, L, io, i, j, d, neg_T);
 }
 
 // Rebuild the generic per-node fluxes (A, B, F) and p from the lean state,

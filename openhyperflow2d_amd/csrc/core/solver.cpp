@@ -1,6 +1,7 @@
 #include "solver.hpp"
 
 #include <algorithm>
+#include <limits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -579,11 +580,37 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
     int negT = 0;
     real dtmin = 1.0;
     ResidualPack* rp = want_res ? &r.res : nullptr;
-    for (int i = P.i0; i < P.i1; i++)
-      for (int j = 0; j < P.ny; j++) {
-        const real d = fromg ? lean_euler_cell<true>(P, L, i, j, rp, &negT) : lean_euler_cell<false>(P, L, i, j, rp, &negT);
-        dtmin = std::min(dtmin, d);
+    if (!fromg && lean_tile && P.ny >= LEAN_TILE_MIN_TJ) {
+      // host emulation of the device's LDS-tiled kernel (same staging and
+      // indexing); unstaged LDS entries are poisoned with NaN
+      constexpr int NT = 256;
+      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, NT);
+      std::vector<real> lds((size_t)LEAN_TILE_FIELDS * T.NC);
+      for (int b = 0; b < T.nbi * T.nbj; b++) {
+        std::fill(lds.begin(), lds.end(), std::numeric_limits<real>::quiet_NaN());
+        int i, j, c, i0, j0;
+        lean_tile_cell(P, T, b, 0, &i, &j, &c, &i0, &j0);
+        for (int t = 0; t < NT; t++) lean_tile_stage(P, L, T, i0, j0, lds.data(), t, NT);
+        for (int t = 0; t < NT; t++) {
+          if (!lean_tile_cell(P, T, b, t, &i, &j, &c, &i0, &j0)) continue;
+          TileIO io(L, (long)i * P.ny + j, lds.data(), T.NC, T.W, c);
+          dtmin = std::min(dtmin, lean_cell_host(P, L, io, i, j, rp, &negT));
+        }
       }
+    } else {
+      for (int i = P.i0; i < P.i1; i++)
+        for (int j = 0; j < P.ny; j++) {
+          real d;
+          if (fromg) {
+            LeanIO<true> io(L, (long)i * P.ny + j);
+            d = lean_cell_host(P, L, io, i, j, rp, &negT);
+          } else {
+            LeanIO<false> io(L, (long)i * P.ny + j);
+            d = lean_cell_host(P, L, io, i, j, rp, &negT);
+          }
+          dtmin = std::min(dtmin, d);
+        }
+    }
     // halo columns keep their exchanged values
     for (int i = 0; i < h.nx; i++) {
       if (i >= P.i0 && i < P.i1) continue;

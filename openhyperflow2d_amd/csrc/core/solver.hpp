@@ -140,6 +140,7 @@ class CpuSolver : public SolverBase {
   // lean inviscid path (off by default on the CPU: the generic stepper is the
   // oracle the device kernels are checked against)
   bool lean = false;
+  bool lean_tile = false;   // emulate the device's LDS-tiled lean kernel
   bool lean_ok = false;
   std::string lean_why;
   int lean_state = 0;   // 1: lean arrays authoritative, A/B/F/p stale

@@ -182,9 +182,12 @@ HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, rea
 //   beta(k) F(k) Src(k) SrcAdd(k)
 //   put_S(k, v) put_beta(k, v) put_dS(k, dsdx, dsdy) keep_dS(k)
 // ---------------------------------------------------------------------------
-template <class IO>
+template <bool RES, class IO>
 HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int n1, int n2, int n3, int n4, int gi,
-                               int j, ResidualPack* res) {
+                               int j, ResidualPack& rp) {
+  // RES is a template flag (not a nullable pointer) so the device kernels
+  // keep the residual pack in registers.
+
   const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
   const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
   const int Num_Eq = num_eq_for(TT);
@@ -203,8 +206,8 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
         const real DD = 1.0;
         const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
         io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, 1.0));
-        if (res) {
-          EqResidual& e = res->eq[k];
+        if (RES) {
+          EqResidual& e = rp.eq[k];
           if (DD >= e.dd_max) {
             e.dd_max = DD;
             e.i = gi;
@@ -265,8 +268,8 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
       }
       const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
       io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, sqrt_res));
-      if (res) {
-        EqResidual& e = res->eq[k];
+      if (RES) {
+        EqResidual& e = rp.eq[k];
         if (DD >= e.dd_max) {
           e.dd_max = DD;
           e.i = gi;
@@ -320,8 +323,9 @@ struct SoAPredictIO {
   }
 };
 
-HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
-                               ResidualPack* res) {
+template <bool RES>
+HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
+                                 ResidualPack& res) {
   const long N = in.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = in.CT[idx];
@@ -338,8 +342,17 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
   SoAPredictIO io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4};
-  predict_core(P, io, CT, in.TT[idx], n1, n2, n3, n4, P.gx0 + i, j, res);
-  (void)TT;
+  predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
+}
+
+HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
+                               ResidualPack* res) {
+  if (res) {
+    predict_cell_t<true>(P, in, out, i, j, *res);
+  } else {
+    ResidualPack d;
+    predict_cell_t<false>(P, in, out, i, j, d);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -469,7 +482,15 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     c.dTdy = (prim_old.Tg[iU] - prim_old.Tg[iD]) * dy_1_m;
   }
 
-  fill_node(c, active ? P.fpa : P.ffc);
+  // P.ffc (NT_FC nodes) differs from P.fpa only in is_mu_t / is_init; patch
+  // those two fields rather than binding a runtime-selected reference into the
+  // kernel-argument block (which makes the compiler copy StepParams to scratch).
+  FillParams fp = P.fpa;
+  if (!active) {
+    fp.is_mu_t = P.ffc.is_mu_t;
+    fp.is_init = P.ffc.is_init;
+  }
+  fill_node(c, fp);
 
   real dt_local = 1.0;
   if (active) {

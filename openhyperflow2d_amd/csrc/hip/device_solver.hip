@@ -77,6 +77,7 @@ __device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
 // Wave-level residual reduction helpers
 // ---------------------------------------------------------------------------
 __device__ inline void shfl_merge(ResidualPack& r, int off) {
+#pragma unroll
   for (int k = 0; k < NEQ; k++) {
     EqResidual o;
     o.dd_max = __shfl_xor(r.eq[k].dd_max, off, WAVE);
@@ -118,13 +119,15 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
   ResidualPack r;
   if (RES) {
     residual_reset(r);
+#pragma unroll
     for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
   }
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    predict_cell(P, in, out, i, j, RES ? &r : nullptr);
+    predict_cell_t<RES>(P, in, out, i, j, r);
   }
   if (RES) {
+#pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
     if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
   }
@@ -188,16 +191,18 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   ResidualPack r;
   if (RES) {
     residual_reset(r);
+#pragma unroll
     for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
   }
   double dtl = 1.0;
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    predict_cell(P, in, mid, i, j, RES ? &r : nullptr);
+    predict_cell_t<RES>(P, in, mid, i, j, r);
     dtl = fill_cell(P, mid, mid, out, i, j, &neg, false);
   }
   if (RES) {
+#pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
     if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
   }
@@ -239,15 +244,63 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
   ResidualPack r;
   if (RES) {
     residual_reset(r);
+#pragma unroll
     for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
   }
   double dtl = 1.0;
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    dtl = lean_euler_cell<FROMG>(P, L, i, j, RES ? &r : nullptr, &neg);
+    dtl = lean_euler_cell<RES, FROMG>(P, L, i, j, r, &neg);
   }
   if (RES) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+// LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
+template <bool RES>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                         int slot, int slot_next, int serial,
+                                                         ResidualPack* partials) {
+  extern __shared__ real lds[];
+  apply_dt(P, sc, slot);
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  if (b == 0 && threadIdx.x == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += P.dt;
+  }
+  int i, j, c, i0, j0;
+  const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
+  lean_tile_stage(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
+  __syncthreads();
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+#pragma unroll
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  if (mine) {
+    TileIO io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
+    dtl = lean_cell<RES>(P, L, io, i, j, r, &neg);
+  }
+  if (RES) {
+#pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
     if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
   }
@@ -503,7 +556,11 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.species = m.mem.alloc<SpeciesProps>(1);
   m.sc = m.mem.alloc<DevScalars>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.sc_host, sizeof(DevScalars), hipHostMallocDefault));
-  m.max_partials = (N + BLOCK - 1) / BLOCK * (BLOCK / WAVE);
+  {
+    const LeanTile T = lean_tile_geom(gi1 - gi0, h.ny, BLOCK);
+    const long nb_tile = (long)T.nbi * T.nbj;
+    m.max_partials = std::max((N + BLOCK - 1) / BLOCK, nb_tile) * (BLOCK / WAVE);
+  }
   m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
   m.res_out = m.mem.alloc<ResidualPack>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.res_host, sizeof(ResidualPack), hipHostMallocDefault));
@@ -809,7 +866,24 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   const int serial = cs.cfg.semantics == Semantics::SERIAL ? 1 : 0;
   const bool euler = P.sm != SM_NS;
   hipStream_t st = m.stream;
-  if (euler && lean && lean_ok) {
+  unsigned nres = nblk;   // workgroups that wrote residual partials
+  if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
+    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK);
+    const unsigned ntile = (unsigned)(T.nbi * T.nbj);
+    const size_t shmem = (size_t)LEAN_TILE_FIELDS * T.NC * sizeof(real);
+    if (want_res)
+      hipLaunchKernelGGL(hf2d_lean_tile<true>, dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
+                         serial, m.partials);
+    else
+      hipLaunchKernelGGL(hf2d_lean_tile<false>, dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
+                         serial, m.partials);
+    HIP_CHECK(hipGetLastError());
+    nres = ntile;
+    sbuf = 1 - sbuf;
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+  } else if (euler && lean && lean_ok) {
     const bool fromg = lean_state == 0;
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, fromg);
     if (want_res) {
@@ -887,7 +961,7 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   StepResult r;
   r.async = true;
   if (want_res) {
-    hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials, (long)nblk * (BLOCK / WAVE),
+    hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials, (long)nres * (BLOCK / WAVE),
                        m.res_out);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(m.res_host, m.res_out, sizeof(ResidualPack), hipMemcpyDeviceToHost, st));

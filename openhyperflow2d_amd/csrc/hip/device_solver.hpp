@@ -40,6 +40,7 @@ class DeviceSolver : public SolverBase {
   // Inviscid: lean kernel on the reduced state (lean_euler.hpp) when the case
   // is eligible; takes precedence over `fused`.
   bool lean = true;
+  bool lean_tile = true;  // LDS-tiled lean kernel for all but the first lean step
   bool lean_ok = false;
   std::string lean_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)

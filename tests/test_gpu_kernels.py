@@ -10,11 +10,24 @@ pytestmark = pytest.mark.gpu
 FIELDS = ["rho", "U", "V", "p", "T"]
 
 
-MODES = {"lean": dict(lean=True), "fused": dict(lean=False, fused=True), "split": dict(lean=False, fused=False)}
+MODES = {
+    "lean_tile": dict(lean=True, lean_tile=True),
+    "lean_flat": dict(lean=True, lean_tile=False),
+    "fused": dict(lean=False, fused=True),
+    "split": dict(lean=False, fused=False),
+}
 
 
-def _run_pair(hf, text, steps, mode="lean"):
-    g = hf.Simulation(text, "gpu", **MODES[mode])
+def _gpu_sim(hf, text, mode):
+    kw = dict(MODES[mode])
+    tile = kw.pop("lean_tile", True)
+    g = hf.Simulation(text, "gpu", **kw)
+    g.solver.lean_tile = tile
+    return g
+
+
+def _run_pair(hf, text, steps, mode="lean_tile"):
+    g = _gpu_sim(hf, text, mode)
     c = hf.Simulation(text, "cpu")
     g.step(steps, residual=True)
     c.step(steps, residual=True)
@@ -29,7 +42,7 @@ def _rel(a, b):
 def test_wedge_euler_gpu_matches_cpu(gpu, mode):
     text = decks.wedge15(200, 40, nmax=1000, nout=10)
     g, c = _run_pair(gpu, text, 50, mode)
-    if mode == "lean":
+    if mode.startswith("lean"):
         assert g.solver.lean_ok, g.solver.lean_why
     for f in FIELDS:
         assert _rel(g.field(f), c.field(f)) < 1e-11, f
@@ -83,7 +96,7 @@ def test_euler_gpu_equals_reference_order(gpu):
 def test_lean_bitwise_with_switches(gpu):
     """Lean GPU steps interleaved with downloads and generic steps stay
     bit-identical to the generic CPU stepper (dt, residuals, fields)."""
-    text = decks.wedge15(300, 60, nmax=10 ** 6, nout=10 ** 5)
+    text = decks.wedge15(301, 77, nmax=10 ** 6, nout=10 ** 5)
     g = gpu.Simulation(text, "gpu", lean=True)
     c = gpu.Simulation(text, "cpu")
     assert g.solver.lean_ok, g.solver.lean_why
