@@ -259,7 +259,11 @@ PYBIND11_MODULE(_hf2d, m) {
 
   py::class_<RefSolver, SolverBase>(m, "RefSolver").def(py::init<Case&>(), py::keep_alive<1, 2>());
 
+  py::class_<LocalGroup, std::shared_ptr<LocalGroup>>(m, "LocalGroup")
+      .def(py::init([](int n) { return make_local_group(n); }), py::arg("n"));
+
   py::class_<DeviceSolver, SolverBase>(m, "DeviceSolver")
+      .def("init_local", &DeviceSolver::init_local, py::arg("group"), py::arg("rank"))
       .def(py::init<Case&, int, int, int>(), py::arg("case"), py::arg("device") = 0, py::arg("gi0") = 0,
            py::arg("gi1") = -1, py::keep_alive<1, 2>())
       .def_static("nccl_unique_id", []() { return py::bytes(DeviceSolver::nccl_unique_id()); })

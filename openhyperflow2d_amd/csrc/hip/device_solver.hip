@@ -21,9 +21,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -383,6 +385,27 @@ struct DevBuf {
   }
 };
 
+struct LocalHostComm : Comm {
+  std::shared_ptr<LocalGroup> g;
+  int r;
+  LocalHostComm(std::shared_ptr<LocalGroup> g_, int r_) : g(std::move(g_)), r(r_) {}
+  int rank() const override { return r; }
+  int size() const override { return g->n; }
+  real allreduce_min(real v) override { return g->reduce(r, v, 0); }
+  real allreduce_sum(real v) override { return g->reduce(r, v, 1); }
+  int allreduce_max_int(int v) override { return (int)g->reduce(r, (double)v, 2); }
+  void allreduce_residual(ResidualPack& p) override {
+    g->packs[r] = p;
+    g->barrier();
+    ResidualPack a = g->packs[0];
+    for (int q = 1; q < g->n; q++) residual_merge_lex(a, g->packs[q]);
+    g->barrier();
+    p = a;
+  }
+};
+
+std::shared_ptr<LocalGroup> make_local_group(int n) { return std::make_shared<LocalGroup>(n); }
+
 struct DeviceSolver::Impl {
   DevBuf mem;
   hipStream_t stream = nullptr;
@@ -408,6 +431,7 @@ struct DeviceSolver::Impl {
   real* halo_recv[2] = {nullptr, nullptr};
   long halo_cap = 0;
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> local;   // in-process virtual ranks (testing)
   int rank = 0, nranks = 1;
 
   LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
@@ -793,6 +817,14 @@ void DeviceSolver::init_comm(const std::string& uid, int rank, int nranks) {
   comm = host_comm.get();
 }
 
+void DeviceSolver::init_local(std::shared_ptr<LocalGroup> g, int rank) {
+  impl->local = g;
+  impl->rank = rank;
+  impl->nranks = g->n;
+  host_comm.reset(new LocalHostComm(g, rank));
+  comm = host_comm.get();
+}
+
 int DeviceSolver::comm_rank() const { return impl->rank; }
 int DeviceSolver::comm_size() const { return impl->nranks; }
 
@@ -800,7 +832,7 @@ int DeviceSolver::comm_size() const { return impl->nranks; }
 // neighbours (rank-1 owns the columns to the left).
 void DeviceSolver::exchange(int group) {
   Impl& m = *impl;
-  if (!m.comm || m.nranks == 1) return;
+  if ((!m.comm && !m.local) || m.nranks == 1) return;
   const int ny = h.ny;
   const long N = h.N;
   ColList L;
@@ -836,6 +868,21 @@ void DeviceSolver::exchange(int group) {
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   if (has_left) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, first, ny, m.halo_send[0]);
   if (has_right) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, last, ny, m.halo_send[1]);
+  if (m.local) {
+    LocalGroup& g = *m.local;
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    g.send_l[m.rank] = m.halo_send[0];
+    g.send_r[m.rank] = m.halo_send[1];
+    g.barrier();
+    if (has_left)
+      HIP_CHECK(hipMemcpyAsync(m.halo_recv[0], g.send_r[m.rank - 1], (size_t)cnt * sizeof(real),
+                               hipMemcpyDeviceToDevice, m.stream));
+    if (has_right)
+      HIP_CHECK(hipMemcpyAsync(m.halo_recv[1], g.send_l[m.rank + 1], (size_t)cnt * sizeof(real),
+                               hipMemcpyDeviceToDevice, m.stream));
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    g.barrier();
+  } else {
   NCCL_CHECK(ncclGroupStart());
   if (has_left) {
     NCCL_CHECK(ncclSend(m.halo_send[0], cnt, ncclDouble, m.rank - 1, m.comm, m.stream));
@@ -846,6 +893,7 @@ void DeviceSolver::exchange(int group) {
     NCCL_CHECK(ncclRecv(m.halo_recv[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
   }
   NCCL_CHECK(ncclGroupEnd());
+  }
   if (has_left) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, 0, ny, m.halo_recv[0]);
   if (has_right) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, h.nx - 1, ny, m.halo_recv[1]);
 }
@@ -944,10 +992,19 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
   }
-  if (m.comm && m.nranks > 1) {
+  if ((m.comm || m.local) && m.nranks > 1) {
     // global dt: MIN over ranks, in place on the next slot
     real* dslot = (real*)&m.sc->dt_bits[slot_next];
-    NCCL_CHECK(ncclAllReduce(dslot, dslot, 1, ncclDouble, ncclMin, m.comm, st));
+    if (m.comm) {
+      NCCL_CHECK(ncclAllReduce(dslot, dslot, 1, ncclDouble, ncclMin, m.comm, st));
+    } else {
+      double v;
+      HIP_CHECK(hipMemcpyAsync(&v, dslot, sizeof v, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+      v = m.local->reduce(m.rank, v, 0);
+      HIP_CHECK(hipMemcpyAsync(dslot, &v, sizeof v, hipMemcpyHostToDevice, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+    }
     exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE);
   }
   if (!cs.cfg.isAdiabaticWall) {

@@ -1,14 +1,56 @@
 // DeviceSolver: MI355X backend of the DEEPS time march (see device_solver.hip).
 #pragma once
 
+#include <algorithm>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../core/solver.hpp"
 
 namespace hf2d {
 
 bool gpu_available();
+
+// In-process stand-in for the RCCL communicator: N DeviceSolvers (one host
+// thread each, possibly sharing one GPU) exchange halo buffers with D2D
+// copies and reduce scalars on the host.  Same call sites and pack layout as
+// the RCCL path; lets the strip decomposition be verified on a single GPU
+// (RCCL refuses two ranks on one device).
+struct LocalGroup {
+  explicit LocalGroup(int n_) : n(n_), send_l(n_), send_r(n_), vals(n_), packs(n_) {}
+  int n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  long gen = 0;
+  std::vector<real*> send_l, send_r;
+  std::vector<double> vals;
+  std::vector<ResidualPack> packs;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const long g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+  double reduce(int rank, double v, int op) {   // 0 min, 1 sum, 2 max
+    vals[rank] = v;
+    barrier();
+    double r = vals[0];
+    for (int q = 1; q < n; q++) r = op == 0 ? std::min(r, vals[q]) : op == 1 ? r + vals[q] : std::max(r, vals[q]);
+    barrier();
+    return r;
+  }
+};
+
+std::shared_ptr<LocalGroup> make_local_group(int n);
 
 class DeviceSolver : public SolverBase {
  public:
@@ -27,6 +69,8 @@ class DeviceSolver : public SolverBase {
   // Multi-GPU: RCCL communicator over the strip ranks.
   static std::string nccl_unique_id();
   void init_comm(const std::string& uid, int rank, int nranks);
+  // in-process virtual ranks (tests on one GPU; see LocalGroup)
+  void init_local(std::shared_ptr<LocalGroup> g, int rank);
   int comm_rank() const;
   int comm_size() const;
   void exchange(int group);

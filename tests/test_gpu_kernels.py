@@ -110,3 +110,64 @@ def test_lean_bitwise_with_switches(gpu):
         np.testing.assert_allclose(sg["rms"], sc["rms"], rtol=1e-12, atol=0)
         for f in FIELDS + ["k", "R", "CP"]:
             np.testing.assert_array_equal(g.field(f), c.field(f), err_msg=f)
+
+
+def _virtual_ranks(hf, text, nranks, schedule, lean=True):
+    """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
+    host thread each, halos through the in-process LocalGroup transport."""
+    import threading
+
+    from openhyperflow2d_amd.parallel.strips import balanced_columns
+
+    nat = hf.native()
+    cases = [nat.Case.from_deck(text, ".", False) for _ in range(nranks)]
+    parts = balanced_columns(np.asarray(cases[0].field("solid")), nranks)
+    group = nat.LocalGroup(nranks)
+    solvers = []
+    for r, (a, b) in enumerate(parts):
+        s = nat.DeviceSolver(cases[r], 0, a, b)
+        s.lean = lean
+        s.init_local(group, r)
+        solvers.append(s)
+    errors = []
+
+    def run(s, n, res):
+        try:
+            s.run_steps(n, res)
+        except Exception as e:   # pragma: no cover - reported below
+            errors.append(e)
+
+    for n, res in schedule:
+        th = [threading.Thread(target=run, args=(s, n, res), daemon=True) for s in solvers]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errors, errors
+        assert not any(t.is_alive() for t in th), "virtual-rank step hung"
+    out = {}
+    for f in FIELDS:
+        full = None
+        for r, (a, b) in enumerate(parts):
+            solvers[r].download()
+            fr = np.asarray(cases[r].field(f))
+            if full is None:
+                full = np.zeros_like(fr)
+            full[a:b] = fr[a:b]
+        out[f] = full
+    return out, dict(solvers[0].summary())
+
+
+@pytest.mark.parametrize("nranks,physics,lean", [(2, "euler", True), (3, "euler", True), (2, "euler", False),
+                                                 (3, "kes", False)])
+def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
+    ns = physics != "euler"
+    text = decks.wedge15(240, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
+    schedule = [(5, True), (6, False), (5, True)]
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean)
+    ref = gpu.Simulation(text, "gpu", lean=lean)
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
