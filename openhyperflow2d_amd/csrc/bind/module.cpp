@@ -223,6 +223,8 @@ PYBIND11_MODULE(_hf2d, m) {
   py::class_<CpuSolver, SolverBase>(m, "CpuSolver")
       .def_readwrite("lean", &CpuSolver::lean)
       .def_readwrite("lean_tile", &CpuSolver::lean_tile)
+      .def_readwrite("lean_sg", &CpuSolver::lean_sg)
+      .def_readonly("lean_sg_ok", &CpuSolver::lean_sg_ok)
       .def_readonly("lean_ok", &CpuSolver::lean_ok)
       .def_readonly("lean_why", &CpuSolver::lean_why)
       .def(py::init<Case&, int, int>(), py::arg("case"), py::arg("gi0") = 0, py::arg("gi1") = -1,
@@ -272,6 +274,10 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("fused", &DeviceSolver::fused)
       .def_readwrite("lean", &DeviceSolver::lean)
       .def_readwrite("lean_tile", &DeviceSolver::lean_tile)
+      .def_readwrite("lean_sg", &DeviceSolver::lean_sg)
+      .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
+      .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },
+                    [](DeviceSolver& d, bool on) { d.set_lean_plain(on); })
       .def_readonly("lean_ok", &DeviceSolver::lean_ok)
       .def_readonly("lean_why", &DeviceSolver::lean_why)
       .def_readonly("gi0", &DeviceSolver::gi0)

@@ -1,5 +1,6 @@
 // Host side of the lean inviscid path (lean_euler.hpp): eligibility and the
 // per-cell neighbour/publish byte.
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -32,11 +33,30 @@ bool lean_eligible(const Case& cs, std::string* why) {
   return true;
 }
 
+bool lean_single_gas(const Case& cs) {
+  static const real zero = 0.0;
+  for (const CellRecord& c : cs.J.c)
+    for (int k = 4; k < 4 + NCOMP; k++)
+      if (std::memcmp(&c.S[k], &zero, sizeof(real)) != 0) return false;   // +0 only
+  return true;
+}
+
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {
   const long N = h.N;
   const int ny = h.ny;
   std::vector<uint8_t> lb(N);
   for (long idx = 0; idx < N; idx++) lb[idx] = h.nb[idx] & (NB_XL | NB_XR | NB_YU | NB_YD);
+  // flag-free interior nodes (predict_core PLAIN fast path)
+  for (long idx = 0; idx < N; idx++) {
+    const u64 CT = h.CT[idx];
+    if (!is_active(CT) || (h.nb[idx] & 15) != 15 || has_all(CT, CT_NONREFLECTED)) continue;
+    bool plain = true;
+    for (int k = 0; k < 4 + NCOMP && plain; k++) {
+      const EqFlags f = eq_flags(k, CT, h.TT[idx], sm);
+      plain = f.upd && f.dx && f.dy && !f.dx2 && !f.dy2 && !pass2_frozen(k, CT, h.TT[idx], sm);
+    }
+    if (plain) lb[idx] |= LB_PLAIN;
+  }
   // a node whose predictor applies d2S/dx2 = 0 reads dS/dx of its x
   // neighbours (likewise y): those neighbours must keep publishing dS/dx.
   for (int i = 0; i < h.nx; i++)

@@ -19,6 +19,14 @@
 // (FROM_GENERIC), and lean_materialize_cell() rebuilds A/B/F/p before any
 // generic step.
 //
+// Single-gas specialisation (SG): when every node's fuel/oxidiser/product
+// partial densities are +0 (air-only decks: all the reference test cases),
+// they stay +0 bit for bit under predictor, fill and Zeldovich chemistry (the
+// species fluxes are +-0, the LxF update yields +0, chemistry maps Y to
+// (0,0,0,1) and stores fabs(0 * rho)), so the species equations, their
+// pre-chemistry copies and betas need not be touched at all; the mixture
+// terms reduce to R = R_air, Cp = Cp_air(T).  lean_single_gas() checks it.
+//
 // Eligibility (lean_eligible() on the host): inviscid, no gas sources,
 // adiabatic walls, Src == 0 everywhere, SrcAdd == 0 except on no-slip nodes
 // (whose SrcAdd lives in its array), every non-solid node set.
@@ -29,7 +37,9 @@
 namespace hf2d {
 
 // per-cell lean byte: neighbour bits (NB_*) | who must publish dS/dx, dS/dy
-enum : uint8_t { LB_DX_OUT = 16, LB_DY_OUT = 32 };
+// LB_PLAIN: interior node on the flag-free predictor fast path (predict_core
+// PLAIN) -- set on the host by lean_flags().
+enum : uint8_t { LB_DX_OUT = 16, LB_DY_OUT = 32, LB_PLAIN = 64 };
 
 struct LeanSoA {
   long N = 0;
@@ -88,6 +98,31 @@ HF_HD inline real lean_flux_B(const LeanSoA& L, int k, long at, real u, real v, 
   }
 }
 
+// The node's own per-step inputs that live in global memory, loaded up front
+// (the tiled kernel issues these loads before its LDS barrier).
+struct LeanOwn {
+  u64 CT = 0;
+  uint8_t lb = 0;
+  bool filled = false;   // set and not solid
+  real beta[4 + NCOMP];
+  real CP = 0, R = 0, kk = 0;
+};
+
+template <int NE = 4 + NCOMP>
+HF_HD inline void lean_load_own(const LeanSoA& L, long idx, LeanOwn& o) {
+  const long N = L.N;
+  o.CT = L.CT[idx];
+  o.lb = L.lb[idx];
+  o.filled = !has_all(o.CT, CT_SOLID) && has_all(o.CT, CT_NODE_IS_SET);
+  if (o.filled) {
+#pragma unroll
+    for (int k = 0; k < NE; k++) o.beta[k] = L.beta[k * N + idx];
+    o.CP = L.CP[idx];
+    o.R = L.R[idx];
+    o.kk = L.kk[idx];
+  }
+}
+
 // Accessor members shared by the global-memory and the LDS-tile IO: the
 // node's own persistent arrays (beta, dS/dx, dS/dy, SrcAdd) stay in global
 // memory, addressed by the global indices idx / iL / iR / iU / iD.
@@ -98,6 +133,7 @@ struct LeanIOCommon {
   uint8_t lb = 0;
   bool noslip = false;
   real FT = 0;
+  const real* obeta = nullptr;   // LeanOwn::beta
   real sm[NEQ];
 
   HF_HD LeanIOCommon(const LeanSoA& l, long i) : L(l), N(l.N), idx(i), iL(i), iR(i), iU(i), iD(i) {}
@@ -111,7 +147,7 @@ struct LeanIOCommon {
   HF_HD real dxR(int k) const { return L.dSdx_in[k * N + iR]; }
   HF_HD real dyU(int k) const { return L.dSdy_in[k * N + iU]; }
   HF_HD real dyD(int k) const { return L.dSdy_in[k * N + iD]; }
-  HF_HD real beta(int k) const { return L.beta[k * N + idx]; }
+  HF_HD real beta(int k) const { return obeta[k]; }
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int k) const { return noslip ? L.SrcAdd[k * N + idx] : 0.0; }
   HF_HD void put_S(int k, real v) { sm[k] = v; }
@@ -184,18 +220,33 @@ struct LeanChemNode {
   u64 CT;
 };
 
+// chemistry_zeldovich() evaluated for a node whose species partial densities
+// are +0: Y = (0, 0, 0, 1), R = R_air, Cp = Cp_air(T) (each zero-fraction term
+// of the mixture sums is +0, so the sums reduce to the air term exactly).
+template <class N>
+HF_HD inline void chemistry_single_gas(N& n, const SpeciesProps& sp) {
+  n.R = ((sp.R[H_FU] * 0. + sp.R[H_OX] * 0.) + sp.R[H_CP] * 0.) + sp.R[H_AIR] * 1.;
+  n.CP = table_eval(sp.Cp[H_AIR], n.Tg) * 1.;
+  n.Y[0] = n.Y[1] = n.Y[2] = 0.;
+  n.Y[3] = 1.;
+}
+
 // One lean step of cell (i, j) through accessor `io` (constructed on idx).
 // Returns the local dt limit (1.0 if none).
-template <bool RES, class IO>
-HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i, int j, ResidualPack& res,
-                            int* neg_T) {
+// OUT: also write the output-only fields (Tg, k, Y); the solver requests them
+// on the last step before control returns to the host (downloads, outputs).
+template <bool RES, bool OUT, class IO>
+HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const LeanOwn& own, int i, int j,
+                            ResidualPack& res, int* neg_T) {
   const long N = L.N;
   const long idx = io.idx;
-  const u64 CT = L.CT[idx];
-  const uint8_t lb = L.lb[idx];
-  constexpr int NE = 4 + NCOMP;
+  const u64 CT = own.CT;
+  const uint8_t lb = own.lb;
+  constexpr int NE = IO::NE;              // transported equations touched
+  constexpr bool SG = IO::NE == 4;        // single-gas specialisation
   io.lb = lb;
-  if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
+  io.obeta = own.beta;
+  if (!own.filled) {
     // neither transported nor filled: carry the state into the other buffers
     for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = io.S(k);
     if (lb & LB_DX_OUT)
@@ -215,7 +266,10 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
     io.set_nb(i, j, P.ny, n1, n2, n3, n4);
     // Equations >= NE are frozen for inviscid cells: TurbType only matters
     // through num_eq_for(), which is >= NE for every model.
-    predict_core<RES>(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
+    if (lb & LB_PLAIN)
+      predict_core<RES, IO, true>(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
+    else
+      predict_core<RES, IO, false>(P, io, CT, (u64)0, n1, n2, n3, n4, P.gx0 + i, j, res);
     if (lb & (LB_DX_OUT | LB_DY_OUT))
       for (int k = NE; k < NEQ; k++) io.keep_dS(k);
   } else {
@@ -227,20 +281,21 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
   // ---- FillNode2D, inviscid subset (fill_node) ----
   LeanChemNode c;
   for (int k = 0; k < NE; k++) c.S[k] = io.sm[k];
-  c.S[NE] = c.S[NE + 1] = 0.;
+  for (int k = NE; k < NEQ; k++) c.S[k] = 0.;
   real* s = c.S;
   // NT_FC nodes are filled with FillNode2D(1, 0, ...) (P.ffc): it differs
   // from P.fpa only in is_mu_t / is_init, which the inviscid fill never reads.
   // (A runtime-selected reference into the kernel-argument block would force
   // a scratch copy of StepParams.)
   const FillParams& F = P.fpa;
-  c.R = L.R[idx];
-  c.CP = L.CP[idx];
-  const real k_old = L.kk[idx];
+  c.R = own.R;
+  c.CP = own.CP;
+  const real k_old = own.kk;
   if (s[I_RHO] == 0 || k_old < 1) {
     // fill_node() skipped the node: keep the previous primitives
     for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = s[k];
-    for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
+    if (!SG)
+      for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
     L.Uout[idx] = u_old;
     L.Vout[idx] = v_old;
     L.Pout[idx] = io.P0();
@@ -296,7 +351,8 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
   const real p = (kk - 1.) * (s[I_RHOE] - s[I_RHO] * (U * U + V * V) * 0.5 - Tmp3);
   const real Tg = p / c.R / s[I_RHO];
   // fluxes of this fill are built from the pre-chemistry species
-  for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
+  if (!SG)
+    for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
   real dt_local = 1.0;
   if (active) {
     if (Tg < 0.) {
@@ -309,10 +365,15 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
         c.Tf = L.Tf[idx];
         c.CT = CT;
         c.lam = c.mu = 0.;
-        chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
-        L.R[idx] = c.R;
+        if (SG)
+          chemistry_single_gas(c, *P.species);
+        else
+          chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
+        if (c.R != own.R) L.R[idx] = c.R;   // constant for a frozen mixture
         L.CP[idx] = c.CP;
-        for (int q = 0; q < NSPEC; q++) L.Y[q * N + idx] = c.Y[q];
+        // Y is output-only except for the no-slip SrcAdd of the next step
+        if (OUT || noslip)
+          for (int q = 0; q < NSPEC; q++) L.Y[q * N + idx] = c.Y[q];
       }
     }
   }
@@ -320,8 +381,10 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
   L.Uout[idx] = U;
   L.Vout[idx] = V;
   L.Pout[idx] = p;
-  L.Tout[idx] = Tg;
-  L.kk[idx] = kk;
+  if (OUT) {
+    L.Tout[idx] = Tg;
+    L.kk[idx] = kk;
+  }
   return dt_local;
 }
 
@@ -334,6 +397,8 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, int i
 // k / flags come straight from global memory (read once).
 // ---------------------------------------------------------------------------
 constexpr int LEAN_TILE_FIELDS = 13;   // S[0..6], Spre[0..2], U, V, p
+constexpr int LEAN_TILE_FIELDS_SG = 7; // single gas: S[0..3], U, V, p
+inline int lean_tile_fields(bool sg) { return sg ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS; }
 constexpr int LEAN_TILE_MIN_TJ = 8;
 
 struct LeanTile {
@@ -354,10 +419,13 @@ inline LeanTile lean_tile_geom(int ncols, int ny, int block) {
 
 // Thread t of nthreads stages its share of tile (i0, j0).  LDS layout:
 // lds[f * NC + c], c = (ii + 1) * W + (jj + 1), ii in [-1, TI], jj in [-1, TJ].
+template <bool SG = false>
 HF_HD inline void lean_tile_stage(const StepParams& P, const LeanSoA& L, const LeanTile& T, int i0, int j0,
                                   real* lds, int t, int nthreads) {
   const long N = L.N;
   const int NC = T.NC;
+  constexpr int NS = SG ? 4 : 4 + NCOMP;          // staged state equations
+  constexpr int FU = SG ? 4 : 10;                 // U, V, p field slots
   for (int c = t; c < NC; c += nthreads) {
     const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
     const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
@@ -365,25 +433,29 @@ HF_HD inline void lean_tile_stage(const StepParams& P, const LeanSoA& L, const L
     if ((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
     const long g = (long)gi * P.ny + gj;
 #pragma unroll
-    for (int f = 0; f < 4 + NCOMP; f++) lds[f * NC + c] = L.Sin[f * N + g];
+    for (int f = 0; f < NS; f++) lds[f * NC + c] = L.Sin[f * N + g];
+    if (!SG)
 #pragma unroll
-    for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + c] = L.Pin_s[f * N + g];
-    lds[10 * NC + c] = L.Uin[g];
-    lds[11 * NC + c] = L.Vin[g];
-    lds[12 * NC + c] = L.Pin[g];
+      for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + c] = L.Pin_s[f * N + g];
+    lds[FU * NC + c] = L.Uin[g];
+    lds[(FU + 1) * NC + c] = L.Vin[g];
+    lds[(FU + 2) * NC + c] = L.Pin[g];
   }
 }
 
+template <bool SG = false>
 struct TileIO : LeanIOCommon {
+  static constexpr int NE = SG ? 4 : 4 + NCOMP;
+  static constexpr int FU = SG ? 4 : 10, FV = FU + 1, FP = FU + 2;
   const real* lds;
   int NC, W, c, cL, cR, cU, cD;
 
   HF_HD TileIO(const LeanSoA& l, long i, const real* s, int nc, int w, int cc)
       : LeanIOCommon(l, i), lds(s), NC(nc), W(w), c(cc), cL(cc), cR(cc), cU(cc), cD(cc) {}
   HF_HD real at(int f, int cc) const { return lds[f * NC + cc]; }
-  HF_HD real U0() const { return at(10, c); }
-  HF_HD real V0() const { return at(11, c); }
-  HF_HD real P0() const { return at(12, c); }
+  HF_HD real U0() const { return at(FU, c); }
+  HF_HD real V0() const { return at(FV, c); }
+  HF_HD real P0() const { return at(FP, c); }
   HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
     set_nb_global(i, j, ny, n1, n2, n3, n4);
     cL = c - n1 * W;
@@ -397,7 +469,7 @@ struct TileIO : LeanIOCommon {
   HF_HD real SU(int k) const { return at(k, cU); }
   HF_HD real SD(int k) const { return at(k, cD); }
   HF_HD real fA(int k, int cc) const {
-    const real u = at(10, cc), p = at(12, cc);
+    const real u = at(FU, cc), p = at(FP, cc);
     switch (k) {
       case I_RHO: return at(1, cc);
       case I_RHOU: return p + at(1, cc) * u;
@@ -407,7 +479,7 @@ struct TileIO : LeanIOCommon {
     }
   }
   HF_HD real fB(int k, int cc) const {
-    const real u = at(10, cc), v = at(11, cc), p = at(12, cc);
+    const real u = at(FU, cc), v = at(FV, cc), p = at(FP, cc);
     switch (k) {
       case I_RHO: return at(2, cc);
       case I_RHOU: return at(2, cc) * u;
@@ -448,17 +520,22 @@ HF_HD inline bool lean_tile_cell(const StepParams& P, const LeanTile& T, int b, 
 template <bool RES, bool FROMG>
 HF_HD inline real lean_euler_cell(const StepParams& P, const LeanSoA& L, int i, int j, ResidualPack& res,
                                   int* neg_T) {
-  LeanIO<FROMG> io(L, (long)i * P.ny + j);
-  return lean_cell<RES>(P, L, io, i, j, res, neg_T);
+  const long idx = (long)i * P.ny + j;
+  LeanOwn own;
+  lean_load_own(L, idx, own);
+  LeanIO<FROMG> io(L, idx);
+  return lean_cell<RES, true>(P, L, io, own, i, j, res, neg_T);
 }
 
 // host convenience: nullable residual pack
 template <class IO>
 inline real lean_cell_host(const StepParams& P, const LeanSoA& L, IO& io, int i, int j, ResidualPack* res,
                            int* neg_T) {
-  if (res) return lean_cell<true>(P, L, io, i, j, *res, neg_T);
+  LeanOwn own;
+  lean_load_own<IO::NE>(L, io.idx, own);
+  if (res) return lean_cell<true, true>(P, L, io, own, i, j, *res, neg_T);
   ResidualPack d;
-  return lean_cell<false>(P, L, io, i, j, d, neg_T);
+  return lean_cell<false, true>(P, L, io, own, i, j, d, neg_T);
 }
 
 // Rebuild the generic per-node fluxes (A, B, F) and p from the lean state,

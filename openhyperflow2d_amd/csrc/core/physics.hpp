@@ -483,13 +483,20 @@ HF_HD inline void chemistry_zeldovich(N& n, const SpeciesProps& sp, int sm, int 
   }
   const real T = n.Tg;
   n.R = sp.R[H_FU] * Yfu + sp.R[H_OX] * Yox + sp.R[H_CP] * Ycp + sp.R[H_AIR] * Yair;
-  n.CP = table_eval(sp.Cp[H_FU], T) * Yfu + table_eval(sp.Cp[H_OX], T) * Yox +
-         table_eval(sp.Cp[H_CP], T) * Ycp + table_eval(sp.Cp[H_AIR], T) * Yair;
+  // mix(tables, Y): sum_s table_s(T) * Y_s.  A species with Y_s == 0
+  // contributes +0 for any finite table value, so its table lookup is skipped
+  // (identical result; saves the linear searches for single-gas flows).
+  auto mix = [&](const TableData* t) {
+    const real a = Yfu != 0 ? table_eval(t[H_FU], T) * Yfu : 0.;
+    const real b = Yox != 0 ? table_eval(t[H_OX], T) * Yox : 0.;
+    const real c = Ycp != 0 ? table_eval(t[H_CP], T) * Ycp : 0.;
+    const real d = Yair != 0 ? table_eval(t[H_AIR], T) * Yair : 0.;
+    return a + b + c + d;
+  };
+  n.CP = mix(sp.Cp);
   if (sm == SM_NS) {
-    n.lam = table_eval(sp.lam[H_FU], T) * Yfu + table_eval(sp.lam[H_OX], T) * Yox +
-            table_eval(sp.lam[H_CP], T) * Ycp + table_eval(sp.lam[H_AIR], T) * Yair;
-    n.mu = table_eval(sp.mu[H_FU], T) * Yfu + table_eval(sp.mu[H_OX], T) * Yox +
-           table_eval(sp.mu[H_CP], T) * Ycp + table_eval(sp.mu[H_AIR], T) * Yair;
+    n.lam = mix(sp.lam);
+    n.mu = mix(sp.mu);
   }
   if (Yair < 1.e-5) Yair = 0.;
   if (Ycp < 1.e-8) Ycp = 0.;

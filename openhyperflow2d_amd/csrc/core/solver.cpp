@@ -290,8 +290,10 @@ void SolverBase::run_steps(long n, bool want_res_last) {
       isSrcAdd = true;
       cycle++;
     }
+    step_outputs = s == n - 1;   // the host may read the full record afterwards
     advance(want_res_last && s == n - 1);
   }
+  step_outputs = true;
   sync_scalars();
 }
 
@@ -330,7 +332,9 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
     for (long k = 0; k < C.Nmax; k++) {
       const bool out_step = (iter / C.NOutStep) * C.NOutStep == iter;
       const long this_iter = iter;
+      step_outputs = out_step || k == C.Nmax - 1;
       advance(out_step || k == C.Nmax - 1);
+      step_outputs = true;
       if (out_step) {
         if (!C.monitors.empty()) sample_monitors(C.monitors);
         if (C.isVerboseOutput && root) {
@@ -430,6 +434,7 @@ void CpuSolver::upload() {
   dsbuf = 0;
   pbuf = 0;
   lean_ok = lean_eligible(cs, &lean_why);
+  lean_sg_ok = lean_ok && lean_single_gas(cs);
   lean_state = 0;
   if (lean_ok) {
     lb = lean_flags(h, cs.cfg.ProblemType);
@@ -585,16 +590,27 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
       // indexing); unstaged LDS entries are poisoned with NaN
       constexpr int NT = 256;
       const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, NT);
-      std::vector<real> lds((size_t)LEAN_TILE_FIELDS * T.NC);
+      const bool sg = lean_sg && lean_sg_ok;
+      std::vector<real> lds((size_t)lean_tile_fields(sg) * T.NC);
       for (int b = 0; b < T.nbi * T.nbj; b++) {
         std::fill(lds.begin(), lds.end(), std::numeric_limits<real>::quiet_NaN());
         int i, j, c, i0, j0;
         lean_tile_cell(P, T, b, 0, &i, &j, &c, &i0, &j0);
-        for (int t = 0; t < NT; t++) lean_tile_stage(P, L, T, i0, j0, lds.data(), t, NT);
+        for (int t = 0; t < NT; t++) {
+          if (sg)
+            lean_tile_stage<true>(P, L, T, i0, j0, lds.data(), t, NT);
+          else
+            lean_tile_stage<false>(P, L, T, i0, j0, lds.data(), t, NT);
+        }
         for (int t = 0; t < NT; t++) {
           if (!lean_tile_cell(P, T, b, t, &i, &j, &c, &i0, &j0)) continue;
-          TileIO io(L, (long)i * P.ny + j, lds.data(), T.NC, T.W, c);
-          dtmin = std::min(dtmin, lean_cell_host(P, L, io, i, j, rp, &negT));
+          if (sg) {
+            TileIO<true> io(L, (long)i * P.ny + j, lds.data(), T.NC, T.W, c);
+            dtmin = std::min(dtmin, lean_cell_host(P, L, io, i, j, rp, &negT));
+          } else {
+            TileIO<false> io(L, (long)i * P.ny + j, lds.data(), T.NC, T.W, c);
+            dtmin = std::min(dtmin, lean_cell_host(P, L, io, i, j, rp, &negT));
+          }
         }
       }
     } else {

@@ -74,6 +74,9 @@ class SolverBase {
   virtual ~SolverBase() = default;
 
   Case& cs;
+  // false: the backend may skip output-only fields on this step (the host
+  // will not read the record before the next step)
+  bool step_outputs = true;
   Comm* comm = nullptr;      // owned elsewhere
   Comm local_comm;
   real dt = 0;               // dt used by the next step
@@ -111,6 +114,7 @@ class SolverBase {
 
 // lean inviscid path (lean.cpp)
 bool lean_eligible(const Case& cs, std::string* why);
+bool lean_single_gas(const Case& cs);
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);
 
 class CpuSolver : public SolverBase {
@@ -141,6 +145,8 @@ class CpuSolver : public SolverBase {
   // oracle the device kernels are checked against)
   bool lean = false;
   bool lean_tile = false;   // emulate the device's LDS-tiled lean kernel
+  bool lean_sg = true;      // single-gas specialisation when the case allows it
+  bool lean_sg_ok = false;
   bool lean_ok = false;
   std::string lean_why;
   int lean_state = 0;   // 1: lean arrays authoritative, A/B/F/p stale

@@ -182,21 +182,28 @@ HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, rea
 //   beta(k) F(k) Src(k) SrcAdd(k)
 //   put_S(k, v) put_beta(k, v) put_dS(k, dsdx, dsdy) keep_dS(k)
 // ---------------------------------------------------------------------------
-template <bool RES, class IO>
+//
+// PLAIN: the caller guarantees an interior node whose IO::NE equations are
+// all transported with plain flux differences (no Dirichlet / Neumann /
+// Cauchy bit, not frozen in pass 2, all four neighbours present, not
+// non-reflecting).  The flags then fold to constants; the arithmetic is the
+// same, so the result is bit-identical to the general path.
+template <bool RES, class IO, bool PLAIN = false>
 HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int n1, int n2, int n3, int n4, int gi,
                                int j, ResidualPack& rp) {
   // RES is a template flag (not a nullable pointer) so the device kernels
   // keep the residual pack in registers.
-
+  if (PLAIN) n1 = n2 = n3 = n4 = 1;
   const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
   const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
-  const int Num_Eq = num_eq_for(TT);
+  const int Num_Eq = PLAIN ? NEQ : num_eq_for(TT);
   const bool axi = P.fpa.FT != 0;
 #pragma unroll
   for (int k = 0; k < IO::NE; k++) {
     real s = io.S(k);
-    const EqFlags f = eq_flags(k, CT, TT, P.sm);
-    if (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT)))) {
+    const EqFlags f = PLAIN ? EqFlags{true, true, true, false, false} : eq_flags(k, CT, TT, P.sm);
+    if (!PLAIN &&
+        (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT))))) {
       // A TCT-frozen turbulence equation whose CT-based pass-2 test says
       // "not frozen" (quirk Q4) is scored against the never-written
       // predictor scratch (0) in the reference: DD = 1, dS = -S.
@@ -257,16 +264,17 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
              (io.Src(k)) * P.dt + io.SrcAdd(k);
     io.put_dS(k, dsdx, dsdy);
     // pass 2a: residual + blending factor
-    if (!pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
+    if ((PLAIN || !pass2_frozen(k, CT, TT, P.sm)) && s != 0.) {
       const real absDD = snew - s;
       real DD, sqrt_res = 0;
       if (std::fabs(s) > 1.e-15) {
         DD = std::fabs(absDD / s);
-        sqrt_res = std::sqrt(DD);
+        // only the square-root blending variants read it (uniform branch)
+        if (P.bff == BFF_SQR || P.bff == BFF_SQRR) sqrt_res = std::sqrt(DD);
       } else {
         DD = 1.0;
       }
-      const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
+      const real bmin = (!PLAIN && has_all(CT, CT_NONREFLECTED)) ? P.nrbc_beta0 : P.beta_min;
       io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, sqrt_res));
       if (RES) {
         EqResidual& e = rp.eq[k];

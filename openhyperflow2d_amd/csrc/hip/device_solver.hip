@@ -274,7 +274,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
 }
 
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
-template <bool RES>
+template <bool RES, bool OUT, bool SG>
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
                                                          int slot, int slot_next, int serial,
                                                          ResidualPack* partials) {
@@ -287,7 +287,10 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
   }
   int i, j, c, i0, j0;
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
-  lean_tile_stage(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
+  // own-cell global inputs first, so they are in flight during the staging
+  LeanOwn own;
+  if (mine) lean_load_own<TileIO<SG>::NE>(L, (long)i * P.ny + j, own);
+  lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
   __syncthreads();
   ResidualPack r;
   if (RES) {
@@ -298,8 +301,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
   double dtl = 1.0;
   int neg = 0;
   if (mine) {
-    TileIO io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
-    dtl = lean_cell<RES>(P, L, io, i, j, r, &neg);
+    TileIO<SG> io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
+    dtl = lean_cell<RES, OUT>(P, L, io, own, i, j, r, &neg);
   }
   if (RES) {
 #pragma unroll
@@ -652,8 +655,11 @@ void DeviceSolver::upload() {
   cp(m.TT, h.TT.data(), N * sizeof(u64));
   cp(m.nb, h.nb.data(), N);
   lean_ok = lean_eligible(cs, &lean_why);
+  lean_sg_ok = lean_ok && lean_single_gas(cs);
   if (lean_ok) {
     lean_bytes = lean_flags(h, cs.cfg.ProblemType);
+    if (!lean_plain)
+      for (auto& b : lean_bytes) b &= (uint8_t)~LB_PLAIN;
     cp(m.lb, lean_bytes.data(), N);
   }
   lean_state = 0;
@@ -677,6 +683,17 @@ void DeviceSolver::upload() {
   sbuf = 0;
   dsbuf = 0;
   pbuf = 0;
+}
+
+void DeviceSolver::set_lean_plain(bool on) {
+  lean_plain = on;
+  if (!lean_ok) return;
+  std::vector<uint8_t> b = lean_flags(h, cs.cfg.ProblemType);
+  if (!on)
+    for (auto& x : b) x &= (uint8_t)~LB_PLAIN;
+  lean_bytes = b;
+  HIP_CHECK(hipMemcpyAsync(impl->lb, lean_bytes.data(), lean_bytes.size(), hipMemcpyHostToDevice, impl->stream));
+  HIP_CHECK(hipStreamSynchronize(impl->stream));
 }
 
 void DeviceSolver::lean_materialize() {
@@ -919,13 +936,28 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
     const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK);
     const unsigned ntile = (unsigned)(T.nbi * T.nbj);
-    const size_t shmem = (size_t)LEAN_TILE_FIELDS * T.NC * sizeof(real);
-    if (want_res)
-      hipLaunchKernelGGL(hf2d_lean_tile<true>, dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
-                         serial, m.partials);
-    else
-      hipLaunchKernelGGL(hf2d_lean_tile<false>, dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
-                         serial, m.partials);
+    const bool sg = lean_sg && lean_sg_ok;
+    const size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
+    const bool out = step_outputs || want_res;
+#define HF2D_LEAN_TILE(R, O, G)                                                                          \
+  hipLaunchKernelGGL((hf2d_lean_tile<R, O, G>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
+                     slot_next, serial, m.partials)
+    if (sg) {
+      if (want_res)
+        HF2D_LEAN_TILE(true, true, true);
+      else if (out)
+        HF2D_LEAN_TILE(false, true, true);
+      else
+        HF2D_LEAN_TILE(false, false, true);
+    } else {
+      if (want_res)
+        HF2D_LEAN_TILE(true, true, false);
+      else if (out)
+        HF2D_LEAN_TILE(false, true, false);
+      else
+        HF2D_LEAN_TILE(false, false, false);
+    }
+#undef HF2D_LEAN_TILE
     HIP_CHECK(hipGetLastError());
     nres = ntile;
     sbuf = 1 - sbuf;

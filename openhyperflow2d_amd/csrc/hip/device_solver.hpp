@@ -85,6 +85,10 @@ class DeviceSolver : public SolverBase {
   // is eligible; takes precedence over `fused`.
   bool lean = true;
   bool lean_tile = true;  // LDS-tiled lean kernel for all but the first lean step
+  bool lean_plain = false; // flag-free predictor fast path (measured slower: off)
+  bool lean_sg = true;     // single-gas specialisation (lean_euler.hpp) if eligible
+  bool lean_sg_ok = false;
+  void set_lean_plain(bool on);
   bool lean_ok = false;
   std::string lean_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
