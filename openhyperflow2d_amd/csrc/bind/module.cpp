@@ -224,6 +224,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean", &CpuSolver::lean)
       .def_readwrite("lean_tile", &CpuSolver::lean_tile)
       .def_readwrite("lean_sg", &CpuSolver::lean_sg)
+      .def_readwrite("lean_tj", &CpuSolver::lean_tj)
+      .def_readwrite("lean_cpt", &CpuSolver::lean_cpt)
       .def_readonly("lean_sg_ok", &CpuSolver::lean_sg_ok)
       .def_readonly("lean_ok", &CpuSolver::lean_ok)
       .def_readonly("lean_why", &CpuSolver::lean_why)
@@ -275,6 +277,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean", &DeviceSolver::lean)
       .def_readwrite("lean_tile", &DeviceSolver::lean_tile)
       .def_readwrite("lean_sg", &DeviceSolver::lean_sg)
+      .def_readwrite("lean_tj", &DeviceSolver::lean_tj)
+      .def_readwrite("lean_occ", &DeviceSolver::lean_occ)
+      .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },
                     [](DeviceSolver& d, bool on) { d.set_lean_plain(on); })

@@ -589,7 +589,7 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
       // host emulation of the device's LDS-tiled kernel (same staging and
       // indexing); unstaged LDS entries are poisoned with NaN
       constexpr int NT = 256;
-      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, NT);
+      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, NT, lean_tj, lean_cpt == 2 ? 2 : 1);
       const bool sg = lean_sg && lean_sg_ok;
       std::vector<real> lds((size_t)lean_tile_fields(sg) * T.NC);
       for (int b = 0; b < T.nbi * T.nbj; b++) {
@@ -602,8 +602,8 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
           else
             lean_tile_stage<false>(P, L, T, i0, j0, lds.data(), t, NT);
         }
-        for (int t = 0; t < NT; t++) {
-          if (!lean_tile_cell(P, T, b, t, &i, &j, &c, &i0, &j0)) continue;
+        for (int t = 0; t < NT * T.CPT; t++) {
+          if (!lean_tile_cell(P, T, b, t % NT, &i, &j, &c, &i0, &j0, t / NT)) continue;
           if (sg) {
             TileIO<true> io(L, (long)i * P.ny + j, lds.data(), T.NC, T.W, c);
             dtmin = std::min(dtmin, lean_cell_host(P, L, io, i, j, rp, &negT));

@@ -274,10 +274,9 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
 }
 
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
-template <bool RES, bool OUT, bool SG>
-__global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
-                                                         int slot, int slot_next, int serial,
-                                                         ResidualPack* partials) {
+template <bool RES, bool OUT, bool SG, int CPT>
+__device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, const LeanTile& T, DevScalars* sc,
+                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
   apply_dt(P, sc, slot);
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
@@ -285,11 +284,15 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
   }
-  int i, j, c, i0, j0;
-  const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
+  int i[CPT], j[CPT], c[CPT], i0, j0;
+  bool mine[CPT];
   // own-cell global inputs first, so they are in flight during the staging
-  LeanOwn own;
-  if (mine) lean_load_own<TileIO<SG>::NE>(L, (long)i * P.ny + j, own);
+  LeanOwn own[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; q++) {
+    mine[q] = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i[q], &j[q], &c[q], &i0, &j0, q);
+    if (mine[q]) lean_load_own<TileIO<SG>::NE>(L, (long)i[q] * P.ny + j[q], own[q]);
+  }
   lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
   __syncthreads();
   ResidualPack r;
@@ -300,9 +303,12 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
   }
   double dtl = 1.0;
   int neg = 0;
-  if (mine) {
-    TileIO<SG> io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
-    dtl = lean_cell<RES, OUT>(P, L, io, own, i, j, r, &neg);
+#pragma unroll
+  for (int q = 0; q < CPT; q++) {
+    if (mine[q]) {
+      TileIO<SG> io(L, (long)i[q] * P.ny + j[q], lds, T.NC, T.W, c[q]);
+      dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, own[q], i[q], j[q], r, &neg));
+    }
   }
   if (RES) {
 #pragma unroll
@@ -320,6 +326,22 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
     if (serial) m = fmin(m, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
   }
+}
+
+// No occupancy attribute on the default kernel: the backend's own register
+// budget (94 VGPRs here) beat every explicit amdgpu_waves_per_eu we tried.
+template <bool RES, bool OUT, bool SG, int OCC = 0, int CPT = 1>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                         int slot, int slot_next, int serial,
+                                                         ResidualPack* partials) {
+  lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
+}
+
+template <bool RES, bool OUT, bool SG, int OCC, int CPT = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC)))
+void hf2d_lean_tile_occ(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
+                        ResidualPack* partials) {
+  lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
 }
 
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, LeanSoA L, SoA g, long c0, long c1) {
@@ -584,8 +606,8 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.sc = m.mem.alloc<DevScalars>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.sc_host, sizeof(DevScalars), hipHostMallocDefault));
   {
-    const LeanTile T = lean_tile_geom(gi1 - gi0, h.ny, BLOCK);
-    const long nb_tile = (long)T.nbi * T.nbj;
+    // any tile shape (lean_tj) covers >= LEAN_TILE_MIN_TJ cells per workgroup
+    const long nb_tile = (long)(gi1 - gi0 + 1) * ((h.ny + LEAN_TILE_MIN_TJ - 1) / LEAN_TILE_MIN_TJ);
     m.max_partials = std::max((N + BLOCK - 1) / BLOCK, nb_tile) * (BLOCK / WAVE);
   }
   m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
@@ -934,28 +956,47 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   unsigned nres = nblk;   // workgroups that wrote residual partials
   if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
-    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK);
+    const int cpt = lean_cpt == 2 ? 2 : 1;
+    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, cpt);
     const unsigned ntile = (unsigned)(T.nbi * T.nbj);
     const bool sg = lean_sg && lean_sg_ok;
     const size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
     const bool out = step_outputs || want_res;
-#define HF2D_LEAN_TILE(R, O, G)                                                                          \
-  hipLaunchKernelGGL((hf2d_lean_tile<R, O, G>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
+#define HF2D_LEAN_TILE(R, O, G, C)                                                                        \
+  hipLaunchKernelGGL((hf2d_lean_tile<R, O, G, 0, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
                      slot_next, serial, m.partials)
-    if (sg) {
+    // all variants of one step must use the cpt the tile geometry was built for
+    if (sg && cpt == 2) {
       if (want_res)
-        HF2D_LEAN_TILE(true, true, true);
+        HF2D_LEAN_TILE(true, true, true, 2);
       else if (out)
-        HF2D_LEAN_TILE(false, true, true);
+        HF2D_LEAN_TILE(false, true, true, 2);
       else
-        HF2D_LEAN_TILE(false, false, true);
+        HF2D_LEAN_TILE(false, false, true, 2);
+    } else if (sg) {
+      if (want_res)
+        HF2D_LEAN_TILE(true, true, true, 1);
+      else if (out)
+        HF2D_LEAN_TILE(false, true, true, 1);
+      else if (lean_occ == 6)
+        hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
+                           m.sc, slot, slot_next, serial, m.partials);
+      else
+        HF2D_LEAN_TILE(false, false, true, 1);
+    } else if (cpt == 2) {
+      if (want_res)
+        HF2D_LEAN_TILE(true, true, false, 2);
+      else if (out)
+        HF2D_LEAN_TILE(false, true, false, 2);
+      else
+        HF2D_LEAN_TILE(false, false, false, 2);
     } else {
       if (want_res)
-        HF2D_LEAN_TILE(true, true, false);
+        HF2D_LEAN_TILE(true, true, false, 1);
       else if (out)
-        HF2D_LEAN_TILE(false, true, false);
+        HF2D_LEAN_TILE(false, true, false, 1);
       else
-        HF2D_LEAN_TILE(false, false, false);
+        HF2D_LEAN_TILE(false, false, false, 1);
     }
 #undef HF2D_LEAN_TILE
     HIP_CHECK(hipGetLastError());

@@ -87,6 +87,9 @@ class DeviceSolver : public SolverBase {
   bool lean_tile = true;  // LDS-tiled lean kernel for all but the first lean step
   bool lean_plain = false; // flag-free predictor fast path (measured slower: off)
   bool lean_sg = true;     // single-gas specialisation (lean_euler.hpp) if eligible
+  int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
+  int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
+  int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
   bool lean_sg_ok = false;
   void set_lean_plain(bool on);
   bool lean_ok = false;

@@ -27,13 +27,16 @@ def _records_wo_scratch(sim):
 
 
 @pytest.mark.parametrize("name", list(_decks()))
-@pytest.mark.parametrize("tile,sg", [(False, False), (True, False), (True, True)])
-def test_lean_equals_generic(hf, name, tile, sg):
+@pytest.mark.parametrize("tile,sg,cpt,tj", [(False, False, 1, 0), (True, False, 1, 0), (True, True, 1, 0),
+                                           (True, True, 2, 0), (True, False, 2, 11)])
+def test_lean_equals_generic(hf, name, tile, sg, cpt, tj):
     text = _decks()[name]
     a = hf.Simulation(text, "cpu", lean=False)
     b = hf.Simulation(text, "cpu", lean=True)
     b.solver.lean_tile = tile
     b.solver.lean_sg = sg
+    b.solver.lean_cpt = cpt
+    b.solver.lean_tj = tj
     assert b.solver.lean_ok, b.solver.lean_why
     assert b.solver.lean_sg_ok
     for s in range(3):

@@ -23,16 +23,26 @@ def main():
     sims = {}
     for v in a.variants.split(","):
         s = hf.Simulation(text, "gpu")
-        if v == "plain":
+        for part in v.split("+")[1:]:
+            if part.startswith("tj"):
+                s.solver.lean_tj = int(part[2:])
+        v0 = v.split("+")[0]
+        if v0 == "plain":
             s.solver.lean_plain = True
-        elif v == "nosg":
+        elif v0 == "nosg":
             s.solver.lean_sg = False
-        elif v == "flat":
+        elif v0.startswith("cpt"):
+            s.solver.lean_cpt = int(v0[3:])
+        elif v0.startswith("occ"):
+            s.solver.lean_occ = int(v0[3:])
+        elif v0.startswith("tj"):
+            s.solver.lean_tj = int(v0[2:])
+        elif v0 == "flat":
             s.solver.lean_tile = False
-        elif v == "split":
+        elif v0 == "split":
             s.solver.lean = False
             s.solver.fused = False
-        elif v == "fused":
+        elif v0 == "fused":
             s.solver.lean = False
         s.step(20)
         sims[v] = s
