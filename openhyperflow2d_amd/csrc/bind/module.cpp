@@ -24,6 +24,22 @@ struct PyComm : Comm {
   std::function<double(double)> f_min, f_sum;
   std::function<int(int)> f_maxi;
   std::function<py::bytes(py::bytes)> f_res;   // allgather-of-packs, returns concatenated bytes
+  // gather(gi0, gi1, strip bytes) -> list of (gi0, gi1, bytes) on rank 0
+  std::function<py::object(int, int, py::bytes)> f_gather;
+  void gather_columns(Field& J, int gi0, int gi1) override {
+    if (!f_gather) return;
+    py::gil_scoped_acquire g;
+    const size_t col = (size_t)J.ny * sizeof(CellRecord);
+    py::object res = f_gather(gi0, gi1, py::bytes((const char*)&J.at(gi0, 0), (size_t)(gi1 - gi0) * col));
+    if (r != 0 || res.is_none()) return;
+    for (auto item : res) {
+      auto t = item.cast<py::tuple>();
+      const int a = t[0].cast<int>(), b = t[1].cast<int>();
+      std::string bytes = t[2].cast<py::bytes>();
+      if (bytes.size() != (size_t)(b - a) * col) throw std::runtime_error("gather_columns: bad strip size");
+      std::memcpy((void*)&J.at(a, 0), bytes.data(), bytes.size());
+    }
+  }
   int rank() const override { return r; }
   int size() const override { return n; }
   real allreduce_min(real v) override { return f_min ? f_min(v) : v; }
@@ -99,6 +115,11 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
+  m.def("request_stop", &request_stop, "ask a running driver to finish the cycle, write outputs and return");
+  m.def("stop_requested", &stop_requested);
+  m.def("clear_stop", &clear_stop);
+  m.def("install_signal_handlers", &install_signal_handlers,
+        "SIGINT/SIGTERM -> graceful stop of SolverBase.run (C-level, works while the GIL is released)");
 
   py::register_exception<DeckError>(m, "DeckError");
 
@@ -200,18 +221,24 @@ PYBIND11_MODULE(_hf2d, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("advance", [](SolverBase& s, bool want) { s.advance(want); }, py::arg("want_residual") = false)
       .def("run",
-           [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose) {
+           [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose,
+              const std::string& metrics) {
              RunOptions o;
+             o.metrics_path = metrics;
              o.max_cycles = max_cycles;
              o.outdir = outdir;
              o.write_outputs = outputs;
              o.write_checkpoint = checkpoint;
              std::ostringstream log;
-             int n = s.run(o, verbose ? &log : nullptr);
+             int n;
+             {
+               py::gil_scoped_release rel;   // comm callbacks re-acquire it
+               n = s.run(o, verbose ? &log : nullptr);
+             }
              return py::make_tuple(n, log.str());
            },
            py::arg("max_cycles") = 1, py::arg("outdir") = ".", py::arg("outputs") = true,
-           py::arg("checkpoint") = true, py::arg("verbose") = true)
+           py::arg("checkpoint") = true, py::arg("verbose") = true, py::arg("metrics") = "")
       .def("download", [](SolverBase& s) { s.download(s.cs.J); })
       .def("upload", &SolverBase::upload)
       .def("sync", &SolverBase::sync_scalars)
@@ -250,7 +277,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("set_exchange", [](CpuSolver& s, std::function<void(CpuSolver&, int)> f) { s.halo_exchange = f; })
       .def("set_comm",
            [](CpuSolver& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
-              std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres) {
+              std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres,
+              std::function<py::object(int, int, py::bytes)> fgather) {
              auto* c = new PyComm();
              c->r = rank;
              c->n = size;
@@ -258,8 +286,11 @@ PYBIND11_MODULE(_hf2d, m) {
              c->f_sum = fsum;
              c->f_maxi = fmaxi;
              c->f_res = fres;
+             c->f_gather = fgather;
              s.comm = c;   // leaked intentionally: lives as long as the solver
-           });
+           },
+           py::arg("rank"), py::arg("size"), py::arg("fmin"), py::arg("fsum"), py::arg("fmaxi"), py::arg("fres"),
+           py::arg("fgather") = nullptr);
 
   py::class_<RefSolver, SolverBase>(m, "RefSolver").def(py::init<Case&>(), py::keep_alive<1, 2>());
 

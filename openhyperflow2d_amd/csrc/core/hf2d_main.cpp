@@ -65,6 +65,7 @@ int main(int argc, char** argv) {
     } else
       solver.reset(new CpuSolver(cs));
     std::cout << "Start computation (" << backend << " backend)...\n" << std::flush;
+    install_signal_handlers();
     RunOptions opt;
     opt.max_cycles = cycles;
     opt.outdir = outdir;

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <limits>
 #include <chrono>
+#include <csignal>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -301,13 +302,41 @@ void SolverBase::sample_monitors(std::vector<MonitorPoint>& mp) {
   if (mp.empty()) return;
   Field& J = cs.J;
   download(J);
+  const auto own = owned_columns();
   for (auto& m : mp) {
     const int i = (int)(m.x / cs.cfg.dx), j = (int)(m.y / cs.cfg.dy);
-    if (J.in(i, j)) {
-      m.p = J.at(i, j).p;
-      m.T = J.at(i, j).Tg;
+    real p = 0, T = 0;
+    const bool mine = J.in(i, j) && i >= own.first && i < own.second;
+    if (mine) {
+      p = J.at(i, j).p;
+      T = J.at(i, j).Tg;
     }
+    if (comm->size() > 1) {   // exactly one rank owns the probe
+      p = comm->allreduce_sum(p);
+      T = comm->allreduce_sum(T);
+    } else if (!J.in(i, j)) {
+      continue;
+    }
+    m.p = p;
+    m.T = T;
   }
+}
+
+namespace {
+volatile std::sig_atomic_t g_stop = 0;
+extern "C" void hf2d_on_signal(int) { g_stop = 1; }
+}  // namespace
+
+void request_stop() { g_stop = 1; }
+bool stop_requested() { return g_stop != 0; }
+void clear_stop() { g_stop = 0; }
+void install_signal_handlers() {
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_handler = hf2d_on_signal;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGINT, &sa, nullptr);
+  sigaction(SIGTERM, &sa, nullptr);
 }
 
 int SolverBase::run(const RunOptions& opt, std::ostream* log) {
@@ -322,6 +351,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
   }
   int I = 0;
   int monitor_cond = 1;
+  bool interrupted = false;
   int cycles = 0;
   using clk = std::chrono::steady_clock;
   do {
@@ -335,6 +365,11 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
       step_outputs = out_step || k == C.Nmax - 1;
       advance(out_step || k == C.Nmax - 1);
       step_outputs = true;
+      if (out_step && comm->allreduce_max_int(stop_requested() ? 1 : 0)) {
+        interrupted = true;
+        if (log && root) *log << "\nInterrupted by user: finishing the cycle outputs and checkpoint.\n";
+        break;
+      }
       if (out_step) {
         if (!C.monitors.empty()) sample_monitors(C.monitors);
         if (C.isVerboseOutput && root) {
@@ -342,8 +377,18 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
           const double d_time = std::chrono::duration<double>(now - mark).count();
           mark = now;
           const double vcomp = d_time > 0 ? C.NOutStep / d_time : 0.;
+          if (!opt.metrics_path.empty()) {
+            std::FILE* mf = std::fopen(opt.metrics_path.c_str(), "a");
+            if (mf) {
+              std::fprintf(mf, "{\"step\": %ld, \"time\": %.17g, \"dt\": %.17g, \"max_rms\": %.17g, \"rms\": [",
+                           last_iter + this_iter, cs.global_time + cur_time_part, dt, last_res.max_rms);
+              for (int q = 0; q < NEQ; q++) std::fprintf(mf, "%s%.17g", q ? ", " : "", last_res.rms[q]);
+              std::fprintf(mf, "], \"step_per_s\": %.6g, \"mcells_it_per_s\": %.6g, \"ranks\": %d}\n", vcomp,
+                           vcomp * (double)C.MaxX * C.MaxY / 1e6, comm->size());
+              std::fclose(mf);
+            }
+          }
           if (opt.write_outputs) {
-            cs.J.nx ? void() : void();
             append_rms(rms_path, last_iter + this_iter, last_res.rms, cs, cs.J);
             if (!C.monitors.empty()) append_monitors(mon_path, cs.global_time + cur_time_part, C.monitors);
           }
@@ -366,6 +411,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
     }
     Field& J = cs.J;
     download(J);
+    if (comm->size() > 1) comm->gather_columns(J, owned_columns().first, owned_columns().second);
     step_seconds = std::chrono::duration<double>(clk::now() - t_cycle).count();
     if (root) {
       for (size_t x = 0; x < C.xcuts.size() && log; x++) {
@@ -403,7 +449,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
              << " Fx = " << x_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body)
              << " Fy = " << y_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body) << "\n";
       }
-      if (opt.write_checkpoint && comm->size() == 1) {
+      if (opt.write_checkpoint) {
         write_hf2d(dir + "/" + C.swap_file, J);
         write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
       }
@@ -412,7 +458,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
       monitor_cond = last_res.max_rms > C.ExitMonitorValue ? 1 : 0;
     else
       monitor_cond = cs.global_time < C.ExitMonitorValue ? 1 : 0;
-  } while (monitor_cond && (opt.max_cycles < 0 || cycles < opt.max_cycles));
+  } while (!interrupted && monitor_cond && (opt.max_cycles < 0 || cycles < opt.max_cycles));
   if (root && opt.write_outputs) save_field_plt(dir + "/" + C.out_file, cs, cs.J, cs.global_time, true);
   return cycles;
 }

@@ -13,6 +13,7 @@
 
 #include <functional>
 #include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -58,6 +59,10 @@ struct Comm {
   virtual void allreduce_residual(ResidualPack&) {}
   virtual int allreduce_max_int(int v) { return v; }
   virtual real allreduce_sum(real v) { return v; }
+  // Outputs of a strip-decomposed run: after every rank refreshed its own
+  // columns [gi0, gi1) of J, rank 0 receives all columns (x-major records of
+  // one column are contiguous, so a strip is one byte range).
+  virtual void gather_columns(Field& /*J*/, int /*gi0*/, int /*gi1*/) {}
 };
 
 struct RunOptions {
@@ -66,6 +71,7 @@ struct RunOptions {
   bool write_checkpoint = true;
   std::string outdir = ".";
   bool verbose = true;
+  std::string metrics_path;  // non-empty: append one JSON line per output step (metrics.jsonl)
 };
 
 class SolverBase {
@@ -107,10 +113,20 @@ class SolverBase {
   // called after an outer-cycle roll-over (cur_time_part folded into global_time)
   virtual void on_cycle_roll() {}
   StepParams make_params(long it) const;
+  // global columns [first, second) this backend owns (strip decomposition)
+  virtual std::pair<int, int> owned_columns() const { return {0, cs.J.nx}; }
 
  protected:
   bool isSrcAdd = false;
 };
+
+// Graceful stop (SIGINT / SIGTERM): the driver finishes the current step,
+// writes the cycle outputs and the checkpoint, then returns.  Multi-rank runs
+// agree on the flag at the next output step.
+void request_stop();
+bool stop_requested();
+void clear_stop();
+void install_signal_handlers();
 
 // lean inviscid path (lean.cpp)
 bool lean_eligible(const Case& cs, std::string* why);
@@ -123,6 +139,7 @@ class CpuSolver : public SolverBase {
   // each interior side.
   CpuSolver(Case& cs, int gi0 = 0, int gi1 = -1);
   StepResult do_step(const StepParams& P, bool want_res) override;
+  std::pair<int, int> owned_columns() const override { return {gi0, gi1}; }
   void download(Field& J) override;
   void upload() override;
   void cycle_update() override;

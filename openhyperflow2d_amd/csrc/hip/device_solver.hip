@@ -414,6 +414,18 @@ struct LocalHostComm : Comm {
   std::shared_ptr<LocalGroup> g;
   int r;
   LocalHostComm(std::shared_ptr<LocalGroup> g_, int r_) : g(std::move(g_)), r(r_) {}
+  void gather_columns(Field& J, int gi0, int gi1) override {
+    g->fields[r] = &J;
+    g->cols[r] = {gi0, gi1};
+    g->barrier();
+    if (r == 0)
+      for (int q = 1; q < g->n; q++) {
+        const auto c = g->cols[q];
+        std::memcpy((void*)&J.at(c.first, 0), (const void*)&g->fields[q]->at(c.first, 0),
+                    (size_t)(c.second - c.first) * J.ny * sizeof(CellRecord));
+      }
+    g->barrier();
+  }
   int rank() const override { return r; }
   int size() const override { return g->n; }
   real allreduce_min(real v) override { return g->reduce(r, v, 0); }
@@ -825,6 +837,37 @@ struct RcclHostComm : Comm {
   real allreduce_min(real v) override { return reduce1(v, ncclMin); }
   real allreduce_sum(real v) override { return reduce1(v, ncclSum); }
   int allreduce_max_int(int v) override { return (int)reduce1((double)v, ncclMax); }
+  // rank 0 receives every strip through a device staging buffer (outputs
+  // only: once per outer cycle)
+  void gather_columns(Field& J, int gi0, int gi1) override {
+    const size_t col = (size_t)J.ny * sizeof(CellRecord);
+    // column ranges of all ranks
+    int* dcols = (int*)buf;
+    int mine[2] = {gi0, gi1};
+    HIP_CHECK(hipMemcpyAsync(dcols, mine, sizeof mine, hipMemcpyHostToDevice, st));
+    NCCL_CHECK(ncclAllGather(dcols, dcols + 2, 2, ncclInt32, c, st));
+    std::vector<int> cols(2 * n);
+    HIP_CHECK(hipMemcpyAsync(cols.data(), dcols + 2, sizeof(int) * 2 * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    size_t maxb = 0;
+    for (int q = 0; q < n; q++) maxb = std::max(maxb, (size_t)(cols[2 * q + 1] - cols[2 * q]) * col);
+    char* stage = nullptr;
+    HIP_CHECK(hipMalloc((void**)&stage, std::max<size_t>(maxb, 1)));
+    if (r == 0) {
+      for (int q = 1; q < n; q++) {
+        const size_t bytes = (size_t)(cols[2 * q + 1] - cols[2 * q]) * col;
+        NCCL_CHECK(ncclRecv(stage, bytes, ncclChar, q, c, st));
+        HIP_CHECK(hipMemcpyAsync((void*)&J.at(cols[2 * q], 0), stage, bytes, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+      }
+    } else {
+      const size_t bytes = (size_t)(gi1 - gi0) * col;
+      HIP_CHECK(hipMemcpyAsync(stage, (const void*)&J.at(gi0, 0), bytes, hipMemcpyHostToDevice, st));
+      NCCL_CHECK(ncclSend(stage, bytes, ncclChar, 0, c, st));
+      HIP_CHECK(hipStreamSynchronize(st));
+    }
+    HIP_CHECK(hipFree(stage));
+  }
   void allreduce_residual(ResidualPack& p) override {
     std::vector<ResidualPack> all(n);
     char* dbuf = (char*)buf;

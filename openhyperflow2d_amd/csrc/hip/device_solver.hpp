@@ -20,7 +20,8 @@ bool gpu_available();
 // the RCCL path; lets the strip decomposition be verified on a single GPU
 // (RCCL refuses two ranks on one device).
 struct LocalGroup {
-  explicit LocalGroup(int n_) : n(n_), send_l(n_), send_r(n_), vals(n_), packs(n_) {}
+  explicit LocalGroup(int n_)
+      : n(n_), send_l(n_), send_r(n_), vals(n_), packs(n_), fields(n_, nullptr), cols(n_) {}
   int n;
   std::mutex mu;
   std::condition_variable cv;
@@ -29,6 +30,8 @@ struct LocalGroup {
   std::vector<real*> send_l, send_r;
   std::vector<double> vals;
   std::vector<ResidualPack> packs;
+  std::vector<Field*> fields;
+  std::vector<std::pair<int, int>> cols;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     const long g = gen;
@@ -57,6 +60,7 @@ class DeviceSolver : public SolverBase {
   DeviceSolver(Case& cs, int device = 0, int gi0 = 0, int gi1 = -1);
   ~DeviceSolver() override;
   StepResult do_step(const StepParams& P, bool want_res) override;
+  std::pair<int, int> owned_columns() const override { return {gi0, gi1}; }
   void download(Field& J) override;
   void upload() override;
   void cycle_update() override;

@@ -50,8 +50,9 @@ class Simulation:
         self.solver.run_steps(int(n), bool(residual))
 
     def run(self, max_cycles: int = 1, outdir: str = ".", outputs: bool = True, checkpoint: bool = True,
-            verbose: bool = True):
-        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose)
+            verbose: bool = True, metrics: str = ""):
+        """Reference driver: outer cycles with outputs; returns (cycles, log text)."""
+        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics)
 
     def summary(self) -> dict:
         return dict(self.solver.summary())

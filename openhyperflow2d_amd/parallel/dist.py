@@ -36,13 +36,14 @@ class DistributedSimulation:
     """A strip of a deck run on this rank."""
 
     def __init__(self, deck_text: str, backend: str = "gpu", *, rank: int = 0, world: int = 1,
-                 device: int = 0, semantics: str = "mpi", fused: bool = True, lean: bool = True, parts=None):
+                 device: int = 0, semantics: str = "mpi", fused: bool = True, lean: bool = True, parts=None,
+                 workdir: str = ".", use_checkpoint: bool = False):
         from .. import native
 
         hf = native()
         self.hf = hf
         self.rank, self.world = rank, world
-        self.case = hf.Case.from_deck(deck_text, ".", False)
+        self.case = hf.Case.from_deck(deck_text, workdir, use_checkpoint)
         self.case.set_semantics(semantics)
         solid = np.asarray(self.case.field("solid"))
         self.parts = parts or balanced_columns(solid, world)
@@ -120,11 +121,21 @@ class DistributedSimulation:
             dist.all_gather(out, arr)
             return b"".join(bytes(o.numpy().tobytes()) for o in out)
 
+        def fgather(gi0, gi1, strip):
+            out = [None] * world if rank == 0 else None
+            dist.gather_object((gi0, gi1, bytes(strip)), out, dst=0)
+            return out
+
         s.set_exchange(exchange)
-        s.set_comm(rank, world, fmin, fsum, fmaxi, fres)
+        s.set_comm(rank, world, fmin, fsum, fmaxi, fres, fgather)
 
     def step(self, n: int, residual: bool = False):
         self.solver.run_steps(int(n), bool(residual))
+
+    def run(self, max_cycles: int = 1, outdir: str = ".", outputs: bool = True, checkpoint: bool = True,
+            verbose: bool = True, metrics: str = ""):
+        """Full DEEPS driver (outer cycles, outputs on rank 0 after a strip gather)."""
+        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics)
 
     def summary(self):
         return dict(self.solver.summary())
