@@ -53,6 +53,9 @@ void Config::load_globals(InputDeck& d) {
   species.gamma = d.get_float("gamma");
   species.Tf = d.get_float("Tf");
   isAdiabaticWall = d.get_int("isAdiabaticWall");
+  // new key (not in the reference, which always runs the Zeldovich model):
+  // 0 frozen mixture, 1 Zeldovich (default), 2 finite-rate H2/air
+  chem_model = d.get_int_or("ChemicalReactionsModel", CRM_ZELDOVICH);
   // combustion products, fuel, oxidizer, air
   species.R[H_CP] = d.get_float("R_cp");
   species.H[H_CP] = d.get_float("H_cp");

@@ -179,4 +179,230 @@ def write(text: str, path: str) -> str:
     return path
 
 
-GENERATORS = {"wedge15": wedge15, "step": step}
+# boundary conditions with the turbulence-equation conditions of Wedge.dat
+_AXIS = "NT_AX_2D, TCT_dkdy_NULL_2D, TCT_depsdy_NULL_2D"
+_OUTFLOW = "NT_D0X_2D, TCT_dkdx_NULL_2D, TCT_depsdx_NULL_2D, CT_NONREFLECTED_2D"
+_FARFIELD = "NT_FARFIELD_2D, TCT_k_CONST_2D, TCT_eps_CONST_2D"
+_WALL = "NT_WNS_2D, TCT_eps_Cmk2kXn_WALL_2D"
+_INFLOW = "NT_FC_2D, TCT_k_CONST_2D, TCT_eps_CONST_2D"
+
+
+def _defaults_from_wedge(t: str, keys: Iterable[str]) -> str:
+    """Add keys the stale reference decks lack (e.g. TriplePoint.dat, SURVEY
+    Q13) with the values of the maintained Wedge.dat deck."""
+    w = _keys(template_text("Wedge.dat"))
+    have = _keys(t)
+    for k in keys:
+        if k not in have:
+            t = set_key(t, k, w[k])
+    return t
+
+
+def _const_table(v: float) -> List[Tuple[float, float]]:
+    return [(0.0, v), (1.0e5, v)]
+
+
+def triple_point(nx: int = 4000, ny: int = 1000, *, nmax: int = 200, nout: int = 100,
+                 project: Optional[str] = None, exit_time: float = 1.0e-30,
+                 gammas: Sequence[float] = (1.5, 1.4, 1.5)) -> str:
+    """Three-state shock interaction (TestCases/TriplePoint.dat, axisymmetric
+    Euler) at a BASELINE grid, with the three states carried by three
+    different gases (fuel/oxidiser/product slots given non-dimensional
+    properties R = 1, Cp = gamma/(gamma-1), no reaction): a 3-component mix.
+
+    The shipped deck is stale (no isAlternateRMS / MonitorIndex / ... keys,
+    SURVEY Q13); the missing keys are filled from Wedge.dat.  Geometry stays in
+    metres (0.07 x 0.03); the grid spacing follows nx, ny."""
+    t = remove_commented_directives(template_text("TriplePoint.dat"))
+    t = _defaults_from_wedge(t, ["isIgnoreUnsetNodes", "ThreadBlockSize", "isAlternateRMS", "MonitorIndex",
+                                 "beta_NonReflectedBC"])
+    project = project or "TriplePoint_%dx%d" % (nx, ny)
+    t = _rename(t, project)
+    ref = _keys(t)
+    ox, oy = int(ref["MaxX"]), int(ref["MaxY"])
+    Lx, Ly = ox * float(ref["dx"]), oy * float(ref["dy"])
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", Lx / nx)
+    t = set_key(t, "dy", Ly / ny)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", exit_time)
+    t = set_key(t, "isAlternateRMS", 1)
+    for name in _tables(t):
+        if re.fullmatch(r"Area\d+", name):
+            rows = _table_rows(t, name)
+            t = set_table(t, name, [(max(1, int(x * nx / ox)), max(1, int(y * ny / oy))) for x, y in rows])
+    # three gases, one per state; no reaction
+    for comp, (flow, sp, g) in enumerate(zip((1, 2, 3), ("Fuel", "OX", "cp"), gammas)):
+        t = set_key(t, "Flow2D-%d.CompIndex" % flow, comp)
+        t = set_key(t, "R_%s" % sp, 1.0)
+        t = set_key(t, "H_%s" % sp, 0.0)
+        t = set_table(t, "Cp_%s" % sp, _const_table(g / (g - 1.0)))
+    t = set_key(t, "Tf", 1.0e30)
+    return t
+
+
+def resonator(nx: int = 2000, ny: int = 200, *, nmax: int = 200, nout: int = 100, turbulence: int = 4,
+              project: Optional[str] = None, exit_time: float = 1.0e-30, jet_mach: float = 1.05,
+              jet_p: float = 2.6e5, jet_T: float = 250.0) -> str:
+    """Hartmann-Sprenger resonator: an under-expanded axisymmetric air jet
+    (nozzle radius 2 mm) impinging on a closed-end tube on the axis, k-eps
+    URANS, no-slip walls.  Domain 0.1 m x 0.01 m (dx = dy = 0.05 mm at
+    2000x200).  No reference deck exists (Makefile:50 names an absent
+    CIAM-Resonator.dat); the geometry is authored here from the Wedge.dat key
+    catalogue (contour + two solid rectangles)."""
+    t = remove_commented_directives(template_text("Wedge.dat"))
+    project = project or "Resonator_%dx%d" % (nx, ny)
+    t = _rename(t, project)
+    L, H = 0.1, 0.01
+    dx, dy = L / nx, H / ny
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", dx)
+    t = set_key(t, "dy", dy)
+    t = set_key(t, "FlowType", 1)
+    t = set_key(t, "ProblemType", 1)
+    t = set_key(t, "TurbulenceModel", turbulence)
+    t = set_key(t, "isTurbulenceReset", 1)
+    t = set_key(t, "isAdiabaticWall", 1)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", exit_time)
+    # flows: 1 jet (Mach/angle/static p,T), 2 ambient, 3 ambient for the rects
+    # (SolidBoundRect2D zeroes the velocity of the flow it references)
+    t = set_key(t, "NumFlow2D", 3)
+    t = set_key(t, "Flow2D-1.Mode", 2)
+    t = set_key(t, "Flow2D-1.Mach", jet_mach)
+    t = set_key(t, "Flow2D-1.Angle", 0.0)
+    t = set_key(t, "Flow2D-1.p", jet_p)
+    t = set_key(t, "Flow2D-1.T", jet_T)
+    t = set_key(t, "Flow2D-1.U", 0.0)
+    t = set_key(t, "Flow2D-1.V", 0.0)
+    for f in (2, 3):
+        t = set_key(t, "Flow2D-%d.CompIndex" % f, 3)
+        t = set_key(t, "Flow2D-%d.Mode" % f, 0)
+        t = set_key(t, "Flow2D-%d.p" % f, 1.0e5)
+        t = set_key(t, "Flow2D-%d.T" % f, 288.0)
+        t = set_key(t, "Flow2D-%d.U" % f, 0.0)
+        t = set_key(t, "Flow2D-%d.V" % f, 0.0)
+    r_n = 0.002
+    # contour on the outermost grid nodes: the reference maps contour points to
+    # nodes as (int)(x / dx), (int)(y / dy - 1)
+    xe, ye = (nx - 0.75) * dx, (ny + 0.25) * dy
+    rows = [(0.0, 0.0), (xe, 0.0), (xe, ye), (0.0, ye), (0.0, r_n)]
+    t = set_table(t, "Contour1", rows)
+    conds = [_AXIS, _OUTFLOW, _FARFIELD, _WALL, _INFLOW]
+    flows = [2, 2, 2, 2, 1]
+    for b in range(1, 6):
+        t = set_key(t, "Contour1.Bound%d.Cond" % b, conds[b - 1])
+        t = set_key(t, "Contour1.Bound%d.Flow2D" % b, flows[b - 1])
+        t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, turbulence)
+        t = set_key(t, "Contour1.Bound%d.isReset" % b, 0)
+    # drop bounds beyond 5 left over from the template
+    for b in range(6, 10):
+        t = re.sub(r"<data/Contour1\.Bound%d\.[^>]*>\n?" % b, "", t)
+    # resonator tube: annular wall + closed end, opening facing the nozzle
+    x_t, l_t, r_t, w = 0.012, 0.012, 0.0022, 0.001
+    t = set_key(t, "NumRects", 2)
+    rects = [(x_t, r_t, l_t, w), (x_t + l_t, 0.0, w, r_t + w)]
+    for k, (xs, ys, dxr, dyr) in enumerate(rects, 1):
+        t = set_key(t, "Rect%d.Xstart" % k, xs)
+        t = set_key(t, "Rect%d.Ystart" % k, ys)
+        t = set_key(t, "Rect%d.DX" % k, dxr)
+        t = set_key(t, "Rect%d.DY" % k, dyr)
+        t = set_key(t, "Rect%d.Flow2D" % k, 3)
+        t = set_key(t, "Rect%d.TurbulenceModel" % k, turbulence)
+    t = set_key(t, "NumArea", 1)
+    t = set_table(t, "Area1", [(nx - 3, ny // 2)])
+    t = set_key(t, "Area1.Type", 1)
+    t = set_key(t, "Area1.Flow2D", 2)
+    t = set_key(t, "Area1.TurbulenceModel", turbulence)
+    t = set_key(t, "Area1.MaterialID", 0)
+    t = re.sub(r"<table=Area2/\d+>.*?<endtable>\n?", "", t, flags=re.S)
+    return t
+
+
+def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100, project: Optional[str] = None,
+             exit_time: float = 1.0e-30, chemistry: int = 2, turbulence: int = 6) -> str:
+    """Axisymmetric Mach-8 H2/air scramjet channel: converging inlet, constant
+    area combustor with a wall H2 injection slot, diverging nozzle.  k-omega
+    SST (TurbulenceModel=6) and finite-rate chemistry
+    (ChemicalReactionsModel=2) are new physics keys (not in the reference).
+    Domain 0.6 m x 0.04 m (dx = dy = 0.1 mm at 6000x400)."""
+    t = remove_commented_directives(template_text("Wedge.dat"))
+    project = project or "Scramjet_%dx%d" % (nx, ny)
+    t = _rename(t, project)
+    L, H = 0.6, 0.04
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", L / nx)
+    t = set_key(t, "dy", H / ny)
+    t = set_key(t, "FlowType", 1)
+    t = set_key(t, "ProblemType", 1)
+    t = set_key(t, "TurbulenceModel", turbulence)
+    t = set_key(t, "isTurbulenceReset", 1)
+    t = set_key(t, "isAdiabaticWall", 1)
+    t = set_key(t, "ChemicalReactionsModel", chemistry)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", exit_time)
+    # 1: Mach-8 air, 2: sonic H2 jet (fuel), 3: ambient at rest (initial fill)
+    t = set_key(t, "NumFlow2D", 3)
+    t = set_key(t, "Flow2D-1.CompIndex", 3)
+    t = set_key(t, "Flow2D-1.Mode", 2)
+    t = set_key(t, "Flow2D-1.Mach", 8.0)
+    t = set_key(t, "Flow2D-1.Angle", 0.0)
+    t = set_key(t, "Flow2D-1.p", 1.2e3)
+    t = set_key(t, "Flow2D-1.T", 226.5)
+    t = set_key(t, "Flow2D-2.CompIndex", 0)
+    t = set_key(t, "Flow2D-2.Mode", 2)
+    t = set_key(t, "Flow2D-2.Mach", 1.0)
+    t = set_key(t, "Flow2D-2.Angle", -90.0)
+    t = set_key(t, "Flow2D-2.p", 2.0e5)
+    t = set_key(t, "Flow2D-2.T", 250.0)
+    t = set_key(t, "Flow2D-3.CompIndex", 3)
+    t = set_key(t, "Flow2D-3.Mode", 2)
+    t = set_key(t, "Flow2D-3.Mach", 8.0)
+    t = set_key(t, "Flow2D-3.Angle", 0.0)
+    t = set_key(t, "Flow2D-3.p", 1.2e3)
+    t = set_key(t, "Flow2D-3.T", 226.5)
+    for f in (1, 2, 3):
+        t = set_key(t, "Flow2D-%d.U" % f, 0.0)
+        t = set_key(t, "Flow2D-%d.V" % f, 0.0)
+    eps = 1e-6
+    # outermost grid nodes: contour points map to (int)(x / dx), (int)(y / dy - 1)
+    L, H = (nx - 0.75) * (L / nx), (ny + 0.25) * (H / ny)
+    Hc = 0.6 * H             # combustor radius
+    x_r0, x_r1 = 0.05, 0.2   # inlet compression ramp
+    x_in, w_in = 0.22, 0.002  # injector slot on the outer wall
+    x_c1 = 0.42               # combustor end / nozzle start
+    rows = [(0.0, 0.0), (L, 0.0), (L, H), (x_c1, Hc), (x_in + w_in, Hc), (x_in, Hc),
+            (x_r1, Hc), (x_r0, H), (0.0, H)]
+    t = set_table(t, "Contour1", rows)
+    conds = [_AXIS, _OUTFLOW, _WALL, _WALL, _INFLOW, _WALL, _WALL, _WALL, _INFLOW]
+    flows = [3, 3, 3, 3, 2, 3, 3, 3, 1]
+    for b in range(1, 10):
+        t = set_key(t, "Contour1.Bound%d.Cond" % b, conds[b - 1])
+        t = set_key(t, "Contour1.Bound%d.Flow2D" % b, flows[b - 1])
+        t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, turbulence)
+        t = set_key(t, "Contour1.Bound%d.isReset" % b, 0)
+    t = set_key(t, "NumArea", 2)
+    t = set_table(t, "Area1", [(3, 3)])
+    t = set_key(t, "Area1.Type", 1)
+    t = set_key(t, "Area1.Flow2D", 3)
+    t = set_key(t, "Area1.TurbulenceModel", turbulence)
+    t = set_key(t, "Area1.MaterialID", 0)
+    t = set_table(t, "Area2", [(nx // 2, ny - 3)])
+    t = set_key(t, "Area2.Type", 0)
+    t = set_key(t, "Area2.Flow2D", 3)
+    t = set_key(t, "Area2.TurbulenceModel", 0)
+    t = set_key(t, "Area2.MaterialID", 0)
+    return t
+
+
+GENERATORS = {"wedge15": wedge15, "step": step, "triple_point": triple_point, "resonator": resonator,
+              "scramjet": scramjet}

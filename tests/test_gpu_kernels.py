@@ -179,3 +179,20 @@ def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
     assert summ["dt"] == ref.summary()["dt"]
     for f in FIELDS:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("name", ["triple_point", "resonator", "scramjet", "step"])
+def test_baseline_config_decks_gpu_match_cpu(gpu, name):
+    """Small versions of the BASELINE.json config decks (axisymmetric k-eps
+    with no-slip tube walls, SST + wall injection, 3-gas triple point,
+    laminar N-S step): GPU == CPU Jacobi stepper."""
+    size = {"triple_point": (210, 90), "resonator": (300, 40), "scramjet": (450, 40), "step": (240, 80)}[name]
+    text = decks.GENERATORS[name](*size, nmax=10 ** 6, nout=10 ** 5)
+    g = gpu.Simulation(text, "gpu")
+    c = gpu.Simulation(text, "cpu")
+    for n, res in [(7, True), (8, False), (5, True)]:
+        g.step(n, residual=res)
+        c.step(n, residual=res)
+    tol = 1e-9 if name != "triple_point" else 1e-12
+    for f in FIELDS:
+        assert _rel(g.field(f), c.field(f)) < tol, f
