@@ -147,7 +147,8 @@ def step(nx: int = 1200, ny: int = 400, *, navier_stokes: bool = True, nmax: int
     for name in _tables(t):
         if re.fullmatch(r"Area\d+", name):
             rows = _table_rows(t, name)
-            t = set_table(t, name, [(int(x / sx), int(y / sy)) for x, y in rows])
+            t = set_table(t, name, [(min(max(int(x / sx), 2), nx - 3), min(max(int(y / sy), 2), ny - 3))
+                                    for x, y in rows])
     return t
 
 
@@ -292,36 +293,43 @@ def resonator(nx: int = 2000, ny: int = 200, *, nmax: int = 200, nout: int = 100
     # contour on the outermost grid nodes: the reference maps contour points to
     # nodes as (int)(x / dx), (int)(y / dy - 1)
     xe, ye = (nx - 0.75) * dx, (ny + 0.25) * dy
-    rows = [(0.0, 0.0), (xe, 0.0), (xe, ye), (0.0, ye), (0.0, r_n)]
+    # resonator tube (inner radius r_t, wall w, open end at x_t facing the
+    # nozzle, closed at x_c) carried by a solid sting to the outlet: the
+    # closed end and the sting are part of the domain contour, the annular
+    # tube wall is a solid rectangle.
+    x_t, x_c, r_t, w = 0.012, 0.024, 0.0022, 0.001
+    r_s = r_t + w
+    rows = [(0.0, 0.0), (x_c, 0.0), (x_c, r_s + dy), (xe, r_s + dy), (xe, ye), (0.0, ye), (0.0, r_n + dy)]
     t = set_table(t, "Contour1", rows)
-    conds = [_AXIS, _OUTFLOW, _FARFIELD, _WALL, _INFLOW]
-    flows = [2, 2, 2, 2, 1]
-    for b in range(1, 6):
+    conds = [_AXIS, _WALL, _WALL, _OUTFLOW, _FARFIELD, _WALL, _INFLOW]
+    flows = [2, 2, 2, 2, 2, 2, 1]
+    for b in range(1, len(conds) + 1):
         t = set_key(t, "Contour1.Bound%d.Cond" % b, conds[b - 1])
         t = set_key(t, "Contour1.Bound%d.Flow2D" % b, flows[b - 1])
         t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, turbulence)
         t = set_key(t, "Contour1.Bound%d.isReset" % b, 0)
-    # drop bounds beyond 5 left over from the template
-    for b in range(6, 10):
+    for b in range(len(conds) + 1, 12):
         t = re.sub(r"<data/Contour1\.Bound%d\.[^>]*>\n?" % b, "", t)
-    # resonator tube: annular wall + closed end, opening facing the nozzle
-    x_t, l_t, r_t, w = 0.012, 0.012, 0.0022, 0.001
-    t = set_key(t, "NumRects", 2)
-    rects = [(x_t, r_t, l_t, w), (x_t + l_t, 0.0, w, r_t + w)]
-    for k, (xs, ys, dxr, dyr) in enumerate(rects, 1):
+    t = set_key(t, "NumRects", 1)
+    for k, (xs, ys, dxr, dyr) in enumerate([(x_t, r_t, x_c - x_t, w)], 1):
         t = set_key(t, "Rect%d.Xstart" % k, xs)
         t = set_key(t, "Rect%d.Ystart" % k, ys)
         t = set_key(t, "Rect%d.DX" % k, dxr)
         t = set_key(t, "Rect%d.DY" % k, dyr)
         t = set_key(t, "Rect%d.Flow2D" % k, 3)
         t = set_key(t, "Rect%d.TurbulenceModel" % k, turbulence)
-    t = set_key(t, "NumArea", 1)
-    t = set_table(t, "Area1", [(nx - 3, ny // 2)])
+    t = set_key(t, "NumArea", 2)
+    t = set_table(t, "Area1", [(3, ny // 2)])
     t = set_key(t, "Area1.Type", 1)
     t = set_key(t, "Area1.Flow2D", 2)
     t = set_key(t, "Area1.TurbulenceModel", turbulence)
     t = set_key(t, "Area1.MaterialID", 0)
-    t = re.sub(r"<table=Area2/\d+>.*?<endtable>\n?", "", t, flags=re.S)
+    # the sting (outside the contour) is solid
+    t = set_table(t, "Area2", [(nx - 3, 1)])
+    t = set_key(t, "Area2.Type", 0)
+    t = set_key(t, "Area2.Flow2D", 3)
+    t = set_key(t, "Area2.TurbulenceModel", 0)
+    t = set_key(t, "Area2.MaterialID", 0)
     return t
 
 
