@@ -71,7 +71,8 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
     const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
     const real kk = 1.5 * TmpI * TmpI;
     const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
-    const real om = std::sqrt(kk) / (std::pow(bstar, 0.25) * l);
+    const real om = hf_max(std::sqrt(kk) / (std::pow(bstar, 0.25) * l),
+                           hf_max(kk / (1.0e5 * n.mu / rho + 1e-300), 1e-6));
     n.S[I_K] = rho * kk;
     n.S[I_OMEGA] = rho * om;
     n.mu_t = (om > 0) ? rho * kk / om : 0.0;
@@ -88,12 +89,16 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
     n.S[I_K] = 1.5 * TmpI * TmpI * rho;
   }
   const real kk = hf_max(n.S[I_K] / rho, 0.0);
-  const real om = hf_max(n.S[I_OMEGA] / rho, 1e-20);
+  const real nu = n.mu / rho;
+  // omega floor: eddy-viscosity ratio nu_t / nu <= 1e5 (keeps the explicit
+  // cross-diffusion and production terms bounded where k ~ 0, e.g. fluid at
+  // rest next to an impulsively started free stream)
+  const real om_floor = hf_max(kk / (1.0e5 * nu + 1e-300), 1e-6);
+  const real om = hf_max(n.S[I_OMEGA] / rho, om_floor);
   if (has_all(n.TurbType, TCT_eps_CONST)) {
     const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
-    n.S[I_OMEGA] = rho * std::sqrt(kk) / (std::pow(bstar, 0.25) * l);
+    n.S[I_OMEGA] = rho * hf_max(std::sqrt(kk) / (std::pow(bstar, 0.25) * l), om_floor);
   }
-  const real nu = n.mu / rho;
   // dkdx.. hold d(k)/dx and d(omega)/dx (already divided by rho, like the k-eps path)
   const real cross = n.dkdx * n.depsdx + n.dkdy * n.depsdy;
   const real CDkw = hf_max(2.0 * rho * so2 / om * cross, 1e-10);
@@ -134,9 +139,15 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   n.B[I_OMEGA] -= n.RY[I_OMEGA];
   n.SrcAdd[I_K] = n.SrcAdd[I_OMEGA] = 0.0;
   if (!has_all(n.TurbType, TCT_k_CONST)) n.Src[I_K] = Pk - bstar * rho * om * kk;
-  if (!has_all(n.TurbType, TCT_eps_CONST))
-    n.Src[I_OMEGA] = gam * rho / hf_max(mut, 1e-30) * Pk - beta * rho * om * om +
-                     2.0 * (1.0 - F1) * rho * so2 / om * cross;
+  if (!has_all(n.TurbType, TCT_eps_CONST)) {
+    // production gamma * rho * S^2 (the Pk limiter applied through nu_t) and
+    // the cross-diffusion term, each bounded by the destruction scale
+    // beta* rho omega^2 * 10 for the explicit DEEPS update
+    const real cap = 10.0 * bstar * rho * om * om;
+    const real Pw = hf_min(gam * rho / hf_max(mut, 1e-30) * Pk, cap);
+    const real CD = hf_max(hf_min(2.0 * (1.0 - F1) * rho * so2 / om * cross, cap), -cap);
+    n.Src[I_OMEGA] = Pw - beta * rho * om * om + CD;
+  }
   const real FT = (real)P.FT;
   n.F[I_K] = FT * (n.mu + mut * sk) * n.dkdy;
   n.F[I_OMEGA] = FT * (n.mu + mut * so) * n.depsdy;
