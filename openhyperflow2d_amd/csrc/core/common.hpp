@@ -242,6 +242,10 @@ struct SpeciesProps {
   TableData Cp[NSPEC];
   TableData lam[NSPEC];
   TableData mu[NSPEC];
+  // finite-rate global reaction 2 fu + ox -> 2 cp (new, ChemicalReactionsModel=2):
+  // W = A exp(-Ta/T) [fu]^a [ox]^b  [mol/m^3/s], concentrations in mol/m^3
+  real arr_A = 1.8e10, arr_Ta = 17614.0, arr_a = 1.0, arr_b = 0.5;
+  real M[NSPEC] = {0, 0, 0, 0};   // molar masses from R_s (kg/mol)
 };
 
 }  // namespace hf2d

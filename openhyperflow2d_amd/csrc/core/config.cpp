@@ -56,6 +56,10 @@ void Config::load_globals(InputDeck& d) {
   // new key (not in the reference, which always runs the Zeldovich model):
   // 0 frozen mixture, 1 Zeldovich (default), 2 finite-rate H2/air
   chem_model = d.get_int_or("ChemicalReactionsModel", CRM_ZELDOVICH);
+  species.arr_A = d.get_float_or("Arrhenius.A", species.arr_A);
+  species.arr_Ta = d.get_float_or("Arrhenius.Ta", species.arr_Ta);
+  species.arr_a = d.get_float_or("Arrhenius.FuelOrder", species.arr_a);
+  species.arr_b = d.get_float_or("Arrhenius.OxOrder", species.arr_b);
   // combustion products, fuel, oxidizer, air
   species.R[H_CP] = d.get_float("R_cp");
   species.H[H_CP] = d.get_float("H_cp");
@@ -77,6 +81,7 @@ void Config::load_globals(InputDeck& d) {
   species.lam[H_AIR] = d.get_table("lam_air").pack();
   species.mu[H_AIR] = d.get_table("mu_air").pack();
   species.Cp[H_AIR] = d.get_table("Cp_air").pack();
+  for (int q = 0; q < NSPEC; q++) species.M[q] = species.R[q] > 0 ? 8.314462618 / species.R[q] : 0.0;
   Hu[H_FU] = species.H[H_FU];
   Hu[H_OX] = species.H[H_OX];
   Hu[H_CP] = species.H[H_CP];

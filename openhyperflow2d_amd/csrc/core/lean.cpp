@@ -18,6 +18,7 @@ bool lean_eligible(const Case& cs, std::string* why) {
   if (C.ProblemType == SM_NS) return no("viscous problem");
   if (!C.sources.empty()) return no("gas sources");
   if (!C.isAdiabaticWall) return no("wall heat transfer");
+  if (C.chem_model == CRM_ARRENIUS) return no("finite-rate chemistry sources");
   for (const CellRecord& c : cs.J.c) {
     if (c.is(CT_SOLID)) continue;
     if (!c.is(CT_NODE_IS_SET)) return no("unset non-solid node");

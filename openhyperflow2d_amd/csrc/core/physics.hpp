@@ -529,6 +529,29 @@ HF_HD inline void chemistry_zeldovich(N& n, const SpeciesProps& sp, int sm, int 
   }
 }
 
+// Finite-rate global H2/air reaction (new; the reference declares the
+// CRM_ARRENIUS slot without implementing it): 2 H2 + O2 -> 2 H2O with
+// W = A exp(-Ta/T) [H2]^a [O2]^b (default: the one-step global rate with
+// A = 1.8e13 (cm^3/mol)^0.5/s, E = 35 kcal/mol, a = 1, b = 0.5, in SI).
+// The chemical energy is part of rho*E through the formation enthalpies
+// (fill_node's Tmp3), so only species sources are needed; the product mass
+// coefficient is (2 M_fu + M_ox) / 2 so mass is conserved exactly by
+// construction.  One step may consume at most the available reactants.
+template <class N>
+HF_HD inline void chemistry_arrhenius_src(N& n, const SpeciesProps& sp, real dt) {
+  const real T = n.Tg;
+  const real Mfu = sp.M[H_FU], Mox = sp.M[H_OX];
+  n.Src[I_YFU] = n.Src[I_YOX] = n.Src[I_YCP] = 0.;
+  if (has_all(n.CT, CT_Y_CONST) || !(Mfu > 0) || !(Mox > 0) || !(T > 0)) return;
+  const real cfu = n.S[I_YFU] / Mfu, cox = n.S[I_YOX] / Mox;   // mol/m^3
+  if (!(cfu > 0) || !(cox > 0)) return;
+  real W = sp.arr_A * std::exp(-sp.arr_Ta / T) * std::pow(cfu, sp.arr_a) * std::pow(cox, sp.arr_b);
+  if (dt > 0) W = hf_min(W, hf_min(0.5 * cfu, cox) / dt);
+  n.Src[I_YFU] = -2.0 * Mfu * W;
+  n.Src[I_YOX] = -Mox * W;
+  n.Src[I_YCP] = (2.0 * Mfu + Mox) * W;
+}
+
 // Number of transported equations for a cell: 9 for k-eps / SST (2 extra),
 // 8 for Spalart-Allmaras, 7 otherwise (deeps2d_core.cpp:4683-4695).
 HF_HD inline int num_eq_for(u64 turb_type) {

@@ -474,8 +474,12 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
       px.Ymix[0] = d.get_float(prefix + ".Y_fuel");
       px.Ymix[1] = d.get_float(prefix + ".Y_ox");
       px.Ymix[2] = d.get_float(prefix + ".Y_cp");
-      // Reference sign error kept (Q10): Y_air = 1 - Yf + Yo + Yc
-      px.Ymix[3] = 1 - px.Ymix[0] + px.Ymix[1] + px.Ymix[2];
+      // Reference sign error kept (Q10): Y_air = 1 - Yf + Yo + Yc.  Decks
+      // using the new finite-rate chemistry get the corrected closure.
+      if (C.chem_model == CRM_ARRENIUS)
+        px.Ymix[3] = 1 - (px.Ymix[0] + px.Ymix[1] + px.Ymix[2]);
+      else
+        px.Ymix[3] = 1 - px.Ymix[0] + px.Ymix[1] + px.Ymix[2];
       Cp = px.Ymix[0] * table_eval(sp.Cp[H_FU], Tg) + px.Ymix[1] * table_eval(sp.Cp[H_OX], Tg) +
            px.Ymix[2] * table_eval(sp.Cp[H_CP], Tg) + px.Ymix[3] * table_eval(sp.Cp[H_AIR], Tg);
       lam = px.Ymix[0] * table_eval(sp.lam[H_FU], Tg) + px.Ymix[1] * table_eval(sp.lam[H_OX], Tg) +

@@ -881,6 +881,7 @@ StepResult RefSolver::do_step(const StepParams& P, bool /*want_res*/) {
           const real AAA = std::sqrt(c.k * c.R * c.Tg);
           dtmin = std::min(dtmin, P.CFL_min * std::min(C.dx / (AAA + std::fabs(c.U)), C.dy / (AAA + std::fabs(c.V))));
           if (C.chem_model != NO_REACTIONS) chemistry_zeldovich(c, C.species, C.ProblemType, C.chem_model);
+          if (C.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, C.species, P.dt);
         }
       } else if (c.is(NT_FC)) {
         fill_node(c, P.ffc);

@@ -508,6 +508,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
       const real AAA = std::sqrt(c.k * c.R * c.Tg);
       dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(c.U)), P.dy / (AAA + std::fabs(c.V)));
       if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
+      if (P.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, *P.species, P.dt);
     }
   }
   for (int k = 0; k < NEQ; k++) {

@@ -363,8 +363,12 @@ def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100,
     t = set_key(t, "ExitMonitorValue", exit_time)
     # 1: Mach-8 air (inflow and initial fill), 2: sonic H2 jet (fuel),
     # 3: wall state at rest (300 K) for the no-slip walls
+    t = _h2_air_species(t)
     t = set_key(t, "NumFlow2D", 3)
-    t = set_key(t, "Flow2D-1.CompIndex", 3)
+    t = set_key(t, "Flow2D-1.CompIndex", 4)      # air = O2 + N2 mixture
+    t = set_key(t, "Flow2D-1.Y_fuel", 0.0)
+    t = set_key(t, "Flow2D-1.Y_ox", AIR_Y_O2)
+    t = set_key(t, "Flow2D-1.Y_cp", 0.0)
     t = set_key(t, "Flow2D-1.Mode", 2)
     t = set_key(t, "Flow2D-1.Mach", 8.0)
     t = set_key(t, "Flow2D-1.Angle", 0.0)
@@ -376,7 +380,10 @@ def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100,
     t = set_key(t, "Flow2D-2.Angle", -90.0)
     t = set_key(t, "Flow2D-2.p", 2.0e4)
     t = set_key(t, "Flow2D-2.T", 250.0)
-    t = set_key(t, "Flow2D-3.CompIndex", 3)
+    t = set_key(t, "Flow2D-3.CompIndex", 4)
+    t = set_key(t, "Flow2D-3.Y_fuel", 0.0)
+    t = set_key(t, "Flow2D-3.Y_ox", AIR_Y_O2)
+    t = set_key(t, "Flow2D-3.Y_cp", 0.0)
     t = set_key(t, "Flow2D-3.Mode", 0)
     t = set_key(t, "Flow2D-3.p", 1.2e3)
     t = set_key(t, "Flow2D-3.T", 300.0)
@@ -420,5 +427,85 @@ def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100,
     return t
 
 
+# H2 / O2 / H2O / N2 in the fuel / oxidiser / product / inert slots, for the
+# finite-rate chemistry decks (Wedge.dat's species data describe an H2/air
+# Zeldovich model with air as the oxidiser and no usable heat of formation).
+# Cp(T) from JANAF-level tables (J/kg/K), formation enthalpies per unit mass.
+_H2_AIR = {
+    "Fuel": (4124.2, 0.0, [(200, 13300), (300, 14310), (600, 14550), (1000, 14990), (1500, 16000),
+                           (2000, 16980), (3000, 18080), (4000, 18800)]),
+    "OX": (259.8, 0.0, [(200, 914), (300, 918), (600, 1003), (1000, 1090), (1500, 1145), (2000, 1181),
+                        (3000, 1240), (4000, 1280)]),
+    "cp": (461.5, -1.3435e7, [(200, 1850), (300, 1864), (600, 2003), (1000, 2288), (1500, 2575),
+                              (2000, 2837), (3000, 3070), (4000, 3180)]),
+    "air": (296.8, 0.0, [(200, 1039), (300, 1040), (600, 1075), (1000, 1167), (1500, 1244), (2000, 1284),
+                         (3000, 1323), (4000, 1340)]),
+}
+AIR_Y_O2 = 0.2329   # air = O2 + N2 by mass
+
+
+def _h2_air_species(t: str) -> str:
+    for sp, (R, H, cp) in _H2_AIR.items():
+        t = set_key(t, "R_%s" % sp, R)
+        t = set_key(t, "H_%s" % sp, H)
+        t = set_table(t, "Cp_%s" % sp, [(float(a), float(b)) for a, b in cp])
+    return t
+
+
+def reactor0d(nx: int = 8, ny: int = 8, *, T: float = 1500.0, p: float = 1.0e5, phi: float = 1.0,
+              nmax: int = 200, nout: int = 100, project: Optional[str] = None) -> str:
+    """Closed slip-wall box at rest with a premixed H2/air charge: every cell is
+    a constant-volume reactor (finite-rate chemistry validation)."""
+    t = remove_commented_directives(template_text("Wedge.dat"))
+    project = project or "Reactor0D"
+    t = _rename(t, project)
+    t = _h2_air_species(t)
+    dx = dy = 1.0e-3
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", dx)
+    t = set_key(t, "dy", dy)
+    t = set_key(t, "ProblemType", 0)
+    t = set_key(t, "FlowType", 0)
+    t = set_key(t, "TurbulenceModel", 0)
+    t = set_key(t, "ChemicalReactionsModel", 2)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", 1.0e-30)
+    # stoichiometric H2/air: Y_H2 / Y_O2 = 2 M_H2 / M_O2
+    r = 2 * 2.016 / 31.999 * phi
+    y_ox = AIR_Y_O2 / (1.0 + r * AIR_Y_O2)
+    y_fu = r * y_ox
+    t = set_key(t, "NumFlow2D", 2)
+    for f in (1, 2):
+        t = set_key(t, "Flow2D-%d.CompIndex" % f, 4)
+        t = set_key(t, "Flow2D-%d.Mode" % f, 0)
+        t = set_key(t, "Flow2D-%d.p" % f, p)
+        t = set_key(t, "Flow2D-%d.T" % f, T)
+        t = set_key(t, "Flow2D-%d.U" % f, 0.0)
+        t = set_key(t, "Flow2D-%d.V" % f, 0.0)
+        t = set_key(t, "Flow2D-%d.Y_fuel" % f, y_fu)
+        t = set_key(t, "Flow2D-%d.Y_ox" % f, y_ox)
+        t = set_key(t, "Flow2D-%d.Y_cp" % f, 0.0)
+    xe, ye = (nx - 0.75) * dx, (ny + 0.25) * dy
+    t = set_table(t, "Contour1", [(0.0, 0.0), (xe, 0.0), (xe, ye), (0.0, ye)])
+    conds = ["NT_AX_2D", "NT_AY_2D", "NT_AX_2D", "NT_AY_2D"]
+    for b in range(1, 5):
+        t = set_key(t, "Contour1.Bound%d.Cond" % b, conds[b - 1])
+        t = set_key(t, "Contour1.Bound%d.Flow2D" % b, 1)
+        t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, 0)
+        t = set_key(t, "Contour1.Bound%d.isReset" % b, 0)
+    for b in range(5, 12):
+        t = re.sub(r"<data/Contour1\.Bound%d\.[^>]*>\n?" % b, "", t)
+    t = set_key(t, "NumArea", 1)
+    t = set_table(t, "Area1", [(nx // 2, ny // 2)])
+    t = set_key(t, "Area1.Type", 1)
+    t = set_key(t, "Area1.Flow2D", 1)
+    t = set_key(t, "Area1.TurbulenceModel", 0)
+    t = set_key(t, "Area1.MaterialID", 0)
+    return t
+
+
 GENERATORS = {"wedge15": wedge15, "step": step, "triple_point": triple_point, "resonator": resonator,
-              "scramjet": scramjet}
+              "scramjet": scramjet, "reactor0d": reactor0d}
