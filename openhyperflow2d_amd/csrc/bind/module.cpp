@@ -214,6 +214,53 @@ PYBIND11_MODULE(_hf2d, m) {
       })
       .def("mass_flow_x", [](const Case& c, double x0, double y0, double dy) {
         return mass_flow_rate_x(c, c.J, x0, y0, dy);
+      })
+      // libOutCFD integrals on the host records (out_cfd_param.cpp)
+      .def("flow2d_count", [](const Case& c) { return (int)c.flows2d.size(); })
+      .def("area_x", [](const Case& c, double x0, double y0, double dy) { return calc_area(c, c.J, x0, y0, dy); })
+      .def("x_force", [](const Case& c, double x0, double y0, double dx, double dy) {
+        return x_force(c, c.J, x0, y0, dx, dy);
+      })
+      .def("y_force", [](const Case& c, double x0, double y0, double dx, double dy) {
+        return y_force(c, c.J, x0, y0, dx, dy);
+      })
+      .def("cx", [](const Case& c, double x0, double y0, double dx, double dy, int flow) {
+        return calc_cx(c, c.J, x0, y0, dx, dy, c.flows2d.at(flow - 1));
+      })
+      .def("cy", [](const Case& c, double x0, double y0, double dx, double dy, int flow) {
+        return calc_cy(c, c.J, x0, y0, dx, dy, c.flows2d.at(flow - 1));
+      })
+      .def("cd", [](const Case& c, double x0, double y0, double dy, int flow) {
+        return calc_cd(c, c.J, x0, y0, dy, c.flows2d.at(flow - 1));
+      })
+      .def("cv", [](const Case& c, double x0, double y0, double dy, double p_amb, int flow) {
+        return calc_cv(c, c.J, x0, y0, dy, p_amb, c.flows2d.at(flow - 1));
+      })
+      .def("average_pressure", [](const Case& c, double x0, double l, double d) {
+        return average_pressure(c, c.J, x0, l, d);
+      })
+      .def("average_temperature", [](const Case& c, double x0, double l, double d, int mid_enthalpy) {
+        return average_temperature(c, c.J, x0, l, d, mid_enthalpy);
+      })
+      .def("derived_field", [](const Case& c, const std::string& name) {
+        // p* (total pressure), T* (total temperature), schlieren |grad rho| (libOutCFD)
+        py::array_t<double> a({c.J.nx, c.J.ny});
+        auto m = a.mutable_unchecked<2>();
+        for (int i = 0; i < c.J.nx; i++)
+          for (int j = 0; j < c.J.ny; j++) {
+            const CellRecord& n = c.J.at(i, j);
+            double v;
+            if (name == "p_total") v = p_asterisk(n);
+            else if (name == "T_total") v = T_asterisk(n);
+            else if (name == "schlieren") v = schlieren(n);
+            else throw std::runtime_error("unknown derived field " + name);
+            m(i, j) = v;
+          }
+        return a;
+      })
+      .def("save_heat_flux", [](const Case& c, const std::string& px, const std::string& py_) {
+        if (!px.empty()) save_x_heat_flux(px, c, c.J);
+        if (!py_.empty()) save_y_heat_flux(py_, c, c.J);
       });
 
   py::class_<SolverBase>(m, "SolverBase")
