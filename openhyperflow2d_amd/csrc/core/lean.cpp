@@ -42,6 +42,15 @@ bool lean_single_gas(const Case& cs) {
   return true;
 }
 
+bool lean_any_cauchy_x(const Case& cs) {
+  for (const CellRecord& c : cs.J.c) {
+    if (!is_active(c.CT)) continue;
+    for (int k = 0; k < NEQ; k++)
+      if (eq_flags(k, c.CT, c.TurbType, cs.cfg.ProblemType).dx2) return true;
+  }
+  return false;
+}
+
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {
   const long N = h.N;
   const int ny = h.ny;

@@ -131,6 +131,7 @@ void install_signal_handlers();
 // lean inviscid path (lean.cpp)
 bool lean_eligible(const Case& cs, std::string* why);
 bool lean_single_gas(const Case& cs);
+bool lean_any_cauchy_x(const Case& cs);
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);
 
 class CpuSolver : public SolverBase {

@@ -391,6 +391,26 @@ __global__ void hf2d_unpack(ColList L, int col, int ny, const real* buf) {
   const int f = t / ny, j = t - f * ny;
   L.f[f][(long)col * ny + j] = buf[t];
 }
+// Both sides in one launch (sides: bit 0 left, bit 1 right).
+__global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, real* bufR, int sides) {
+  const int cnt = L.nf * ny;
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool right = t >= cnt;
+  if (right) t -= cnt;
+  if (t >= cnt || !(sides & (right ? 2 : 1))) return;
+  const int f = t / ny, j = t - f * ny;
+  (right ? bufR : bufL)[t] = L.f[f][(long)(right ? colR : colL) * ny + j];
+}
+__global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* bufL, const real* bufR,
+                             int sides) {
+  const int cnt = L.nf * ny;
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool right = t >= cnt;
+  if (right) t -= cnt;
+  if (t >= cnt || !(sides & (right ? 2 : 1))) return;
+  const int f = t / ny, j = t - f * ny;
+  L.f[f][(long)(right ? colR : colL) * ny + j] = (right ? bufR : bufL)[t];
+}
 
 // ---------------------------------------------------------------------------
 // DeviceSolver
@@ -690,6 +710,7 @@ void DeviceSolver::upload() {
   cp(m.nb, h.nb.data(), N);
   lean_ok = lean_eligible(cs, &lean_why);
   lean_sg_ok = lean_ok && lean_single_gas(cs);
+  lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
   if (lean_ok) {
     lean_bytes = lean_flags(h, cs.cfg.ProblemType);
     if (!lean_plain)
@@ -923,12 +944,16 @@ void DeviceSolver::exchange(int group) {
     for (int k = 0; k < NEQ; k++) L.f[L.nf++] = base + (long)k * N;
   };
   if (group == CpuSolver::HALO_LEAN) {
-    for (int k = 0; k < 4 + NCOMP; k++) L.f[L.nf++] = m.S[sbuf] + (long)k * N;
-    for (int k = 0; k < NCOMP; k++) L.f[L.nf++] = m.Spre[pbuf] + (long)k * N;
+    // single gas: the species (and their pre-chemistry copies) are +0 on
+    // every rank; dS/dx only travels if some node applies d2/dx2 = 0
+    const bool sg = lean_sg && lean_sg_ok;
+    for (int k = 0; k < (sg ? 4 : 4 + NCOMP); k++) L.f[L.nf++] = m.S[sbuf] + (long)k * N;
+    if (!sg)
+      for (int k = 0; k < NCOMP; k++) L.f[L.nf++] = m.Spre[pbuf] + (long)k * N;
     L.f[L.nf++] = m.U[pbuf];
     L.f[L.nf++] = m.V[pbuf];
     L.f[L.nf++] = m.P2[pbuf];
-    add_eq(m.dSdx[dsbuf]);
+    if (lean_has_cauchy_x) add_eq(m.dSdx[dsbuf]);
   } else if (group == CpuSolver::HALO_MID) {
     add_eq(m.S[1 - sbuf]);
   } else if (group == CpuSolver::HALO_QDIR) {
@@ -945,11 +970,12 @@ void DeviceSolver::exchange(int group) {
     L.f[L.nf++] = m.lam_t;
   }
   const int cnt = L.nf * ny;
-  const unsigned nb = (unsigned)((cnt + BLOCK - 1) / BLOCK);
+  const unsigned nb2 = (unsigned)((2 * cnt + BLOCK - 1) / BLOCK);
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
-  if (has_left) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, first, ny, m.halo_send[0]);
-  if (has_right) hipLaunchKernelGGL(hf2d_pack, dim3(nb), dim3(BLOCK), 0, m.stream, L, last, ny, m.halo_send[1]);
+  const int sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
+  hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, first, last, ny, m.halo_send[0],
+                     m.halo_send[1], sides);
   if (m.local) {
     LocalGroup& g = *m.local;
     HIP_CHECK(hipStreamSynchronize(m.stream));
@@ -976,8 +1002,8 @@ void DeviceSolver::exchange(int group) {
   }
   NCCL_CHECK(ncclGroupEnd());
   }
-  if (has_left) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, 0, ny, m.halo_recv[0]);
-  if (has_right) hipLaunchKernelGGL(hf2d_unpack, dim3(nb), dim3(BLOCK), 0, m.stream, L, h.nx - 1, ny, m.halo_recv[1]);
+  hipLaunchKernelGGL(hf2d_unpack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, 0, h.nx - 1, ny, m.halo_recv[0],
+                     m.halo_recv[1], sides);
 }
 
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {

@@ -95,6 +95,7 @@ class DeviceSolver : public SolverBase {
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
   int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
   bool lean_sg_ok = false;
+  bool lean_has_cauchy_x = true;   // some node reads dS/dx of an x neighbour (halo must carry it)
   void set_lean_plain(bool on);
   bool lean_ok = false;
   std::string lean_why;
