@@ -96,3 +96,30 @@ std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {
 }
 
 }  // namespace hf2d
+
+namespace hf2d {
+
+void compute_generic_flags(const Case& cs, HostArrays& h) {
+  const long N = h.N;
+  const std::vector<uint8_t> lb = lean_flags(h, cs.cfg.ProblemType);
+  const bool src_all = cs.cfg.chem_model == CRM_ARRENIUS || !cs.cfg.sources.empty();
+  static const real zero = 0.0;
+  auto nonzero = [&](const std::vector<real>& a, long idx, int k0, int k1) {
+    for (int k = k0; k < k1; k++)
+      if (std::memcmp(&a[(size_t)k * N + idx], &zero, sizeof(real)) != 0) return true;   // +0 only
+    return false;
+  };
+  h.gf.assign(N, 0);
+  for (long idx = 0; idx < N; idx++) {
+    uint8_t g = 0;
+    if (lb[idx] & LB_DX_OUT) g |= GF_DX_OUT;
+    if (lb[idx] & LB_DY_OUT) g |= GF_DY_OUT;
+    if (src_all || nonzero(h.Src, idx, 0, 4 + NCOMP)) g |= GF_SRC;
+    const u64 CT = h.CT[idx];
+    const bool wall_gas = !has_all(CT, CT_SOLID) && (has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW));
+    if (wall_gas || nonzero(h.SrcAdd, idx, 0, NEQ)) g |= GF_SRCADD;
+    h.gf[idx] = g;
+  }
+}
+
+}  // namespace hf2d

@@ -186,6 +186,7 @@ SoA HostArrays::view(int sb, int db, int pb) {
   s.CT = CT.data();
   s.TT = TT.data();
   s.nb = nb.data();
+  s.gf = gf.empty() ? nullptr : gf.data();
   s.iw = iw.data();
   s.jw = jw.data();
   return s;
@@ -476,6 +477,7 @@ CpuSolver::CpuSolver(Case& c, int g0, int g1) : SolverBase(c), gi0(g0), gi1(g1 <
 
 void CpuSolver::upload() {
   h.from_field(cs.J, gi0 - l_off);
+  compute_generic_flags(cs, h);
   sbuf = 0;
   dsbuf = 0;
   pbuf = 0;

@@ -40,6 +40,7 @@ struct HostArrays {
   std::vector<real> l_min, y_plus, Re_local, BGX, BGY, Tf, Q_conv, grad, qdir;
   std::vector<u64> CT, TT;
   std::vector<uint8_t> nb;
+  std::vector<uint8_t> gf;  // GF_* traffic flags (compute_generic_flags)
   std::vector<int32_t> iw, jw;
   std::vector<real> time;   // per-cell record time (checkpoint only)
 
@@ -132,6 +133,8 @@ void install_signal_handlers();
 bool lean_eligible(const Case& cs, std::string* why);
 bool lean_single_gas(const Case& cs);
 bool lean_any_cauchy_x(const Case& cs);
+// per-cell GF_* flags of the generic stepper (from the uploaded host arrays)
+void compute_generic_flags(const Case& cs, HostArrays& h);
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);
 
 class CpuSolver : public SolverBase {

@@ -23,6 +23,16 @@ namespace hf2d {
 // Neighbour-present bits packed per cell.
 enum : uint8_t { NB_XL = 1, NB_XR = 2, NB_YU = 4, NB_YD = 8 };
 
+// Per-cell traffic flags of the generic stepper (compute_generic_flags):
+//   GF_DX_OUT / GF_DY_OUT  dS/dx, dS/dy of this node are read by a Cauchy
+//                          (d2/dx2 = 0) neighbour, so they must be published
+//   GF_SRC                 Src of the flow/species equations may be non-zero
+//                          (sources, finite-rate chemistry)
+//   GF_SRCADD              SrcAdd may be non-zero (wall nodes)
+// Skipped loads are replaced by the +0 the arrays provably hold, skipped
+// stores would rewrite unchanged values, so results are bit-identical.
+enum : uint8_t { GF_DX_OUT = 1, GF_DY_OUT = 2, GF_SRC = 4, GF_SRCADD = 8 };
+
 // Raw SoA view.  Equation arrays are [k * N + idx], idx = i * ny + j
 // (x-major, matching the .hf2d file; a column is contiguous).
 struct SoA {
@@ -64,6 +74,7 @@ struct SoA {
   u64* CT = nullptr;
   u64* TT = nullptr;
   uint8_t* nb = nullptr;
+  uint8_t* gf = nullptr;   // GF_* flags (nullptr: all set)
   int32_t* iw = nullptr;
   int32_t* jw = nullptr;
 };
@@ -317,18 +328,19 @@ struct SoAPredictIO {
   HF_HD real dyD(int k) const { return in.dSdy[k * N + iD]; }
   HF_HD real beta(int k) const { return in.beta[k * N + idx]; }
   HF_HD real F(int k) const { return in.F[k * N + idx]; }
-  HF_HD real Src(int k) const { return in.Src[k * N + idx]; }
-  HF_HD real SrcAdd(int k) const { return in.SrcAdd[k * N + idx]; }
+  HF_HD real Src(int k) const { return (k >= 4 + NCOMP || (gf & GF_SRC)) ? in.Src[k * N + idx] : 0.0; }
+  HF_HD real SrcAdd(int k) const { return (gf & GF_SRCADD) ? in.SrcAdd[k * N + idx] : 0.0; }
   HF_HD void put_S(int k, real v) const { out.S[k * N + idx] = v; }
   HF_HD void put_beta(int k, real v) const { out.beta[k * N + idx] = v; }
   HF_HD void put_dS(int k, real a, real b) const {
-    out.dSdx[k * N + idx] = a;
-    out.dSdy[k * N + idx] = b;
+    if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = a;
+    if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = b;
   }
   HF_HD void keep_dS(int k) const {
-    out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
-    out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
+    if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
+    if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
   }
+  uint8_t gf = 0xff;
 };
 
 template <bool RES>
@@ -337,11 +349,12 @@ HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& 
   const long N = in.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = in.CT[idx];
+  const uint8_t gf = in.gf ? in.gf[idx] : (uint8_t)0xff;
   if (!is_active(CT)) {
     for (int k = 0; k < NEQ; k++) {
       out.S[k * N + idx] = in.S[k * N + idx];
-      out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
-      out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
+      if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
+      if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
     }
     return;
   }
@@ -349,7 +362,7 @@ HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& 
   const uint8_t nbm = in.nb[idx];
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-  SoAPredictIO io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4};
+  SoAPredictIO io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
   predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
 }
 
@@ -382,14 +395,17 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     return 1.0;
   }
   const bool active = !has_all(CT, NT_FC);
+  const uint8_t gf = sin.gf ? sin.gf[idx] : (uint8_t)0xff;
+  const bool axi = P.fpa.FT != 0;   // F is only read by the axisymmetric predictor
+  const bool ns = P.sm == SM_NS;    // turbulence sources live in Src[I_K], Src[I_EPS]
   c.CT = CT;
   c.TurbType = sin.TT[idx];
   for (int k = 0; k < NEQ; k++) {
     c.A[k] = sin.A[k * N + idx];
     c.B[k] = sin.B[k * N + idx];
-    c.F[k] = sin.F[k * N + idx];
-    c.Src[k] = sin.Src[k * N + idx];
-    c.SrcAdd[k] = sin.SrcAdd[k * N + idx];
+    c.F[k] = axi ? sin.F[k * N + idx] : 0.0;
+    c.Src[k] = ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) ? sin.Src[k * N + idx] : 0.0;
+    c.SrcAdd[k] = (gf & GF_SRCADD) ? sin.SrcAdd[k * N + idx] : 0.0;
     c.RX[k] = c.RY[k] = 0;
   }
   c.U = prim_old.U[idx];
@@ -416,12 +432,14 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     c.Y[s] = sin.Y[s * N + idx];
     c.droYdx[s] = c.droYdy[s] = 0;
   }
-  c.dUdx = sin.grad[G_DUDX * N + idx];
-  c.dUdy = sin.grad[G_DUDY * N + idx];
-  c.dVdx = sin.grad[G_DVDX * N + idx];
-  c.dVdy = sin.grad[G_DVDY * N + idx];
-  c.dTdx = sin.grad[G_DTDX * N + idx];
-  c.dTdy = sin.grad[G_DTDY * N + idx];
+  if (!(active && ns)) {   // velocity/temperature gradients are recomputed below for active viscous nodes
+    c.dUdx = sin.grad[G_DUDX * N + idx];
+    c.dUdy = sin.grad[G_DUDY * N + idx];
+    c.dVdx = sin.grad[G_DVDX * N + idx];
+    c.dVdy = sin.grad[G_DVDY * N + idx];
+    c.dTdx = sin.grad[G_DTDX * N + idx];
+    c.dTdy = sin.grad[G_DTDY * N + idx];
+  }
   c.dkdx = sin.grad[G_DKDX * N + idx];
   c.dkdy = sin.grad[G_DKDY * N + idx];
   c.depsdx = sin.grad[G_DEDX * N + idx];
@@ -515,9 +533,9 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     out.S[k * N + idx] = c.S[k];
     out.A[k * N + idx] = c.A[k];
     out.B[k * N + idx] = c.B[k];
-    out.F[k * N + idx] = c.F[k];
-    out.Src[k * N + idx] = c.Src[k];
-    out.SrcAdd[k * N + idx] = c.SrcAdd[k];
+    if (axi) out.F[k * N + idx] = c.F[k];
+    if ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) out.Src[k * N + idx] = c.Src[k];
+    if (gf & GF_SRCADD) out.SrcAdd[k * N + idx] = c.SrcAdd[k];
   }
   out.U[idx] = c.U;
   out.V[idx] = c.V;

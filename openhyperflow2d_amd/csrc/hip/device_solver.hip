@@ -476,6 +476,7 @@ struct DeviceSolver::Impl {
   // U/V on pbuf), per-cell neighbour/publish byte
   real *Spre[2], *P2[2];
   uint8_t* lb;
+  uint8_t* gf;   // generic-stepper GF_* traffic flags
   int32_t *iw, *jw;
   SpeciesProps* species = nullptr;
   DevScalars* sc = nullptr;
@@ -564,6 +565,7 @@ struct DeviceSolver::Impl {
     s.CT = CT;
     s.TT = TT;
     s.nb = nb;
+    s.gf = gf;
     s.iw = iw;
     s.jw = jw;
     return s;
@@ -606,6 +608,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     m.P2[b] = m.mem.alloc<real>(N);
   }
   m.lb = m.mem.alloc<uint8_t>(N);
+  m.gf = m.mem.alloc<uint8_t>(N);
   m.F = m.mem.alloc<real>(NEQ * N);
   m.Src = m.mem.alloc<real>(NEQ * N);
   m.SrcAdd = m.mem.alloc<real>(NEQ * N);
@@ -708,6 +711,8 @@ void DeviceSolver::upload() {
   cp(m.CT, h.CT.data(), N * sizeof(u64));
   cp(m.TT, h.TT.data(), N * sizeof(u64));
   cp(m.nb, h.nb.data(), N);
+  compute_generic_flags(cs, h);
+  cp(m.gf, h.gf.data(), N);
   lean_ok = lean_eligible(cs, &lean_why);
   lean_sg_ok = lean_ok && lean_single_gas(cs);
   lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
