@@ -357,6 +357,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_sg", &DeviceSolver::lean_sg)
       .def_readwrite("lean_tj", &DeviceSolver::lean_tj)
       .def_readwrite("lean_occ", &DeviceSolver::lean_occ)
+      .def_readwrite("use_graph", &DeviceSolver::use_graph)
+      .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },

@@ -81,6 +81,15 @@ struct SoA {
 
 enum { G_DUDX = 0, G_DUDY, G_DVDX, G_DVDY, G_DTDX, G_DTDY, G_DKDX, G_DKDY, G_DEDX, G_DEDY, NGRAD };
 
+// CFL / blending-factor scenario tables (deck CFL_Scenario, beta_Scenario)
+// for device-side evaluation: the device kernels read the iteration number
+// from device memory, so a captured step graph stays valid while the
+// scenario ramps.
+struct ScenarioTables {
+  TableData cfl, beta;
+  real CFL = 0, beta0 = 0;
+};
+
 struct StepParams {
   int nx, ny;        // local array extents (including halo columns)
   int i0, i1;        // owned/computed column range [i0, i1)
@@ -98,6 +107,7 @@ struct StepParams {
   FillParams fpa;    // for active cells (is_mu_t / is_init per TurbStartIter)
   FillParams ffc;    // for NT_FC cells: FillNode2D(1, 0, ...)
   const SpeciesProps* species;  // host or device pointer
+  const ScenarioTables* scen = nullptr;   // device: evaluate beta_min / CFL_min per step
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

@@ -57,6 +57,8 @@ constexpr int WAVE = 64;
 // Per-step scalars living on the device.
 struct DevScalars {
   unsigned long long dt_bits[3];   // rotating dt slots (IEEE bits of positive doubles)
+  double iter[3];                  // iteration number of the step using the slot
+  double beta_min[3], cfl_min[3];  // scenario values of that iteration
   double time_part;                // accumulated dt since the cycle start
   int neg_T;
   int pad;
@@ -73,6 +75,23 @@ __device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
   P.dt = dt;
   P.dtdx = dt / P.dx;
   P.dtdy = dt / P.dy;
+  if (P.scen) {   // scenario values of this step's iteration (scenario_next)
+    P.beta_min = sc->beta_min[slot];
+    P.CFL_min = sc->cfl_min[slot];
+  }
+}
+
+// Run once per step by one thread of the step's first kernel: iteration
+// number and CFL / beta scenario values (SolverBase::make_params arithmetic)
+// of the next step.
+__device__ inline void scenario_next(const StepParams& P, DevScalars* sc, int slot, int slot_next) {
+  const double it = sc->iter[slot] + 1.0;
+  sc->iter[slot_next] = it;
+  if (P.scen) {
+    const real bs = table_eval(P.scen->beta, it), cs = table_eval(P.scen->cfl, it);
+    sc->beta_min[slot_next] = (bs < P.scen->beta0) ? bs : P.scen->beta0;   // std::min(beta0, bs)
+    sc->cfl_min[slot_next] = (cs < P.scen->CFL) ? cs : P.scen->CFL;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -116,6 +135,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
     // writing) and accumulate physical time.
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
   }
   const long c = c0 + g;
   ResidualPack r;
@@ -188,6 +208,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   if (g == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
   }
   const long c = c0 + g;
   ResidualPack r;
@@ -241,6 +262,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
   if (g == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
   }
   const long c = c0 + g;
   ResidualPack r;
@@ -283,6 +305,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   if (b == 0 && threadIdx.x == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
   }
   int i[CPT], j[CPT], c[CPT], i0, j0;
   bool mine[CPT];
@@ -479,6 +502,7 @@ struct DeviceSolver::Impl {
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   int32_t *iw, *jw;
   SpeciesProps* species = nullptr;
+  ScenarioTables* scen = nullptr;
   DevScalars* sc = nullptr;
   DevScalars* sc_host = nullptr;   // pinned
   ResidualPack* partials = nullptr;
@@ -588,6 +612,11 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   dev = device;
   HIP_CHECK(hipSetDevice(dev));
   HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
+  {
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+    cu_count = prop.multiProcessorCount;
+  }
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
@@ -638,6 +667,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.iw = m.mem.alloc<int32_t>(N);
   m.jw = m.mem.alloc<int32_t>(N);
   m.species = m.mem.alloc<SpeciesProps>(1);
+  m.scen = m.mem.alloc<ScenarioTables>(1);
   m.sc = m.mem.alloc<DevScalars>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.sc_host, sizeof(DevScalars), hipHostMallocDefault));
   {
@@ -653,10 +683,19 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     m.halo_send[d] = m.mem.alloc<real>(m.halo_cap);
     m.halo_recv[d] = m.mem.alloc<real>(m.halo_cap);
   }
+  // hipMemset on device memory is asynchronous and runs on the null stream,
+  // which does not order against the non-blocking solver stream: drain the
+  // zero-fills before upload() copies the state in.
+  HIP_CHECK(hipDeviceSynchronize());
   upload();
 }
 
 DeviceSolver::~DeviceSolver() {
+  try {
+    flush_pending();
+  } catch (...) {
+  }
+  graph.reset();
   host_comm.reset();
   if (impl) {
     if (impl->comm) ncclCommDestroy(impl->comm);
@@ -669,6 +708,7 @@ DeviceSolver::~DeviceSolver() {
 void* DeviceSolver::stream() const { return (void*)impl->stream; }
 
 void DeviceSolver::upload() {
+  flush_pending();
   HIP_CHECK(hipSetDevice(dev));
   h.from_field(cs.J, gi0 - l_off);
   Impl& m = *impl;
@@ -726,6 +766,11 @@ void DeviceSolver::upload() {
   cp(m.iw, h.iw.data(), N * sizeof(int32_t));
   cp(m.jw, h.jw.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
+  scen_host.cfl = cs.cfg.CFL_Scenario.pack();
+  scen_host.beta = cs.cfg.beta_Scenario.pack();
+  scen_host.CFL = cs.cfg.CFL;
+  scen_host.beta0 = cs.cfg.beta0;
+  cp(m.scen, &scen_host, sizeof(ScenarioTables));
   DevScalars s0{};
   const double d0 = dt;
   std::memcpy(&s0.dt_bits[0], &d0, 8);
@@ -733,6 +778,14 @@ void DeviceSolver::upload() {
   std::memcpy(&s0.dt_bits[1], &one, 8);
   s0.dt_bits[2] = s0.dt_bits[1];
   s0.time_part = 0.0;
+  s0.iter[0] = s0.iter[1] = s0.iter[2] = (double)(last_iter + iter);
+  {
+    const StepParams Pi = make_params(last_iter + iter);
+    for (int q = 0; q < 3; q++) {
+      s0.beta_min[q] = Pi.beta_min;
+      s0.cfl_min[q] = Pi.CFL_min;
+    }
+  }
   time_offset = -cur_time_part;
   last_dev_time = 0.0;
   *m.sc_host = s0;
@@ -770,6 +823,7 @@ void DeviceSolver::lean_materialize() {
 }
 
 void DeviceSolver::download(Field& J) {
+  flush_pending();
   HIP_CHECK(hipSetDevice(dev));
   Impl& m = *impl;
   if (lean_state) lean_materialize();
@@ -811,6 +865,7 @@ void DeviceSolver::download(Field& J) {
 void DeviceSolver::on_cycle_roll() { time_offset = last_dev_time; }
 
 void DeviceSolver::sync_scalars() {
+  flush_pending();
   Impl& m = *impl;
   HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
   HIP_CHECK(hipStreamSynchronize(m.stream));
@@ -827,6 +882,7 @@ void DeviceSolver::sync_scalars() {
 
 // Called at each outer-cycle boundary by the driver (time_part restarts).
 void DeviceSolver::cycle_update() {
+  flush_pending();
   Impl& m = *impl;
   if (cs.cfg.ProblemType == SM_NS && cs.cfg.semantics != Semantics::SERIAL) {
     StepParams P = make_params(last_iter);
@@ -1011,7 +1067,128 @@ void DeviceSolver::exchange(int group) {
                      m.halo_recv[1], sides);
 }
 
+// ---------------------------------------------------------------------------
+// Step graphs.  Plain steps (no residual pass, no host read-back) are queued
+// and executed GRAPH_STEPS at a time as one captured hipGraph: every kernel
+// argument is step-invariant over that window (dt, time and the scenario
+// CFL/beta come from device memory; ping-pong parities repeat every 2 steps
+// and dt slots every 3, so 6 steps bring both back), which removes the
+// per-launch host cost that dominates small multi-GPU strips.  Any capture
+// error disables graphs for the solver and the queue runs eagerly.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int GRAPH_STEPS = 6;
+uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fused, bool tile, bool sg, int cpt,
+                         int tj) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+  mix((uint64_t)P.fpa.is_mu_t);
+  mix((uint64_t)P.fpa.is_init);
+  mix((uint64_t)P.fpa.isSrcAdd);
+  mix((uint64_t)lean_state);
+  mix((uint64_t)lean);
+  mix((uint64_t)fused);
+  mix((uint64_t)tile);
+  mix((uint64_t)sg);
+  mix((uint64_t)cpt);
+  mix((uint64_t)tj);
+  return h;
+}
+}  // namespace
+
+struct DeviceSolver::GraphCache {
+  hipGraphExec_t exec = nullptr;
+  uint64_t sig = 0;
+  ~GraphCache() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+  }
+};
+
+void DeviceSolver::flush_pending() {
+  if (pending.empty()) return;
+  std::vector<StepParams> q;
+  q.swap(pending);
+  for (const StepParams& p : q) do_step_eager(p, false);
+}
+
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
+  Impl& m = *impl;
+  const bool plain = use_graph && !want_res && !step_outputs && !m.local && !(lean && lean_ok && lean_state == 0);
+  if (!plain || (pending.empty() && nstep % GRAPH_STEPS != 0)) {
+    flush_pending();
+    return do_step_eager(P0, want_res);
+  }
+  pending.push_back(P0);
+  if ((int)pending.size() == GRAPH_STEPS) run_graph();
+  StepResult r;
+  r.async = true;
+  return r;
+}
+
+void DeviceSolver::run_graph() {
+  Impl& m = *impl;
+  const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
+                                       lean_cpt, lean_tj);
+  bool same = true;
+  for (const StepParams& p : pending)
+    same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
+                                   lean_tj) == sig;
+  if (!same) {
+    flush_pending();
+    return;
+  }
+  if (!graph) graph.reset(new GraphCache);
+  if (graph->exec && graph->sig == sig) {
+    HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
+    nstep += GRAPH_STEPS;   // ping-pong parities are unchanged after an even number of steps
+    pending.clear();
+    graph_launches++;
+    return;
+  }
+  // capture the window (host bookkeeping advances as in eager mode)
+  const long nstep0 = nstep;
+  const int ab = abuf, ds = dsbuf, pb = pbuf, sb = sbuf, ls = lean_state;
+  std::vector<StepParams> q;
+  q.swap(pending);
+  hipGraph_t g = nullptr;
+  bool ok = hipStreamBeginCapture(m.stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  if (ok) {
+    try {
+      for (const StepParams& p : q) do_step_eager(p, false);
+    } catch (const std::exception&) {
+      ok = false;
+    }
+    hipGraph_t gg = nullptr;
+    const bool ended = hipStreamEndCapture(m.stream, &gg) == hipSuccess;
+    ok = ok && ended && gg != nullptr;
+    if (gg && !ok) (void)hipGraphDestroy(gg);
+    g = ok ? gg : nullptr;
+  }
+  hipGraphExec_t exec = nullptr;
+  if (ok) ok = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) == hipSuccess;
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
+  // restore the bookkeeping and execute
+  nstep = nstep0;
+  abuf = ab;
+  dsbuf = ds;
+  pbuf = pb;
+  sbuf = sb;
+  lean_state = ls;
+  if (!ok) {
+    use_graph = false;   // eager from now on
+    for (const StepParams& p : q) do_step_eager(p, false);
+    return;
+  }
+  if (graph->exec) (void)hipGraphExecDestroy(graph->exec);
+  graph->exec = exec;
+  graph->sig = sig;
+  HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
+  nstep += GRAPH_STEPS;
+  graph_launches++;
+}
+
+StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   Impl& m = *impl;
   StepParams P = P0;
   P.nx = h.nx;
@@ -1021,6 +1198,7 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   P.gx0 = gi0 - l_off;
   P.do_residual = want_res ? 1 : 0;
   P.species = m.species;
+  P.scen = m.scen;
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
   const unsigned nblk = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
   const int slot = nstep % 3, slot_next = (nstep + 1) % 3;
@@ -1030,7 +1208,13 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   unsigned nres = nblk;   // workgroups that wrote residual partials
   if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
-    const int cpt = lean_cpt == 2 ? 2 : 1;
+    // two cells per thread unless that leaves fewer than ~2 workgroups per CU
+    // (small strips of a multi-GPU run)
+    int cpt = lean_cpt == 2 ? 2 : 1;
+    if (cpt == 2) {
+      const LeanTile T2 = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 2);
+      if ((long)T2.nbi * T2.nbj < 2L * cu_count) cpt = 1;
+    }
     const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, cpt);
     const unsigned ntile = (unsigned)(T.nbi * T.nbj);
     const bool sg = lean_sg && lean_sg_ok;
@@ -1176,7 +1360,10 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   return r;
 }
 
-void DeviceSolver::synchronize() { HIP_CHECK(hipStreamSynchronize(impl->stream)); }
+void DeviceSolver::synchronize() {
+  flush_pending();
+  HIP_CHECK(hipStreamSynchronize(impl->stream));
+}
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device) {
   return std::unique_ptr<SolverBase>(new DeviceSolver(cs, device < 0 ? 0 : device));

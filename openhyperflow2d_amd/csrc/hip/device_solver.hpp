@@ -60,6 +60,7 @@ class DeviceSolver : public SolverBase {
   DeviceSolver(Case& cs, int device = 0, int gi0 = 0, int gi1 = -1);
   ~DeviceSolver() override;
   StepResult do_step(const StepParams& P, bool want_res) override;
+  StepResult do_step_eager(const StepParams& P, bool want_res);
   std::pair<int, int> owned_columns() const override { return {gi0, gi1}; }
   void download(Field& J) override;
   void upload() override;
@@ -93,7 +94,8 @@ class DeviceSolver : public SolverBase {
   bool lean_sg = true;     // single-gas specialisation (lean_euler.hpp) if eligible
   int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
-  int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
+  int lean_cpt = 2;
+  int cu_count = 256;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
   bool lean_sg_ok = false;
   bool lean_has_cauchy_x = true;   // some node reads dS/dx of an x neighbour (halo must carry it)
   void set_lean_plain(bool on);
@@ -101,12 +103,21 @@ class DeviceSolver : public SolverBase {
   std::string lean_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
   std::vector<uint8_t> lean_bytes;
+  ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
   void lean_materialize();
   std::unique_ptr<Comm> host_comm;
+  // step graphs (see device_solver.hip)
+  bool use_graph = true;
+  long graph_launches = 0;
+  void flush_pending();
 
  private:
   struct Impl;
   std::unique_ptr<Impl> impl;
+  struct GraphCache;
+  std::unique_ptr<GraphCache> graph;
+  std::vector<StepParams> pending;
+  void run_graph();
 };
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device);

@@ -196,3 +196,23 @@ def test_baseline_config_decks_gpu_match_cpu(gpu, name):
     tol = 1e-9 if name != "triple_point" else 1e-12
     for f in FIELDS:
         assert _rel(g.field(f), c.field(f)) < tol, f
+
+
+@pytest.mark.parametrize("physics", ["euler", "kes"])
+def test_step_graphs_bitwise(gpu, physics):
+    """Plain steps replayed as captured 6-step hipGraphs (device-side dt,
+    time and CFL/beta scenario) == eager launches, bit for bit."""
+    ns = physics != "euler"
+    text = decks.wedge15(300, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    b.solver.use_graph = False
+    for n, res in [(40, False), (13, True), (61, False)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+    assert a.solver.graph_launches > 0
+    assert b.solver.graph_launches == 0
+    assert a.summary()["dt"] == b.summary()["dt"]
+    assert a.summary()["time"] == b.summary()["time"]
+    for f in FIELDS + ["k", "R", "CP"]:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)

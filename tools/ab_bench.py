@@ -29,6 +29,8 @@ def main():
         v0 = v.split("+")[0]
         if v0 == "plain":
             s.solver.lean_plain = True
+        elif v0 == "nograph":
+            s.solver.use_graph = False
         elif v0 == "nosg":
             s.solver.lean_sg = False
         elif v0.startswith("cpt"):
