@@ -121,7 +121,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
 
 def is_built() -> bool:
-    return os.path.exists(ext_path())
+    bindir = os.path.join(os.path.dirname(ext_path()), "bin")
+    return all(os.path.exists(p) for p in (ext_path(), os.path.join(bindir, "hf2d"), os.path.join(bindir, "hf2d_cpu")))
 
 
 if __name__ == "__main__":
