@@ -424,10 +424,18 @@ __global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, re
   const int f = t / ny, j = t - f * ny;
   (right ? bufR : bufL)[t] = L.f[f][(long)(right ? colR : colL) * ny + j];
 }
+// Also folds the dt gathered from the other ranks (ndt > 0: dtr[q], q != self)
+// into the next dt slot: MIN of positive doubles, exact in any order.
 __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* bufL, const real* bufR,
-                             int sides) {
+                             int sides, DevScalars* sc, int dslot, const double* dtr, int ndt, int self) {
   const int cnt = L.nf * ny;
   int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0 && ndt > 0) {
+    double m = bits_to_d(sc->dt_bits[dslot]);
+    for (int q = 0; q < ndt; q++)
+      if (q != self) m = fmin(m, dtr[q]);
+    sc->dt_bits[dslot] = d_to_bits(m);
+  }
   const bool right = t >= cnt;
   if (right) t -= cnt;
   if (t >= cnt || !(sides & (right ? 2 : 1))) return;
@@ -512,6 +520,7 @@ struct DeviceSolver::Impl {
   real* halo_send[2] = {nullptr, nullptr};
   real* halo_recv[2] = {nullptr, nullptr};
   long halo_cap = 0;
+  double* dt_recv = nullptr;   // dt of every rank (gathered with the halo)
   ncclComm_t comm = nullptr;
   std::shared_ptr<LocalGroup> local;   // in-process virtual ranks (testing)
   int rank = 0, nranks = 1;
@@ -977,6 +986,8 @@ void DeviceSolver::init_comm(const std::string& uid, int rank, int nranks) {
   NCCL_CHECK(ncclCommInitRank(&impl->comm, nranks, id, rank));
   impl->rank = rank;
   impl->nranks = nranks;
+  impl->dt_recv = impl->mem.alloc<double>(nranks);
+  HIP_CHECK(hipDeviceSynchronize());
   host_comm.reset(new RcclHostComm(impl->comm, impl->stream, rank, nranks));
   comm = host_comm.get();
 }
@@ -985,6 +996,8 @@ void DeviceSolver::init_local(std::shared_ptr<LocalGroup> g, int rank) {
   impl->local = g;
   impl->rank = rank;
   impl->nranks = g->n;
+  impl->dt_recv = impl->mem.alloc<double>(g->n);
+  HIP_CHECK(hipDeviceSynchronize());
   host_comm.reset(new LocalHostComm(g, rank));
   comm = host_comm.get();
 }
@@ -993,8 +1006,11 @@ int DeviceSolver::comm_rank() const { return impl->rank; }
 int DeviceSolver::comm_size() const { return impl->nranks; }
 
 // Halo exchange of one field group with RCCL send/recv to the strip
-// neighbours (rank-1 owns the columns to the left).
-void DeviceSolver::exchange(int group) {
+// neighbours (rank-1 owns the columns to the left).  dt_slot >= 0: the
+// same RCCL group also sends this rank's dt of that slot to every other rank
+// and unpack folds the MIN in -- one grouped p2p launch per step instead of a
+// send/recv group plus an all-reduce.
+void DeviceSolver::exchange(int group, int dt_slot) {
   Impl& m = *impl;
   if ((!m.comm && !m.local) || m.nranks == 1) return;
   const int ny = h.ny;
@@ -1037,12 +1053,19 @@ void DeviceSolver::exchange(int group) {
   const int sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
   hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, first, last, ny, m.halo_send[0],
                      m.halo_send[1], sides);
+  const bool gather_dt = dt_slot >= 0;
+  unsigned long long* my_dt = gather_dt ? &m.sc->dt_bits[dt_slot] : nullptr;
   if (m.local) {
     LocalGroup& g = *m.local;
     HIP_CHECK(hipStreamSynchronize(m.stream));
     g.send_l[m.rank] = m.halo_send[0];
     g.send_r[m.rank] = m.halo_send[1];
+    g.dt_src[m.rank] = my_dt;
     g.barrier();
+    if (gather_dt)
+      for (int q = 0; q < m.nranks; q++)
+        if (q != m.rank)
+          HIP_CHECK(hipMemcpyAsync(m.dt_recv + q, g.dt_src[q], sizeof(double), hipMemcpyDeviceToDevice, m.stream));
     if (has_left)
       HIP_CHECK(hipMemcpyAsync(m.halo_recv[0], g.send_r[m.rank - 1], (size_t)cnt * sizeof(real),
                                hipMemcpyDeviceToDevice, m.stream));
@@ -1061,10 +1084,18 @@ void DeviceSolver::exchange(int group) {
     NCCL_CHECK(ncclSend(m.halo_send[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
     NCCL_CHECK(ncclRecv(m.halo_recv[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
   }
+  if (gather_dt)
+    for (int q = 0; q < m.nranks; q++)
+      if (q != m.rank) {
+        NCCL_CHECK(ncclSend(my_dt, 1, ncclDouble, q, m.comm, m.stream));
+        NCCL_CHECK(ncclRecv(m.dt_recv + q, 1, ncclDouble, q, m.comm, m.stream));
+      }
   NCCL_CHECK(ncclGroupEnd());
   }
-  hipLaunchKernelGGL(hf2d_unpack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, 0, h.nx - 1, ny, m.halo_recv[0],
-                     m.halo_recv[1], sides);
+  hipLaunchKernelGGL(hf2d_unpack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, m.stream, L, 0, h.nx - 1, ny,
+                     m.halo_recv[0], m.halo_recv[1], sides, m.sc, gather_dt ? dt_slot : 0, m.dt_recv,
+                     gather_dt ? m.nranks : 0, m.rank);
+  HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------------------
@@ -1323,21 +1354,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
   }
-  if ((m.comm || m.local) && m.nranks > 1) {
-    // global dt: MIN over ranks, in place on the next slot
-    real* dslot = (real*)&m.sc->dt_bits[slot_next];
-    if (m.comm) {
-      NCCL_CHECK(ncclAllReduce(dslot, dslot, 1, ncclDouble, ncclMin, m.comm, st));
-    } else {
-      double v;
-      HIP_CHECK(hipMemcpyAsync(&v, dslot, sizeof v, hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipStreamSynchronize(st));
-      v = m.local->reduce(m.rank, v, 0);
-      HIP_CHECK(hipMemcpyAsync(dslot, &v, sizeof v, hipMemcpyHostToDevice, st));
-      HIP_CHECK(hipStreamSynchronize(st));
-    }
-    exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE);
-  }
+  // new-state halo + global dt (MIN over ranks into the next slot)
+  if ((m.comm || m.local) && m.nranks > 1) exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
   if (!cs.cfg.isAdiabaticWall) {
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     hipLaunchKernelGGL(hf2d_wall_solid, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1);

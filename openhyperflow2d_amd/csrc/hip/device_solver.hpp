@@ -21,13 +21,14 @@ bool gpu_available();
 // (RCCL refuses two ranks on one device).
 struct LocalGroup {
   explicit LocalGroup(int n_)
-      : n(n_), send_l(n_), send_r(n_), vals(n_), packs(n_), fields(n_, nullptr), cols(n_) {}
+      : n(n_), send_l(n_), send_r(n_), dt_src(n_, nullptr), vals(n_), packs(n_), fields(n_, nullptr), cols(n_) {}
   int n;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   long gen = 0;
   std::vector<real*> send_l, send_r;
+  std::vector<const unsigned long long*> dt_src;   // device dt slot of each rank
   std::vector<double> vals;
   std::vector<ResidualPack> packs;
   std::vector<Field*> fields;
@@ -78,7 +79,7 @@ class DeviceSolver : public SolverBase {
   void init_local(std::shared_ptr<LocalGroup> g, int rank);
   int comm_rank() const;
   int comm_size() const;
-  void exchange(int group);
+  void exchange(int group, int dt_slot = -1);
 
   HostArrays h;           // host staging copy
   int dev = 0;
