@@ -350,6 +350,8 @@ PYBIND11_MODULE(_hf2d, m) {
            py::arg("gi1") = -1, py::keep_alive<1, 2>())
       .def_static("nccl_unique_id", []() { return py::bytes(DeviceSolver::nccl_unique_id()); })
       .def("init_comm", [](DeviceSolver& s, py::bytes uid, int r, int n) { s.init_comm(std::string(uid), r, n); })
+      .def("comm_rank", &DeviceSolver::comm_rank)
+      .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("fused", &DeviceSolver::fused)
       .def_readwrite("lean", &DeviceSolver::lean)

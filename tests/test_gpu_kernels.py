@@ -216,3 +216,20 @@ def test_step_graphs_bitwise(gpu, physics):
     assert a.summary()["time"] == b.summary()["time"]
     for f in FIELDS + ["k", "R", "CP"]:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
+def test_rccl_single_rank_comm(gpu, tmp_path):
+    """The RCCL communicator path (ncclCommInitRank, host reductions, strip
+    gather for outputs) on a one-rank communicator == no communicator."""
+    text = decks.wedge15(200, 40, nmax=30, nout=10)
+    a = gpu.Simulation(text, "gpu", workdir=str(tmp_path))
+    b = gpu.Simulation(text, "gpu")
+    a.solver.init_comm(gpu.native().DeviceSolver.nccl_unique_id(), 0, 1)
+    assert a.solver.comm_size() == 1
+    for n, res in [(13, False), (7, True), (12, False)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+    for f in FIELDS:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+    a.run(1, str(tmp_path), outputs=True, checkpoint=False, verbose=False)
+    assert any(p.suffix == ".plt" for p in tmp_path.iterdir())
