@@ -267,6 +267,22 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("run_steps", &SolverBase::run_steps, py::arg("n"), py::arg("want_residual_last") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("advance", [](SolverBase& s, bool want) { s.advance(want); }, py::arg("want_residual") = false)
+      .def("set_comm",
+           [](SolverBase& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
+              std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres,
+              std::function<py::object(int, int, py::bytes)> fgather) {
+             auto* c = new PyComm();
+             c->r = rank;
+             c->n = size;
+             c->f_min = fmin;
+             c->f_sum = fsum;
+             c->f_maxi = fmaxi;
+             c->f_res = fres;
+             c->f_gather = fgather;
+             s.comm = c;   // leaked intentionally: lives as long as the solver
+           },
+           py::arg("rank"), py::arg("size"), py::arg("fmin"), py::arg("fsum"), py::arg("fmaxi"), py::arg("fres"),
+           py::arg("fgather") = nullptr)
       .def("run",
            [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose,
               const std::string& metrics) {
@@ -321,23 +337,7 @@ PYBIND11_MODULE(_hf2d, m) {
              if (a.size() != s.halo_doubles(g) * s.h.ny) throw std::runtime_error("halo size mismatch");
              s.unpack_column(g, li, a.data());
            })
-      .def("set_exchange", [](CpuSolver& s, std::function<void(CpuSolver&, int)> f) { s.halo_exchange = f; })
-      .def("set_comm",
-           [](CpuSolver& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
-              std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres,
-              std::function<py::object(int, int, py::bytes)> fgather) {
-             auto* c = new PyComm();
-             c->r = rank;
-             c->n = size;
-             c->f_min = fmin;
-             c->f_sum = fsum;
-             c->f_maxi = fmaxi;
-             c->f_res = fres;
-             c->f_gather = fgather;
-             s.comm = c;   // leaked intentionally: lives as long as the solver
-           },
-           py::arg("rank"), py::arg("size"), py::arg("fmin"), py::arg("fsum"), py::arg("fmaxi"), py::arg("fres"),
-           py::arg("fgather") = nullptr);
+      .def("set_exchange", [](CpuSolver& s, std::function<void(CpuSolver&, int)> f) { s.halo_exchange = f; });
 
   py::class_<RefSolver, SolverBase>(m, "RefSolver").def(py::init<Case&>(), py::keep_alive<1, 2>());
 
@@ -350,6 +350,15 @@ PYBIND11_MODULE(_hf2d, m) {
            py::arg("gi1") = -1, py::keep_alive<1, 2>())
       .def_static("nccl_unique_id", []() { return py::bytes(DeviceSolver::nccl_unique_id()); })
       .def("init_comm", [](DeviceSolver& s, py::bytes uid, int r, int n) { s.init_comm(std::string(uid), r, n); })
+      .def("p2p_export", [](DeviceSolver& s, int r, int n) { return py::bytes(s.p2p_export(r, n)); },
+           py::arg("rank"), py::arg("nranks"))
+      .def("p2p_import",
+           [](DeviceSolver& s, const std::vector<py::bytes>& d) {
+             std::vector<std::string> v;
+             for (const auto& b : d) v.push_back(std::string(b));
+             s.p2p_import(v);
+           })
+      .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())

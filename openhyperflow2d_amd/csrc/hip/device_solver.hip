@@ -20,6 +20,7 @@
 // the next step's kernels read it from there.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <cstdio>
@@ -444,6 +445,116 @@ __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* 
 }
 
 // ---------------------------------------------------------------------------
+// xGMI peer-to-peer halo transport (default for multi-GPU strips).
+//
+// Every rank owns one fine-grained "mailbox" allocation, mapped into its
+// peers with IPC handles:
+//   flags[nranks]  u64   step sequence number last published by rank q
+//   dtr[2][nranks] f64   dt of rank q for sequence parity 0/1
+//   recv[2][2][cap] f64  halo columns for parity 0/1 from the left/right
+// One single-workgroup kernel per exchange replaces pack + RCCL group +
+// unpack: it stores this rank's boundary columns straight into the
+// neighbours' mailboxes and its dt into every peer's, releases its flag at
+// system scope, waits (bounded) for every peer's flag of the same sequence
+// number, then unpacks its own mailbox into the ghost columns and folds the
+// MIN of all dt into the next dt slot -- bitwise the RCCL path's result.
+// Parity double buffering is safe without a second handshake: a peer writes
+// parity p again only at sequence s+2, after it has seen this rank's flag
+// s+1, which is published after the unpack of s.  The sequence counter lives
+// in device memory, so the kernel replays unchanged inside step graphs.
+// ---------------------------------------------------------------------------
+constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
+constexpr int P2P_THREADS = 512;
+
+struct P2PArgs {
+  ColList L;
+  int first, last, ghostL, ghostR, ny, cnt, sides;
+  long cap;                              // doubles per (parity, side) mailbox slot
+  real* peer_recv_l;                     // left neighbour's recv base (this rank is its right side)
+  real* peer_recv_r;                     // right neighbour's recv base
+  real* my_recv;
+  unsigned long long* const* peer_flags; // [nranks] flag array of each rank (self: own)
+  double* const* peer_dtr;               // [nranks] dtr array of each rank
+  unsigned long long* my_flags;
+  double* my_dtr;
+  unsigned long long* seq;               // device-side sequence counter
+  DevScalars* sc;
+  int dslot, fold_dt, rank, nranks;
+};
+
+__device__ inline double p2p_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+__global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
+  const unsigned long long seq = *a.seq + 1;
+  const int par = (int)(seq & 1);
+  const int ny = a.ny;
+  // 1. push boundary columns and this rank's dt into the peers' mailboxes
+  if (a.sides & 1) {
+    real* dst = a.peer_recv_l + ((long)par * 2 + 1) * a.cap;   // left neighbour receives "from right"
+    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      dst[t] = a.L.f[f][(long)a.first * ny + j];
+    }
+  }
+  if (a.sides & 2) {
+    real* dst = a.peer_recv_r + ((long)par * 2) * a.cap;       // right neighbour receives "from left"
+    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      dst[t] = a.L.f[f][(long)a.last * ny + j];
+    }
+  }
+  const double mydt = bits_to_d(a.sc->dt_bits[a.dslot]);
+  for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
+    if (q != a.rank) a.peer_dtr[q][par * a.nranks + a.rank] = mydt;
+  __threadfence_system();
+  __syncthreads();
+  // 2. publish, 3. wait for every peer's publication of the same sequence
+  for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
+    if (q != a.rank) __hip_atomic_store(&a.peer_flags[q][a.rank], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const bool failed = __hip_atomic_load(&a.sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2;
+  for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS) {
+    if (q == a.rank || failed) continue;   // after one timeout, stop waiting (the host reports it)
+    long spins = 0;
+    while (__hip_atomic_load(&a.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > P2P_SPIN_LIMIT) {
+        atomicOr(&a.sc->neg_T, 2);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // 4. unpack this rank's mailbox into the ghost columns
+  if (a.sides & 1) {
+    const real* src = a.my_recv + ((long)par * 2) * a.cap;
+    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      a.L.f[f][(long)a.ghostL * ny + j] = p2p_load(src + t);
+    }
+  }
+  if (a.sides & 2) {
+    const real* src = a.my_recv + ((long)par * 2 + 1) * a.cap;
+    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      a.L.f[f][(long)a.ghostR * ny + j] = p2p_load(src + t);
+    }
+  }
+  // 5. global dt: MIN over ranks (exact in any order)
+  if (threadIdx.x == 0) {
+    if (a.fold_dt) {
+      double m = mydt;
+      for (int q = 0; q < a.nranks; q++)
+        if (q != a.rank) m = fmin(m, p2p_load(a.my_dtr + par * a.nranks + q));
+      a.sc->dt_bits[a.dslot] = d_to_bits(m);
+    }
+    *a.seq = seq;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // DeviceSolver
 // ---------------------------------------------------------------------------
 struct DevBuf {
@@ -524,6 +635,17 @@ struct DeviceSolver::Impl {
   ncclComm_t comm = nullptr;
   std::shared_ptr<LocalGroup> local;   // in-process virtual ranks (testing)
   int rank = 0, nranks = 1;
+  // xGMI peer-to-peer transport (hf2d_p2p_xchg)
+  struct P2P {
+    bool on = false;
+    char* base = nullptr;                 // fine-grained mailbox (p2p_layout)
+    size_t bytes = 0, off_dtr = 0, off_recv = 0;
+    unsigned long long* seq = nullptr;    // device-side exchange counter
+    std::vector<char*> peer_base;         // mailbox of every rank (self: base)
+    std::vector<void*> opened;            // IPC mappings to close
+    unsigned long long** d_flags = nullptr;
+    double** d_dtr = nullptr;
+  } p2p;
 
   LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
     LeanSoA L;
@@ -707,6 +829,8 @@ DeviceSolver::~DeviceSolver() {
   graph.reset();
   host_comm.reset();
   if (impl) {
+    if (impl->stream) (void)hipStreamSynchronize(impl->stream);
+    for (void* p : impl->p2p.opened) (void)hipIpcCloseMemHandle(p);
     if (impl->comm) ncclCommDestroy(impl->comm);
     if (impl->sc_host) (void)hipHostFree(impl->sc_host);
     if (impl->res_host) (void)hipHostFree(impl->res_host);
@@ -882,7 +1006,14 @@ void DeviceSolver::sync_scalars() {
   std::memcpy(&dt, &m.sc_host->dt_bits[slot], 8);
   cur_time_part = m.sc_host->time_part - time_offset;
   last_dev_time = m.sc_host->time_part;
-  if (comm->allreduce_max_int(m.sc_host->neg_T)) {
+  const int err = comm->allreduce_max_int(m.sc_host->neg_T);
+  if (err & 2) {
+    char b[256];
+    std::snprintf(b, sizeof b, "ERROR: P2P halo exchange timed out (peer rank not responding) before iteration %ld",
+                  last_iter + iter);
+    throw std::runtime_error(b);
+  }
+  if (err) {
     char b[256];
     std::snprintf(b, sizeof b, "ERROR: Computational unstability (Tg < 0) before iteration %ld", last_iter + iter);
     throw std::runtime_error(b);
@@ -1002,6 +1133,103 @@ void DeviceSolver::init_local(std::shared_ptr<LocalGroup> g, int rank) {
   comm = host_comm.get();
 }
 
+namespace {
+struct P2PDesc {
+  uint32_t magic;
+  int32_t pid, device, rank, nranks, pad;
+  uint64_t ptr, bytes;
+  char handle[HIP_IPC_HANDLE_SIZE];
+};
+constexpr uint32_t P2P_MAGIC = 0x68663270;   // "hf2p"
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+std::string DeviceSolver::p2p_export(int rank, int nranks) {
+  HIP_CHECK(hipSetDevice(dev));
+  Impl& m = *impl;
+  if (m.p2p.base) throw std::runtime_error("p2p_export: mailbox already exported");
+  if (nranks < 1 || rank < 0 || rank >= nranks) throw std::runtime_error("p2p_export: bad rank/nranks");
+  m.rank = rank;
+  m.nranks = nranks;
+  Impl::P2P& p = m.p2p;
+  p.off_dtr = align_up((size_t)nranks * 8, 256);
+  p.off_recv = align_up(p.off_dtr + (size_t)2 * nranks * 8, 256);
+  p.bytes = p.off_recv + (size_t)4 * m.halo_cap * sizeof(real);
+  void* b = nullptr;
+  HIP_CHECK(hipExtMallocWithFlags(&b, p.bytes, hipDeviceMallocFinegrained));
+  m.mem.ptrs.push_back(b);
+  p.base = (char*)b;
+  HIP_CHECK(hipMemset(p.base, 0, p.bytes));
+  p.seq = m.mem.alloc<unsigned long long>(1);
+  HIP_CHECK(hipDeviceSynchronize());
+  P2PDesc d{};
+  d.magic = P2P_MAGIC;
+  d.pid = (int32_t)getpid();
+  d.device = dev;
+  d.rank = rank;
+  d.nranks = nranks;
+  d.ptr = (uint64_t)(uintptr_t)p.base;
+  d.bytes = p.bytes;
+  hipIpcMemHandle_t h;
+  HIP_CHECK(hipIpcGetMemHandle(&h, p.base));
+  std::memcpy(d.handle, &h, sizeof(h));
+  return std::string((const char*)&d, sizeof d);
+}
+
+void DeviceSolver::p2p_import(const std::vector<std::string>& descs) {
+  HIP_CHECK(hipSetDevice(dev));
+  Impl& m = *impl;
+  Impl::P2P& p = m.p2p;
+  if (!p.base) throw std::runtime_error("p2p_import before p2p_export");
+  if ((int)descs.size() != m.nranks) throw std::runtime_error("p2p_import: need one descriptor per rank");
+  p.peer_base.assign(m.nranks, nullptr);
+  for (int q = 0; q < m.nranks; q++) {
+    P2PDesc d;
+    if (descs[q].size() != sizeof d) throw std::runtime_error("p2p_import: bad descriptor size");
+    std::memcpy(&d, descs[q].data(), sizeof d);
+    if (d.magic != P2P_MAGIC || d.rank != q || d.nranks != m.nranks || d.bytes != p.bytes)
+      throw std::runtime_error("p2p_import: descriptor mismatch (rank " + std::to_string(q) + ")");
+    if (q == m.rank) {
+      p.peer_base[q] = p.base;
+    } else if (d.pid == (int32_t)getpid()) {   // in-process virtual rank
+      if (d.device != dev) {
+        const hipError_t e = hipDeviceEnablePeerAccess(d.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(e);
+        (void)hipGetLastError();
+      }
+      p.peer_base[q] = (char*)(uintptr_t)d.ptr;
+    } else {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, d.handle, sizeof h);
+      void* ptr = nullptr;
+      HIP_CHECK(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+      p.opened.push_back(ptr);
+      p.peer_base[q] = (char*)ptr;
+    }
+  }
+  std::vector<unsigned long long*> fl(m.nranks);
+  std::vector<double*> dr(m.nranks);
+  for (int q = 0; q < m.nranks; q++) {
+    fl[q] = (unsigned long long*)p.peer_base[q];
+    dr[q] = (double*)(p.peer_base[q] + p.off_dtr);
+  }
+  p.d_flags = m.mem.alloc<unsigned long long*>(m.nranks);
+  p.d_dtr = m.mem.alloc<double*>(m.nranks);
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(p.d_flags, fl.data(), m.nranks * sizeof(void*), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(p.d_dtr, dr.data(), m.nranks * sizeof(void*), hipMemcpyHostToDevice));
+  p.on = m.nranks > 1;
+}
+
+bool DeviceSolver::p2p_active() const { return impl->p2p.on; }
+
+void DeviceSolver::p2p_set(bool on) {
+  flush_pending();
+  if (on && (impl->p2p.peer_base.empty() || impl->nranks < 2)) throw std::runtime_error("p2p_set: no imported peers");
+  impl->p2p.on = on;
+  graph.reset();   // captured exchanges belong to the old transport
+}
+
 int DeviceSolver::comm_rank() const { return impl->rank; }
 int DeviceSolver::comm_size() const { return impl->nranks; }
 
@@ -1012,7 +1240,7 @@ int DeviceSolver::comm_size() const { return impl->nranks; }
 // send/recv group plus an all-reduce.
 void DeviceSolver::exchange(int group, int dt_slot) {
   Impl& m = *impl;
-  if ((!m.comm && !m.local) || m.nranks == 1) return;
+  if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
   const int ny = h.ny;
   const long N = h.N;
   ColList L;
@@ -1051,6 +1279,36 @@ void DeviceSolver::exchange(int group, int dt_slot) {
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   const int sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
+  if (m.p2p.on) {
+    if (L.nf * ny > m.halo_cap) throw std::runtime_error("p2p halo exceeds mailbox capacity");
+    Impl::P2P& p = m.p2p;
+    P2PArgs a;
+    a.L = L;
+    a.first = first;
+    a.last = last;
+    a.ghostL = 0;
+    a.ghostR = h.nx - 1;
+    a.ny = ny;
+    a.cnt = cnt;
+    a.sides = sides;
+    a.cap = m.halo_cap;
+    a.peer_recv_l = has_left ? (real*)(p.peer_base[m.rank - 1] + p.off_recv) : nullptr;
+    a.peer_recv_r = has_right ? (real*)(p.peer_base[m.rank + 1] + p.off_recv) : nullptr;
+    a.my_recv = (real*)(p.base + p.off_recv);
+    a.peer_flags = p.d_flags;
+    a.peer_dtr = p.d_dtr;
+    a.my_flags = (unsigned long long*)p.base;
+    a.my_dtr = (double*)(p.base + p.off_dtr);
+    a.seq = p.seq;
+    a.sc = m.sc;
+    a.dslot = dt_slot >= 0 ? dt_slot : 0;
+    a.fold_dt = dt_slot >= 0 ? 1 : 0;
+    a.rank = m.rank;
+    a.nranks = m.nranks;
+    hipLaunchKernelGGL(hf2d_p2p_xchg, dim3(1), dim3(P2P_THREADS), 0, m.stream, a);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, first, last, ny, m.halo_send[0],
                      m.halo_send[1], sides);
   const bool gather_dt = dt_slot >= 0;
@@ -1144,7 +1402,9 @@ void DeviceSolver::flush_pending() {
 
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   Impl& m = *impl;
-  const bool plain = use_graph && !want_res && !step_outputs && !m.local && !(lean && lean_ok && lean_state == 0);
+  // (the in-process host transport synchronises on the host: eager only)
+  const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
+                     !(lean && lean_ok && lean_state == 0);
   if (!plain || (pending.empty() && nstep % GRAPH_STEPS != 0)) {
     flush_pending();
     return do_step_eager(P0, want_res);
@@ -1355,7 +1615,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     pbuf = 1 - pbuf;
   }
   // new-state halo + global dt (MIN over ranks into the next slot)
-  if ((m.comm || m.local) && m.nranks > 1) exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
+  if ((m.comm || m.local || m.p2p.on) && m.nranks > 1)
+    exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
   if (!cs.cfg.isAdiabaticWall) {
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     hipLaunchKernelGGL(hf2d_wall_solid, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1);

@@ -77,6 +77,14 @@ class DeviceSolver : public SolverBase {
   void init_comm(const std::string& uid, int rank, int nranks);
   // in-process virtual ranks (tests on one GPU; see LocalGroup)
   void init_local(std::shared_ptr<LocalGroup> g, int rank);
+  // Multi-GPU: xGMI peer-to-peer mailboxes (hf2d_p2p_xchg).  Every rank
+  // exports a descriptor, the descriptors are all-gathered by the caller
+  // (torch.distributed, any backend) and imported on every rank; from then on
+  // the per-step halo + dt exchange is one device kernel (no RCCL, no host).
+  std::string p2p_export(int rank, int nranks);
+  void p2p_import(const std::vector<std::string>& descs);
+  bool p2p_active() const;
+  void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import
   int comm_rank() const;
   int comm_size() const;
   void exchange(int group, int dt_slot = -1);

@@ -1,10 +1,13 @@
 """Distributed runner: one process per GPU (or per CPU rank), torchrun-style env.
 
-GPU ranks: torch.distributed only bootstraps — rank 0 creates an RCCL unique
-id which is broadcast over the default process group; afterwards every
-per-step exchange (halo send/recv to the strip neighbours, MIN all-reduce of
-dt) is issued by the native DeviceSolver with RCCL on its own HIP stream, so
-the inner loop never returns to Python.
+GPU ranks: torch.distributed only bootstraps.  By default every rank exports
+an IPC descriptor of its fine-grained xGMI mailbox, the descriptors are
+all-gathered once, and afterwards each step's exchange (halo columns to the
+strip neighbours + every rank's dt, MIN-folded on device) is ONE device kernel
+per rank (DeviceSolver p2p transport, hf2d_p2p_xchg).  ``transport="rccl"``
+(or HF2D_TRANSPORT=rccl) instead issues pack + grouped ncclSend/ncclRecv +
+unpack on the solver stream.  Either way the inner loop never returns to
+Python and is captured in step graphs.
 
 CPU ranks (tests, gloo): the native CpuSolver calls back into Python for the
 halo columns and the scalar reductions, which go over torch.distributed.
@@ -37,7 +40,7 @@ class DistributedSimulation:
 
     def __init__(self, deck_text: str, backend: str = "gpu", *, rank: int = 0, world: int = 1,
                  device: int = 0, semantics: str = "mpi", fused: bool = True, lean: bool = True, parts=None,
-                 workdir: str = ".", use_checkpoint: bool = False):
+                 workdir: str = ".", use_checkpoint: bool = False, transport: Optional[str] = None):
         from .. import native
 
         hf = native()
@@ -49,16 +52,13 @@ class DistributedSimulation:
         self.parts = parts or balanced_columns(solid, world)
         gi0, gi1 = self.parts[rank]
         self.backend = backend
+        self.transport = "none"
         if backend == "gpu":
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
             self.solver.lean = lean
             if world > 1:
-                import torch.distributed as dist
-
-                obj = [hf.DeviceSolver.nccl_unique_id() if rank == 0 else None]
-                dist.broadcast_object_list(obj, src=0)
-                self.solver.init_comm(obj[0], rank, world)
+                self._wire_gpu(transport or os.environ.get("HF2D_TRANSPORT", "p2p"))
         elif backend == "cpu":
             self.solver = hf.CpuSolver(self.case, gi0, gi1)
             self.solver.lean = lean
@@ -66,6 +66,99 @@ class DistributedSimulation:
                 self._wire_cpu()
         else:
             raise ValueError(backend)
+
+    # -- GPU transports -------------------------------------------------------
+    def _wire_gpu(self, transport: str):
+        """Per-step halo + dt exchange between the strip GPUs.
+
+        ``p2p`` (default): xGMI peer-to-peer mailboxes -- the descriptors of
+        every rank's IPC-exported mailbox are all-gathered here once, then each
+        step exchanges with one device kernel (no RCCL launch, no host).
+        ``rccl``: pack kernel + grouped ncclSend/ncclRecv + unpack kernel.
+        Host-side reductions (output steps only) use RCCL when the process
+        group is NCCL/RCCL, else torch.distributed callbacks.  If any rank
+        cannot map its peers' mailboxes, every rank falls back to RCCL.
+        """
+        import torch
+        import torch.distributed as dist
+
+        if transport not in ("p2p", "rccl"):
+            raise ValueError("transport must be p2p or rccl, got %r" % transport)
+        s = self.solver
+        rank, world = self.rank, self.world
+        nccl = dist.get_backend() == "nccl"
+        if nccl or transport == "rccl":
+            obj = [self.hf.DeviceSolver.nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            s.init_comm(obj[0], rank, world)
+        else:
+            s.set_comm(rank, world, *self._py_comm_funcs())
+        self.transport = "rccl"
+        if transport != "p2p":
+            return
+        ok = 1
+        err = ""
+        try:
+            desc = s.p2p_export(rank, world)
+        except Exception as e:  # pragma: no cover - hardware dependent
+            desc, ok, err = b"", 0, str(e)
+        descs = [None] * world
+        dist.all_gather_object(descs, desc)
+        if ok and all(descs):
+            try:
+                s.p2p_import(descs)
+            except Exception as e:  # pragma: no cover - hardware dependent
+                ok, err = 0, str(e)
+        else:
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32)
+        if nccl:
+            flag = flag.cuda()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
+            self.transport = "p2p"
+        else:
+            s.p2p_active = False
+            if not nccl:
+                obj = [self.hf.DeviceSolver.nccl_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                s.init_comm(obj[0], rank, world)
+            if err:
+                print("[hf2d rank %d] p2p transport unavailable (%s); using RCCL" % (rank, err), flush=True)
+
+    def _py_comm_funcs(self):
+        import torch
+        import torch.distributed as dist
+
+        rank, world = self.rank, self.world
+
+        def fmin(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return float(t.item())
+
+        def fsum(v):
+            t = torch.tensor([v], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return float(t.item())
+
+        def fmaxi(v):
+            t = torch.tensor([v], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return int(t.item())
+
+        def fres(b):
+            arr = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+            out = [torch.empty_like(arr) for _ in range(world)]
+            dist.all_gather(out, arr)
+            return b"".join(bytes(o.numpy().tobytes()) for o in out)
+
+        def fgather(gi0, gi1, strip):
+            out = [None] * world if rank == 0 else None
+            dist.gather_object((gi0, gi1, bytes(strip)), out, dst=0)
+            return out
+
+        return fmin, fsum, fmaxi, fres, fgather
 
     # -- gloo wiring for the CPU stepper ------------------------------------
     def _wire_cpu(self):
@@ -100,34 +193,8 @@ class DistributedSimulation:
             if "r" in bufs:
                 solver.unpack_column(group, n_loc - 1, bufs["r"].numpy())
 
-        def fmin(v):
-            t = torch.tensor([v], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            return float(t.item())
-
-        def fsum(v):
-            t = torch.tensor([v], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            return float(t.item())
-
-        def fmaxi(v):
-            t = torch.tensor([v], dtype=torch.int64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return int(t.item())
-
-        def fres(b):
-            arr = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-            out = [torch.empty_like(arr) for _ in range(world)]
-            dist.all_gather(out, arr)
-            return b"".join(bytes(o.numpy().tobytes()) for o in out)
-
-        def fgather(gi0, gi1, strip):
-            out = [None] * world if rank == 0 else None
-            dist.gather_object((gi0, gi1, bytes(strip)), out, dst=0)
-            return out
-
         s.set_exchange(exchange)
-        s.set_comm(rank, world, fmin, fsum, fmaxi, fres, fgather)
+        s.set_comm(rank, world, *self._py_comm_funcs())
 
     def step(self, n: int, residual: bool = False):
         self.solver.run_steps(int(n), bool(residual))

@@ -120,9 +120,11 @@ def test_lean_bitwise_with_switches(gpu):
     np.testing.assert_array_equal(rg, rc)
 
 
-def _virtual_ranks(hf, text, nranks, schedule, lean=True):
+def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
-    host thread each, halos through the in-process LocalGroup transport."""
+    host thread each, halos through the in-process LocalGroup transport (or,
+    p2p=True, the device-side mailbox transport: one exchange kernel per step,
+    step graphs on)."""
     import threading
 
     from openhyperflow2d_amd.parallel.strips import balanced_columns
@@ -137,6 +139,11 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True):
         s.lean = lean
         s.init_local(group, r)
         solvers.append(s)
+    if p2p:
+        descs = [s.p2p_export(r, nranks) for r, s in enumerate(solvers)]
+        for s in solvers:
+            s.p2p_import(descs)
+            assert s.p2p_active
     errors = []
 
     def run(s, n, res):
@@ -153,6 +160,8 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True):
             t.join(timeout=120)
         assert not errors, errors
         assert not any(t.is_alive() for t in th), "virtual-rank step hung"
+    if p2p:
+        assert all(s.graph_launches > 0 for s in solvers) or max(n for n, _ in schedule) < 12
     out = {}
     for f in FIELDS:
         full = None
@@ -177,6 +186,74 @@ def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
     for n, res in schedule:
         ref.step(n, residual=res)
     assert summ["dt"] == ref.summary()["dt"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+# <= 3 in-process ranks: their streams must land on distinct hardware queues
+# (GPU_MAX_HW_QUEUES=4) or a spinning exchange could sit in front of the step
+# it waits for; separate processes (the real deployment) have no such limit.
+@pytest.mark.parametrize("nranks,physics,lean", [(2, "euler", True), (3, "euler", True), (3, "kes", False)])
+def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
+    """xGMI mailbox transport (hf2d_p2p_xchg: direct peer stores, system-scope
+    flags, device-side dt MIN) inside captured step graphs == one GPU, bit for
+    bit (in-process ranks share the device; the protocol is the multi-GPU one)."""
+    ns = physics != "euler"
+    text = decks.wedge15(240, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
+    schedule = [(5, True), (30, False), (7, True), (25, False)]
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean, p2p=True)
+    ref = gpu.Simulation(text, "gpu", lean=lean)
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
+    assert summ["time"] == ref.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def _p2p_proc_worker(rank, world, port, text, schedule, out):
+    import os
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from openhyperflow2d_amd.parallel.dist import DistributedSimulation
+
+    sim = DistributedSimulation(text, "gpu", rank=rank, world=world, device=0, transport="p2p")
+    assert sim.transport == "p2p", sim.transport
+    for n, res in schedule:
+        sim.step(n, residual=res)
+    fields = {f: sim.gather_field(f) for f in FIELDS}
+    if rank == 0:
+        np.savez(out, dt=sim.summary()["dt"], graphs=sim.solver.graph_launches, **fields)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_p2p_two_processes_ipc(gpu, tmp_path):
+    """Two OS processes (one GPU, gloo bootstrap): mailboxes mapped through
+    hipIpcOpenMemHandle, the exact multi-GPU code path; == one GPU bitwise."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    text = decks.wedge15(240, 60, nmax=10 ** 6, nout=10 ** 5)
+    schedule = [(5, True), (30, False), (7, True)]
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    out = str(tmp_path / "p2p.npz")
+    mp.start_processes(_p2p_proc_worker, args=(2, port, text, schedule, out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    assert int(got["graphs"]) > 0
+    ref = gpu.Simulation(text, "gpu")
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert float(got["dt"]) == ref.summary()["dt"]
     for f in FIELDS:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
