@@ -48,7 +48,7 @@ def _ninja_file() -> str:
         f"cxxflags = {common} -x c++ -I{CSRC}",
         f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC}",
         f"pyflags = -I{_pybind_include()} -I{py_inc}",
-        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx",
         "rule cxx",
         "  command = $hipcc $cxxflags $extra -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",

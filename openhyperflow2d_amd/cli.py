@@ -3,6 +3,8 @@
   python -m openhyperflow2d_amd run  deck.dat [--backend gpu|cpu|ref] [--cycles N]
                                      [--outdir DIR] [--semantics mpi|serial]
                                      [--no-checkpoint] [--no-lean] [--metrics FILE]
+                                     [--profile FILE] [--fault-inject step:N,rank:R,kind:nan|kill]
+                                     [--transport p2p|rccl]
   python -m openhyperflow2d_amd deck wedge15 --nx 2000 --ny 200 -o w.dat
   python -m openhyperflow2d_amd info deck.dat
   python -m openhyperflow2d_amd build
@@ -51,7 +53,7 @@ def _cmd_run(a) -> int:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         sim = DistributedSimulation(text, backend, rank=rank, world=world, device=local_rank,
                                     semantics=a.semantics, lean=not a.no_lean, workdir=workdir,
-                                    use_checkpoint=not a.no_checkpoint)
+                                    use_checkpoint=not a.no_checkpoint, transport=a.transport)
     else:
         sim = hf.Simulation(text, backend, workdir=workdir, use_checkpoint=not a.no_checkpoint,
                             semantics=a.semantics, device=a.device,
@@ -60,8 +62,13 @@ def _cmd_run(a) -> int:
     if rank == 0:
         print("hf2d: %s  %dx%d  backend=%s  ranks=%d" % (os.path.basename(a.deck), sim.case.nx, sim.case.ny,
                                                           backend, world), flush=True)
-    cycles, log = sim.run(max_cycles=a.cycles, outdir=outdir, outputs=True, checkpoint=not a.no_checkpoint,
-                          verbose=True, metrics=a.metrics or "")
+    try:
+        cycles, log = sim.run(max_cycles=a.cycles, outdir=outdir, outputs=True, checkpoint=not a.no_checkpoint,
+                              verbose=True, metrics=a.metrics or "", profile=a.profile or "",
+                              fault=a.fault_inject or "")
+    except RuntimeError as e:
+        print(str(e), file=sys.stderr, flush=True)
+        return 3
     if rank == 0:
         sys.stdout.write(log)
         print("\nReady. Computation finished (%d cycles)." % cycles, flush=True)
@@ -131,6 +138,10 @@ def main(argv=None) -> int:
     r.add_argument("--no-lean", action="store_true")
     r.add_argument("--device", type=int, default=0)
     r.add_argument("--metrics", help="append per-output-step JSON lines to this file")
+    r.add_argument("--profile", help="write per-phase wall-clock JSON (steps/sync/gather/outputs) to this file")
+    r.add_argument("--fault-inject", dest="fault_inject", metavar="SPEC",
+                   help="step:N[,rank:R][,kind:nan|kill] -- test hook for the failure/restart paths")
+    r.add_argument("--transport", choices=["p2p", "rccl"], help="multi-GPU exchange (default p2p)")
     d = sub.add_parser("deck", help="write a generated deck")
     d.add_argument("name")
     d.add_argument("--nx", type=int)

@@ -267,6 +267,13 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("run_steps", &SolverBase::run_steps, py::arg("n"), py::arg("want_residual_last") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("advance", [](SolverBase& s, bool want) { s.advance(want); }, py::arg("want_residual") = false)
+      .def_property_readonly("phase_times",
+                             [](const SolverBase& s) {
+                               py::dict d;
+                               for (const auto& kv : s.phase_acc)
+                                 d[py::str(kv.first)] = py::make_tuple(kv.second.first, kv.second.second);
+                               return d;
+                             })
       .def("set_comm",
            [](SolverBase& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
               std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres,
@@ -285,23 +292,33 @@ PYBIND11_MODULE(_hf2d, m) {
            py::arg("fgather") = nullptr)
       .def("run",
            [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose,
-              const std::string& metrics) {
+              const std::string& metrics, const std::string& profile, long fault_step, int fault_rank,
+              const std::string& fault_kind) {
              RunOptions o;
              o.metrics_path = metrics;
+             o.profile_path = profile;
+             o.fault_step = fault_step;
+             o.fault_rank = fault_rank;
+             o.fault_kind = fault_kind;
              o.max_cycles = max_cycles;
              o.outdir = outdir;
              o.write_outputs = outputs;
              o.write_checkpoint = checkpoint;
              std::ostringstream log;
              int n;
-             {
+             try {
                py::gil_scoped_release rel;   // comm callbacks re-acquire it
                n = s.run(o, verbose ? &log : nullptr);
+             } catch (const std::exception& e) {
+               // keep the driver log (it names the error snapshot / last checkpoint)
+               throw std::runtime_error(std::string(e.what()) + "\n--- driver log ---\n" + log.str());
              }
              return py::make_tuple(n, log.str());
            },
            py::arg("max_cycles") = 1, py::arg("outdir") = ".", py::arg("outputs") = true,
-           py::arg("checkpoint") = true, py::arg("verbose") = true, py::arg("metrics") = "")
+           py::arg("checkpoint") = true, py::arg("verbose") = true, py::arg("metrics") = "",
+           py::arg("profile") = "", py::arg("fault_step") = -1, py::arg("fault_rank") = 0,
+           py::arg("fault_kind") = "nan")
       .def("download", [](SolverBase& s) { s.download(s.cs.J); })
       .def("upload", &SolverBase::upload)
       .def("sync", &SolverBase::sync_scalars)

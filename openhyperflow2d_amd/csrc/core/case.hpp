@@ -97,6 +97,7 @@ class Case {
   real dt0 = 1.0;
   real global_time = 0.0;
   bool preloaded = false;
+  long restart_iter = 0;     // iteration count from the .hf2d.meta sidecar of a preloaded checkpoint
   std::string swap_path;     // resolved checkpoint path ("" = none)
   std::ostream* log = nullptr;
 

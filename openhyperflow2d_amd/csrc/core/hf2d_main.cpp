@@ -33,8 +33,9 @@ int main(int argc, char** argv) {
     std::printf("\n\n\tFlowNode2D size = %d bytes\n\n", (int)sizeof(CellRecord));
     return 0;
   }
-  std::string backend, deck_path, outdir = ".";
+  std::string backend, deck_path, outdir = ".", profile, fault_kind = "nan";
   int cycles = -1, device = -1;
+  long fault_step = -1;
   bool serial = false, use_ckpt = true;
   for (int a = 1; a < argc; a++) {
     std::string s = argv[a];
@@ -44,6 +45,9 @@ int main(int argc, char** argv) {
     else if (s == "--no-checkpoint") use_ckpt = false;
     else if (s == "--outdir" && a + 1 < argc) outdir = argv[++a];
     else if (s == "--device" && a + 1 < argc) device = std::atoi(argv[++a]);
+    else if (s == "--profile" && a + 1 < argc) profile = argv[++a];
+    else if (s == "--fault-step" && a + 1 < argc) fault_step = std::atol(argv[++a]);
+    else if (s == "--fault-kind" && a + 1 < argc) fault_kind = argv[++a];
     else deck_path = s;
   }
   try {
@@ -69,6 +73,9 @@ int main(int argc, char** argv) {
     RunOptions opt;
     opt.max_cycles = cycles;
     opt.outdir = outdir;
+    opt.profile_path = profile;
+    opt.fault_step = fault_step;
+    opt.fault_kind = fault_kind;
     solver->run(opt, &std::cout);
     std::cout << "\nResults saved in file \"" << cs.cfg.out_file << "\".\n";
     std::cout << "\nReady. Computation finished.\n";

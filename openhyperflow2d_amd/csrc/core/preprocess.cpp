@@ -563,6 +563,11 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
     if (read_hf2d(swap_path, J)) {
       preloaded = true;
       say("Mapping computation area...OK (preloaded " + swap_path + ")\n");
+      // the reference restarts its iteration counter at 0 (it is not in the
+      // .hf2d image); the sidecar makes a resumed run continue the count
+      double mdt = 0, mtime = 0;
+      long mit = 0;
+      if (read_meta(swap_path, mit, mdt, mtime) && mit > 0) restart_iter = mit;
     }
   }
   const bool PreloadFlag = preloaded;

@@ -199,6 +199,7 @@ SolverBase::SolverBase(Case& c) : cs(c) {
   comm = &local_comm;
   dt = c.dt0;
   dt_running = c.dt0;
+  last_iter = c.restart_iter;
 }
 
 StepParams SolverBase::make_params(long it) const {
@@ -340,7 +341,111 @@ void install_signal_handlers() {
   sigaction(SIGTERM, &sa, nullptr);
 }
 
+namespace {
+using pclk = std::chrono::steady_clock;
+
+// Wall-clock + profiler range around one driver phase.
+struct PhaseScope {
+  SolverBase& s;
+  const char* name;
+  pclk::time_point t0;
+  PhaseScope(SolverBase& s_, const char* n) : s(s_), name(n), t0(pclk::now()) { s.trace_push(n); }
+  ~PhaseScope() {
+    s.trace_pop();
+    auto& a = s.phase_acc[name];
+    a.first += std::chrono::duration<double>(pclk::now() - t0).count();
+    a.second++;
+  }
+};
+
+std::string plt_stem(const std::string& f) {
+  const size_t dot = f.rfind('.');
+  return dot == std::string::npos ? f : f.substr(0, dot);
+}
+}  // namespace
+
+void SolverBase::write_profile(const std::string& path, int cycles) const {
+  std::FILE* f = std::fopen(path.c_str(), "w");
+  if (!f) return;
+  double total = 0;   // top-level phases (nested ones are named "<parent>.<child>")
+  for (const auto& kv : phase_acc)
+    if (kv.first.find('.') == std::string::npos) total += kv.second.first;
+  const double iters = (double)(last_iter + iter);
+  std::fprintf(f, "{\"rank\": %d, \"ranks\": %d, \"grid\": [%d, %d], \"cycles\": %d, \"iterations\": %.0f, "
+               "\"seconds\": %.6f, \"mcells_it_per_s\": %.6g, \"phases\": {",
+               comm->rank(), comm->size(), cs.cfg.MaxX, cs.cfg.MaxY, cycles, iters, total,
+               total > 0 ? iters * cs.cfg.MaxX * cs.cfg.MaxY / total / 1e6 : 0.0);
+  bool first = true;
+  for (const auto& kv : phase_acc) {
+    std::fprintf(f, "%s\"%s\": {\"seconds\": %.6f, \"calls\": %ld}", first ? "" : ", ", kv.first.c_str(),
+                 kv.second.first, kv.second.second);
+    first = false;
+  }
+  std::fprintf(f, "}}\n");
+  std::fclose(f);
+}
+
+// Numerical failure (Tg < 0) or transport failure: write the error snapshot
+// <Project>-err.plt (multi-rank: rank-<r>-<Project>-err.plt with that rank's
+// strip, as the reference names them per rank), keep the last good
+// checkpoint of the previous cycle for a restart, and report where.
+void SolverBase::failure_snapshot(const RunOptions& opt, const std::string& dir, const std::string& why,
+                                  std::ostream* log) {
+  Config& C = cs.cfg;
+  const int nr = comm->size(), r = comm->rank();
+  try {
+    download(cs.J);   // device state at the failing step
+  } catch (...) {
+  }
+  const std::string name = (nr > 1 ? "rank-" + std::to_string(r) + "-" : std::string()) + plt_stem(C.out_file) +
+                           "-err.plt";
+  if (opt.write_outputs) save_field_plt(dir + "/" + name, cs, cs.J, cs.global_time + cur_time_part, true);
+  if (log && (r == 0 || nr > 1)) {
+    *log << "\n" << why << "\nError snapshot: " << dir << "/" << name;
+    if (opt.write_checkpoint)
+      *log << "; last good checkpoint (iteration " << last_iter << "): " << dir << "/" << C.swap_file;
+    *log << "\n" << std::flush;
+  }
+}
+
+void SolverBase::inject_fault(const RunOptions& opt) {
+  if (opt.fault_kind == "kill") {
+    std::fflush(stdout);
+    std::raise(SIGKILL);
+    return;
+  }
+  // an active gas cell nearest the centre of this rank's strip
+  const auto own = owned_columns();
+  const Field& J = cs.J;
+  const int ci = (own.first + own.second) / 2, cj = J.ny / 2;
+  for (int d = 0; d < std::max(J.nx, J.ny); d++)
+    for (int i = std::max(own.first, ci - d); i <= std::min(own.second - 1, ci + d); i++)
+      for (int j = std::max(0, cj - d); j <= std::min(J.ny - 1, cj + d); j++) {
+        const u64 CT = J.at(i, j).CT;
+        if (has_all(CT, CT_NODE_IS_SET) && !has_all(CT, CT_SOLID) && !has_all(CT, NT_FC)) {
+          poison_cell(i, j);
+          return;
+        }
+      }
+}
+
 int SolverBase::run(const RunOptions& opt, std::ostream* log) {
+  const std::string dir0 = opt.outdir.empty() ? "." : opt.outdir;
+  int cycles = 0;
+  try {
+    cycles = run_cycles(opt, log);
+  } catch (const std::runtime_error& e) {
+    const std::string msg = e.what();
+    if (msg.find("unstability") != std::string::npos || msg.find("P2P") != std::string::npos)
+      failure_snapshot(opt, dir0, msg, log);
+    if (!opt.profile_path.empty()) write_profile(opt.profile_path, cycle);
+    throw;
+  }
+  if (!opt.profile_path.empty()) write_profile(opt.profile_path, cycles);
+  return cycles;
+}
+
+int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
   Config& C = cs.cfg;
   const bool root = comm->rank() == 0;
   const std::string dir = opt.outdir.empty() ? "." : opt.outdir;
@@ -363,8 +468,13 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
     for (long k = 0; k < C.Nmax; k++) {
       const bool out_step = (iter / C.NOutStep) * C.NOutStep == iter;
       const long this_iter = iter;
+      if (opt.fault_step >= 0 && last_iter + iter == opt.fault_step && comm->rank() == opt.fault_rank)
+        inject_fault(opt);
       step_outputs = out_step || k == C.Nmax - 1;
-      advance(out_step || k == C.Nmax - 1);
+      {
+        PhaseScope ph(*this, "steps");
+        advance(out_step || k == C.Nmax - 1);
+      }
       step_outputs = true;
       if (out_step && comm->allreduce_max_int(stop_requested() ? 1 : 0)) {
         interrupted = true;
@@ -405,14 +515,18 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
         }
       }
     }
-    sync_scalars();
-    cycle_update();
-    if (cs.cfg.sources.size() && comm->size() == 1) {
-      // sources are re-applied every cycle in the MPI build (deeps2d_core.cpp:1716-1722)
+    {
+      PhaseScope ph(*this, "sync");
+      sync_scalars();
+      cycle_update();
     }
     Field& J = cs.J;
-    download(J);
-    if (comm->size() > 1) comm->gather_columns(J, owned_columns().first, owned_columns().second);
+    {
+      PhaseScope ph(*this, "gather");
+      download(J);
+      if (comm->size() > 1) comm->gather_columns(J, owned_columns().first, owned_columns().second);
+    }
+    PhaseScope ph_out(*this, "outputs");
     step_seconds = std::chrono::duration<double>(clk::now() - t_cycle).count();
     if (root) {
       for (size_t x = 0; x < C.xcuts.size() && log; x++) {
@@ -451,6 +565,7 @@ int SolverBase::run(const RunOptions& opt, std::ostream* log) {
              << " Fy = " << y_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body) << "\n";
       }
       if (opt.write_checkpoint) {
+        PhaseScope ph(*this, "outputs.checkpoint");   // nested in "outputs"
         write_hf2d(dir + "/" + C.swap_file, J);
         write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
       }
@@ -474,6 +589,13 @@ CpuSolver::CpuSolver(Case& c, int g0, int g1) : SolverBase(c), gi0(g0), gi1(g1 <
   h.allocate((gi1 - gi0) + lh + rh, c.J.ny);
   upload();
 }
+
+void CpuSolver::poison_cell(int gi, int j) {
+  const long idx = (long)(gi - gi0 + l_off) * h.ny + j;
+  h.S[sbuf][(long)I_RHOE * h.N + idx] = -1.0e30;
+}
+
+void RefSolver::poison_cell(int gi, int j) { cs.J.at(gi, j).S[I_RHOE] = -1.0e30; }
 
 void CpuSolver::upload() {
   h.from_field(cs.J, gi0 - l_off);

@@ -12,6 +12,7 @@
 #pragma once
 
 #include <functional>
+#include <map>
 #include <memory>
 #include <utility>
 #include <string>
@@ -73,6 +74,14 @@ struct RunOptions {
   std::string outdir = ".";
   bool verbose = true;
   std::string metrics_path;  // non-empty: append one JSON line per output step (metrics.jsonl)
+  // per-phase wall-clock profile (JSON written when run() returns or fails)
+  std::string profile_path;
+  // Fault injection (tests of the failure / restart paths): at global
+  // iteration fault_step on rank fault_rank, "nan" poisons one active cell
+  // (negative energy -> Tg < 0 -> error snapshot), "kill" raises SIGKILL.
+  long fault_step = -1;
+  int fault_rank = 0;
+  std::string fault_kind = "nan";
 };
 
 class SolverBase {
@@ -102,6 +111,7 @@ class SolverBase {
   void run_steps(long n, bool want_res_last = false);
   // Full DEEPS2D_Run driver.  Returns the number of cycles run.
   int run(const RunOptions& opt, std::ostream* log);
+  void write_profile(const std::string& path, int cycles) const;
 
   // Backend interface
   virtual StepResult do_step(const StepParams& P, bool want_res) = 0;
@@ -114,11 +124,22 @@ class SolverBase {
   // called after an outer-cycle roll-over (cur_time_part folded into global_time)
   virtual void on_cycle_roll() {}
   StepParams make_params(long it) const;
+  // Overwrite the energy of global cell (gi, j) (owned by this backend) with
+  // a negative value: fault injection for the Tg < 0 failure path.
+  virtual void poison_cell(int gi, int j) = 0;
+  // Profiler ranges around driver phases (device backends: roctx).
+  virtual void trace_push(const char*) {}
+  virtual void trace_pop() {}
+  // accumulated wall-clock seconds and entry count per driver phase
+  std::map<std::string, std::pair<double, long>> phase_acc;
   // global columns [first, second) this backend owns (strip decomposition)
   virtual std::pair<int, int> owned_columns() const { return {0, cs.J.nx}; }
 
  protected:
   bool isSrcAdd = false;
+  int run_cycles(const RunOptions& opt, std::ostream* log);
+  void failure_snapshot(const RunOptions& opt, const std::string& dir, const std::string& why, std::ostream* log);
+  void inject_fault(const RunOptions& opt);
 };
 
 // Graceful stop (SIGINT / SIGTERM): the driver finishes the current step,
@@ -147,6 +168,7 @@ class CpuSolver : public SolverBase {
   void download(Field& J) override;
   void upload() override;
   void cycle_update() override;
+  void poison_cell(int gi, int j) override;
 
   HostArrays h;
   int gi0, gi1;     // owned global columns
@@ -184,6 +206,7 @@ class RefSolver : public SolverBase {
   StepResult do_step(const StepParams& P, bool want_res) override;
   void download(Field&) override {}
   void upload() override {}
+  void poison_cell(int gi, int j) override;
   std::vector<CellRecord> core;   // FlowNodeCore2D scratch (NextNode)
 };
 

@@ -20,6 +20,7 @@
 // the next step's kernels read it from there.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <unistd.h>
 
 #include <condition_variable>
@@ -996,6 +997,19 @@ void DeviceSolver::download(Field& J) {
 }
 
 void DeviceSolver::on_cycle_roll() { time_offset = last_dev_time; }
+
+void DeviceSolver::poison_cell(int gi, int j) {
+  flush_pending();
+  Impl& m = *impl;
+  const long idx = (long)(gi - gi0 + l_off) * h.ny + j;
+  static const real bad = -1.0e30;
+  HIP_CHECK(hipMemcpyAsync(m.S[sbuf] + (long)I_RHOE * h.N + idx, &bad, sizeof bad, hipMemcpyHostToDevice, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+}
+
+// driver phases as roctx ranges (rocprofv3 --marker-trace)
+void DeviceSolver::trace_push(const char* name) { roctxRangePush(name); }
+void DeviceSolver::trace_pop() { roctxRangePop(); }
 
 void DeviceSolver::sync_scalars() {
   flush_pending();

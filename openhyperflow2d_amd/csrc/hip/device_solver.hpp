@@ -68,6 +68,9 @@ class DeviceSolver : public SolverBase {
   void cycle_update() override;
   void sync_scalars() override;
   void on_cycle_roll() override;
+  void poison_cell(int gi, int j) override;
+  void trace_push(const char* name) override;
+  void trace_pop() override;
   double time_offset = 0.0, last_dev_time = 0.0;
   void synchronize();
   void* stream() const;

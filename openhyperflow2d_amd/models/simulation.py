@@ -13,6 +13,27 @@ from typing import Optional
 import numpy as np
 
 
+def parse_fault(spec: str):
+    """``step:N[,rank:R][,kind:nan|kill]`` -> (N, R, kind); "" -> (-1, 0, "nan").
+
+    Fault injection for the failure paths: ``nan`` poisons one
+    active cell's energy at global iteration N on rank R (Tg < 0 -> error
+    snapshot ``<Project>-err.plt``, the last good checkpoint is kept),
+    ``kill`` SIGKILLs that rank (restart from the checkpoint)."""
+    if not spec:
+        return -1, 0, "nan"
+    kv = {}
+    for part in spec.split(","):
+        k, _, v = part.partition(":")
+        kv[k.strip()] = v.strip()
+    if "step" not in kv:
+        raise ValueError("fault spec needs step:N, got %r" % spec)
+    kind = kv.get("kind", "nan")
+    if kind not in ("nan", "kill"):
+        raise ValueError("fault kind must be nan or kill, got %r" % kind)
+    return int(kv["step"]), int(kv.get("rank", 0)), kind
+
+
 class Simulation:
     def __init__(self, deck_text: str, backend: Optional[str] = None, *, workdir: str = ".",
                  use_checkpoint: bool = False, device: int = 0, semantics: str = "mpi",
@@ -50,9 +71,10 @@ class Simulation:
         self.solver.run_steps(int(n), bool(residual))
 
     def run(self, max_cycles: int = 1, outdir: str = ".", outputs: bool = True, checkpoint: bool = True,
-            verbose: bool = True, metrics: str = ""):
+            verbose: bool = True, metrics: str = "", profile: str = "", fault: str = ""):
         """Reference driver: outer cycles with outputs; returns (cycles, log text)."""
-        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics)
+        step, rank, kind = parse_fault(fault)
+        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics, profile, step, rank, kind)
 
     def summary(self) -> dict:
         return dict(self.solver.summary())

@@ -19,6 +19,7 @@ from typing import Optional
 
 import numpy as np
 
+from ..models.simulation import parse_fault
 from .strips import balanced_columns
 
 
@@ -200,9 +201,10 @@ class DistributedSimulation:
         self.solver.run_steps(int(n), bool(residual))
 
     def run(self, max_cycles: int = 1, outdir: str = ".", outputs: bool = True, checkpoint: bool = True,
-            verbose: bool = True, metrics: str = ""):
+            verbose: bool = True, metrics: str = "", profile: str = "", fault: str = ""):
         """Full DEEPS driver (outer cycles, outputs on rank 0 after a strip gather)."""
-        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics)
+        step, rank, kind = parse_fault(fault)
+        return self.solver.run(max_cycles, outdir, outputs, checkpoint, verbose, metrics, profile, step, rank, kind)
 
     def summary(self):
         return dict(self.solver.summary())
