@@ -48,6 +48,9 @@ struct Config {
   int TurbMod = 0, TurbStartIter = 0, TurbExtModel = 0, isTurbulenceReset = 0;
   int FT = FT_FLAT, ProblemType = SM_EULER;
   real CFL = 0;
+  // new key (not in the reference): viscous time-step bound for N-S,
+  // dt <= ViscousCFL * rho / ((mu + mu_t) (1/dx^2 + 1/dy^2)); 0 = off (reference)
+  real ViscousCFL = 0;
   Table CFL_Scenario, beta_Scenario;
   int NSaveStep = 1, Nmax = 1, NOutStep = 1;
   int isAlternateRMS = 0, isIgnoreUnsetNodes = 0, MonitorIndex = 0;

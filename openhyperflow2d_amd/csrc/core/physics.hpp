@@ -33,6 +33,7 @@ struct FillParams {
   int isSrcAdd = 0;
   real turb_I = 0.005;    // FlowNodeTurbulence2D::I
   int sst_version = 2003; // new model (not in reference)
+  real dt = 0.0;          // time step of the fill's step (SST point-implicit destruction)
 };
 
 HF_HD inline real hf_max(real a, real b) { return a > b ? a : b; }
@@ -67,12 +68,19 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   const real bstar = 0.09, a1 = 0.31, kappa = 0.41;
   const real rho = n.S[I_RHO];
   const real dmin = hf_max(n.l_min, 1e-12);
+  // Free-stream / inflow omega: the mixing-length estimate, but never below
+  // k / (10 nu) (eddy-viscosity ratio <= 10, Menter's free-stream range).  A
+  // larger ratio at a Mach-8, low-density inflow (nu ~ 1e-3 m^2/s) makes the
+  // explicit viscous number nu_t dt / dx^2 exceed the stability bound on
+  // 0.1 mm grids, since dt follows the inviscid CFL only.
+  auto omega_inflow = [&](real kk_, real l_) {
+    return hf_max(std::sqrt(kk_) / (std::pow(bstar, 0.25) * l_), hf_max(kk_ / (10.0 * n.mu / rho + 1e-300), 1e-6));
+  };
   if (is_init) {
     const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
     const real kk = 1.5 * TmpI * TmpI;
     const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
-    const real om = hf_max(std::sqrt(kk) / (std::pow(bstar, 0.25) * l),
-                           hf_max(kk / (1.0e5 * n.mu / rho + 1e-300), 1e-6));
+    const real om = omega_inflow(kk, l);
     n.S[I_K] = rho * kk;
     n.S[I_OMEGA] = rho * om;
     n.mu_t = (om > 0) ? rho * kk / om : 0.0;
@@ -97,7 +105,7 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   const real om = hf_max(n.S[I_OMEGA] / rho, om_floor);
   if (has_all(n.TurbType, TCT_eps_CONST)) {
     const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
-    n.S[I_OMEGA] = rho * hf_max(std::sqrt(kk) / (std::pow(bstar, 0.25) * l), om_floor);
+    n.S[I_OMEGA] = rho * hf_max(omega_inflow(kk, l), om_floor);
   }
   // dkdx.. hold d(k)/dx and d(omega)/dx (already divided by rho, like the k-eps path)
   const real cross = n.dkdx * n.depsdx + n.dkdy * n.depsdy;
@@ -138,7 +146,15 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   n.B[I_K] -= n.RY[I_K];
   n.B[I_OMEGA] -= n.RY[I_OMEGA];
   n.SrcAdd[I_K] = n.SrcAdd[I_OMEGA] = 0.0;
-  if (!has_all(n.TurbType, TCT_k_CONST)) n.Src[I_K] = Pk - bstar * rho * om * kk;
+  // Point-implicit (Patankar) destruction: with the explicit DEEPS update the
+  // sink rho*phi*r (r = beta* omega for k, beta omega for omega) is applied as
+  // rho*phi*r / (1 + dt r), i.e. phi_new = phi / (1 + dt r) for the sink alone,
+  // which can never drive k or omega negative however large omega gets next to
+  // a no-slip wall (omega_w = 60 nu / (beta1 d^2)) on fine grids.
+  const real rk = bstar * om, rw = beta * om;
+  const real ik = P.dt > 0 ? 1.0 / (1.0 + P.dt * rk) : 1.0;
+  const real iw = P.dt > 0 ? 1.0 / (1.0 + P.dt * rw) : 1.0;
+  if (!has_all(n.TurbType, TCT_k_CONST)) n.Src[I_K] = Pk - rho * kk * rk * ik;
   if (!has_all(n.TurbType, TCT_eps_CONST)) {
     // production gamma * rho * S^2 (the Pk limiter applied through nu_t) and
     // the cross-diffusion term, each bounded by the destruction scale
@@ -146,7 +162,7 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
     const real cap = 10.0 * bstar * rho * om * om;
     const real Pw = hf_min(gam * rho / hf_max(mut, 1e-30) * Pk, cap);
     const real CD = hf_max(hf_min(2.0 * (1.0 - F1) * rho * so2 / om * cross, cap), -cap);
-    n.Src[I_OMEGA] = Pw - beta * rho * om * om + CD;
+    n.Src[I_OMEGA] = Pw - rho * om * rw * iw + CD;
   }
   const real FT = (real)P.FT;
   n.F[I_K] = FT * (n.mu + mut * sk) * n.dkdy;

@@ -217,6 +217,7 @@ StepParams SolverBase::make_params(long it) const {
   P.beta_min = std::min(C.beta0, beta_scen);
   P.nrbc_beta0 = C.nrbc_beta0;
   P.CFL_min = std::min(C.CFL, cfl_scen);
+  P.visc_cfl = C.ViscousCFL;
   P.bff = C.bff;
   P.alternate_rms = C.isAlternateRMS;
   P.sm = C.ProblemType;

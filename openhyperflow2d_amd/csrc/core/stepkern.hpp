@@ -99,6 +99,7 @@ struct StepParams {
   real beta_min;     // min(beta0, beta_Scenario(it))
   real nrbc_beta0;
   real CFL_min;      // min(CFL, CFL_Scenario(it))
+  real visc_cfl;     // Config::ViscousCFL (0: inviscid CFL only, as the reference)
   int bff;
   int alternate_rms;
   int do_residual;
@@ -522,6 +523,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   // those two fields rather than binding a runtime-selected reference into the
   // kernel-argument block (which makes the compiler copy StepParams to scratch).
   FillParams fp = P.fpa;
+  fp.dt = P.dt;
   if (!active) {
     fp.is_mu_t = P.ffc.is_mu_t;
     fp.is_init = P.ffc.is_init;
@@ -535,6 +537,10 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     } else {
       const real AAA = std::sqrt(c.k * c.R * c.Tg);
       dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(c.U)), P.dy / (AAA + std::fabs(c.V)));
+      if (P.visc_cfl > 0 && P.sm == SM_NS) {
+        const real nu_eff = (c.mu + c.mu_t) / c.S[I_RHO];
+        if (nu_eff > 0) dt_local = hf_min(dt_local, P.visc_cfl / (nu_eff * (1.0 / (P.dx * P.dx) + 1.0 / (P.dy * P.dy))));
+      }
       if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
       if (P.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, *P.species, P.dt);
     }

@@ -334,14 +334,14 @@ def resonator(nx: int = 2000, ny: int = 200, *, nmax: int = 200, nout: int = 100
 
 
 def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100, project: Optional[str] = None,
-             exit_time: float = 1.0e-30, chemistry: int = 2, turbulence: int = 4) -> str:
+             exit_time: float = 1.0e-30, chemistry: int = 2, turbulence: int = 6) -> str:
     """Axisymmetric Mach-8 H2/air scramjet channel: converging inlet, constant
     area combustor with a wall H2 injection slot, straight to the outlet.
     Finite-rate chemistry (ChemicalReactionsModel=2) and k-omega SST
-    (turbulence=6) are new physics keys (not in the reference).  The default
-    turbulence model is k-eps: the explicit SST source treatment still goes
-    unstable at the impulsive Mach-8 start on the 6000x400 grid
-    (tools/stability_probe.py), k-eps and laminar runs are stable.
+    (TurbulenceModel=6, the default here) are new physics keys (not in the
+    reference).  SST runs with point-implicit k/omega destruction and a
+    free-stream eddy-viscosity ratio <= 10; tools/stability_probe.py shows the
+    6000x400 start stable for 3000+ steps (profiles/sst_scramjet_probe.log).
     Domain 0.6 m x 0.04 m (dx = dy = 0.1 mm at 6000x400)."""
     t = remove_commented_directives(template_text("Wedge.dat"))
     project = project or "Scramjet_%dx%d" % (nx, ny)
