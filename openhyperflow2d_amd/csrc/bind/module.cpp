@@ -388,6 +388,10 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
+      .def_readwrite("lean_march", &DeviceSolver::lean_march)
+      .def_readwrite("lean_pipe", &DeviceSolver::lean_pipe)
+      .def_property("lean_sgtab", [](const DeviceSolver& d) { return d.lean_sgtab; },
+                    [](DeviceSolver& d, bool on) { d.lean_sgtab = on; d.upload(); })
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },
                     [](DeviceSolver& d, bool on) { d.set_lean_plain(on); })

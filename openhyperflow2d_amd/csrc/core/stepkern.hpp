@@ -216,8 +216,9 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
   // RES is a template flag (not a nullable pointer) so the device kernels
   // keep the residual pack in registers.
   if (PLAIN) n1 = n2 = n3 = n4 = 1;
-  const real n_n_1 = 1. / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
-  const real m_m_1 = 1. / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+  // 1 / max(n1 + n2, 1) with n in {0, 1}: exactly 0.5 or 1 (no division)
+  const real n_n_1 = (n1 + n2 > 1) ? 0.5 : 1.0;
+  const real m_m_1 = (n3 + n4 > 1) ? 0.5 : 1.0;
   const int Num_Eq = PLAIN ? NEQ : num_eq_for(TT);
   const bool axi = P.fpa.FT != 0;
 #pragma unroll

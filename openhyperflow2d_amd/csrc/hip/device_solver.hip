@@ -369,6 +369,213 @@ void hf2d_lean_tile_occ(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc, int
   lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
 }
 
+// Software-pipelined lean step: a persistent grid (a few workgroups per CU)
+// walks the CPT=1 tiles tile = b, b + G, b + 2G, ...; while tile k is
+// computed from LDS, the staged fields and own-cell data of tile k+G are
+// already in flight into registers, and are written to LDS after the barrier
+// that ends tile k.  The one-shot tile kernel runs every workgroup's load
+// phase at once and then every compute phase; here HBM streaming overlaps
+// the FP64 work.  Same lean_cell() / TileIO arithmetic: fields bitwise equal
+// to hf2d_lean_tile (residual sums accumulate in a different order).
+constexpr int PIPE_SLOTS = 2;   // LDS slots per thread: (TIh + 2) * (TJ + 2) <= 2 * BLOCK for CPT = 1
+
+template <int NE>
+__device__ __forceinline__ void lean_load_own_all(const LeanSoA& L, long idx, LeanOwn& o) {
+  const long N = L.N;   // unconditional: a prefetch must not wait for CT
+  o.CT = L.CT[idx];
+  o.lb = L.lb[idx];
+#pragma unroll
+  for (int k = 0; k < NE; k++) o.beta[k] = L.beta[k * N + idx];
+  o.CP = L.CP[idx];
+  o.R = L.R[idx];
+  o.kk = L.kk[idx];
+}
+
+template <bool RES, bool OUT, bool SG>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_pipe(StepParams P, LeanSoA L, LeanTile T, int ntiles,
+                                                        DevScalars* sc, int slot, int slot_next, int serial,
+                                                        ResidualPack* partials) {
+  extern __shared__ real lds[];
+  constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
+  constexpr int NS = SG ? 4 : 4 + NCOMP;
+  constexpr int FU = SG ? 4 : 10;
+  apply_dt(P, sc, slot);
+  const unsigned G = gridDim.x;
+  const unsigned b = xcd_remap(blockIdx.x, G);
+  if (b == 0 && threadIdx.x == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
+  }
+  const long N = L.N;
+  const int t = threadIdx.x;
+  real st[PIPE_SLOTS][NF];
+  bool sv[PIPE_SLOTS];
+  LeanOwn own;
+  bool mine = false;
+  int ci = 0, cj = 0, cc = 0;
+  auto issue = [&](int tile) {
+    int i0, j0;
+    mine = lean_tile_cell(P, T, tile, t, &ci, &cj, &cc, &i0, &j0, 0);
+    if (mine) lean_load_own_all<NS>(L, (long)ci * P.ny + cj, own);
+#pragma unroll
+    for (int s = 0; s < PIPE_SLOTS; s++) {
+      const int c = t + s * BLOCK;
+      const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
+      const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
+      const int gi = i0 + ii, gj = j0 + jj;
+      sv[s] = c < T.NC && !(xh && yh) && gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny;
+      if (sv[s]) {
+        const long g = (long)gi * P.ny + gj;
+#pragma unroll
+        for (int f = 0; f < NS; f++) st[s][f] = L.Sin[f * N + g];
+        if (!SG)
+#pragma unroll
+          for (int f = 0; f < NCOMP; f++) st[s][4 + NCOMP + f] = L.Pin_s[f * N + g];
+        st[s][FU] = L.Uin[g];
+        st[s][FU + 1] = L.Vin[g];
+        st[s][FU + 2] = L.Pin[g];
+      }
+    }
+  };
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+#pragma unroll
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  if ((int)b < ntiles) issue((int)b);
+  for (int tile = (int)b; tile < ntiles; tile += (int)G) {
+#pragma unroll
+    for (int s = 0; s < PIPE_SLOTS; s++)
+      if (sv[s])
+#pragma unroll
+        for (int f = 0; f < NF; f++) lds[f * T.NC + t + s * BLOCK] = st[s][f];
+    LeanOwn cur = own;
+    cur.filled = mine && !has_all(cur.CT, CT_SOLID) && has_all(cur.CT, CT_NODE_IS_SET);
+    const bool cm = mine;
+    const int i = ci, j = cj, c = cc;
+    __syncthreads();
+    if (tile + (int)G < ntiles) issue(tile + (int)G);
+    if (cm) {
+      TileIO<SG> io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
+      dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, cur, i, j, r, &neg));
+    }
+    __syncthreads();
+  }
+  if (RES) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+// Register-marching lean step (lean_euler.hpp MarchIO): one wavefront per
+// workgroup owns 64 consecutive rows q = chunk * ny + j and marches through
+// the chunk's C columns.  Each column's staged fields are loaded once per
+// wave (no x halo re-reads, no LDS, no barrier), the column two ahead and the
+// next column's own data are in flight while the current one is computed.
+constexpr int MARCH_BLOCK = WAVE;
+
+template <bool RES, bool OUT, bool SG>
+__global__ __launch_bounds__(MARCH_BLOCK) void hf2d_lean_march(StepParams P, LeanSoA L, MarchGeom G, DevScalars* sc,
+                                                               int slot, int slot_next, int serial,
+                                                               ResidualPack* partials) {
+  using IO = MarchIO<SG>;
+  constexpr int NF = IO::NF;
+  apply_dt(P, sc, slot);
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  if (b == 0 && threadIdx.x == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
+  }
+  const int lane = threadIdx.x;
+  const long ny = P.ny;
+  const long q = (long)b * MARCH_BLOCK + lane;
+  const bool live = q < G.nrows;
+  const int chunk = live ? (int)(q / ny) : 0;
+  const int j = live ? (int)(q - (long)chunk * ny) : 0;
+  const int ia = P.i0 + chunk * G.C;
+  // the wave's edge lanes also carry the row beyond it (lane 0: j-1, lane 63: j+1)
+  const int hj = lane == 0 ? j - 1 : (lane == MARCH_BLOCK - 1 ? j + 1 : -1);
+  const bool hl = live && hj >= 0 && hj < P.ny;
+  real Lc[NF], Cc[NF], Rc[NF], Xc[NF], Hc[NF], Hr[NF], Hx[NF];
+#pragma unroll
+  for (int f = 0; f < NF; f++) Lc[f] = Cc[f] = Rc[f] = Xc[f] = Hc[f] = Hr[f] = Hx[f] = 0.0;
+  if (live && ia - 1 >= 0) march_load<SG>(L, (long)(ia - 1) * ny + j, Lc);
+  if (live) march_load<SG>(L, (long)ia * ny + j, Cc);
+  if (hl) march_load<SG>(L, (long)ia * ny + hj, Hc);
+  if (live && ia + 1 < P.nx) march_load<SG>(L, (long)(ia + 1) * ny + j, Rc);
+  if (hl && ia + 1 < P.nx) march_load<SG>(L, (long)(ia + 1) * ny + hj, Hr);
+  LeanOwn oc, on;
+  if (live && ia < P.i1) lean_load_own<IO::NE>(L, (long)ia * ny + j, oc);
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+#pragma unroll
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  for (int s = 0; s < G.C; s++) {
+    const int i = ia + s;
+    // in flight during this column: column i+2 (right neighbour of the next
+    // one) and the next column's own data
+    if (s + 2 <= G.C && i + 2 < P.nx) {
+      if (live) march_load<SG>(L, (long)(i + 2) * ny + j, Xc);
+      if (hl) march_load<SG>(L, (long)(i + 2) * ny + hj, Hx);
+    }
+    if (live && s + 1 < G.C && i + 1 < P.i1) lean_load_own<IO::NE>(L, (long)(i + 1) * ny + j, on);
+    real Uc[NF], Dc[NF];
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+      const real up = __shfl_down(Cc[f], 1, MARCH_BLOCK);
+      const real dn = __shfl_up(Cc[f], 1, MARCH_BLOCK);
+      Uc[f] = lane == MARCH_BLOCK - 1 ? Hc[f] : up;
+      Dc[f] = lane == 0 ? Hc[f] : dn;
+    }
+    if (live && i < P.i1) {
+      IO io(L, (long)i * ny + j, Cc, Lc, Rc, Uc, Dc);
+      dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, oc, i, j, r, &neg));
+    }
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+      Lc[f] = Cc[f];
+      Cc[f] = Rc[f];
+      Rc[f] = Xc[f];
+      Hc[f] = Hr[f];
+      Hr[f] = Hx[f];
+    }
+    oc = on;
+  }
+  if (RES) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if (lane == 0) partials[b] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  if (neg) atomicOr(&sc->neg_T, 1);
+  if (lane == 0) {
+    double m = dtl;
+    if (serial) m = fmin(m, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, LeanSoA L, SoA g, long c0, long c1) {
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   if (c >= c1) return;
@@ -648,9 +855,11 @@ struct DeviceSolver::Impl {
     double** d_dtr = nullptr;
   } p2p;
 
+  SGTable sgt;   // single-gas Cp table (kernel argument copy)
   LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
     LeanSoA L;
     L.N = h.N;
+    L.sgt = sgt;
     L.Sin = S[sb];
     L.Sout = S[1 - sb];
     L.Pin_s = Spre[pb];
@@ -806,6 +1015,8 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     // any tile shape (lean_tj) covers >= LEAN_TILE_MIN_TJ cells per workgroup
     const long nb_tile = (long)(gi1 - gi0 + 1) * ((h.ny + LEAN_TILE_MIN_TJ - 1) / LEAN_TILE_MIN_TJ);
     m.max_partials = std::max((N + BLOCK - 1) / BLOCK, nb_tile) * (BLOCK / WAVE);
+    // marching kernel: one partial per wave, rows rounded up to whole chunks (C <= 64)
+    m.max_partials = std::max(m.max_partials, (N + 64L * h.ny) / WAVE + 1);
   }
   m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
   m.res_out = m.mem.alloc<ResidualPack>(1);
@@ -900,6 +1111,8 @@ void DeviceSolver::upload() {
   cp(m.iw, h.iw.data(), N * sizeof(int32_t));
   cp(m.jw, h.jw.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
+  m.sgt = sg_table_set(cs.cfg.species);
+  if (!lean_sgtab) m.sgt.n = 0;
   scen_host.cfl = cs.cfg.CFL_Scenario.pack();
   scen_host.beta = cs.cfg.beta_Scenario.pack();
   scen_host.CFL = cs.cfg.CFL;
@@ -1382,7 +1595,7 @@ void DeviceSolver::exchange(int group, int dt_slot) {
 namespace {
 constexpr int GRAPH_STEPS = 6;
 uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fused, bool tile, bool sg, int cpt,
-                         int tj) {
+                         int tj, int march, int pipe) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
   mix((uint64_t)P.fpa.is_mu_t);
@@ -1395,6 +1608,8 @@ uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fu
   mix((uint64_t)sg);
   mix((uint64_t)cpt);
   mix((uint64_t)tj);
+  mix((uint64_t)march);
+  mix((uint64_t)pipe);
   return h;
 }
 }  // namespace
@@ -1433,11 +1648,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
   const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj);
+                                       lean_cpt, lean_tj, lean_march, lean_pipe);
   bool same = true;
   for (const StepParams& p : pending)
     same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj) == sig;
+                                   lean_tj, lean_march, lean_pipe) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -1511,7 +1726,58 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   const bool euler = P.sm != SM_NS;
   hipStream_t st = m.stream;
   unsigned nres = nblk;   // workgroups that wrote residual partials
-  if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
+  long npart = -1;        // residual partials written (-1: nres * waves per block)
+  const bool sg_now = lean_sg && lean_sg_ok;
+  if (euler && lean && lean_ok && lean_march > 0 && lean_state == 1) {
+    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+    const MarchGeom G = march_geom(P.i1 - P.i0, P.ny, lean_march);
+    const unsigned nw = (unsigned)((G.nrows + MARCH_BLOCK - 1) / MARCH_BLOCK);
+    const bool out = step_outputs || want_res;
+#define HF2D_MARCH(R, O, S)                                                                                 \
+  hipLaunchKernelGGL((hf2d_lean_march<R, O, S>), dim3(nw), dim3(MARCH_BLOCK), 0, st, P, L, G, m.sc, slot, slot_next, \
+                     serial, m.partials)
+    if (sg_now) {
+      if (want_res) HF2D_MARCH(true, true, true);
+      else if (out) HF2D_MARCH(false, true, true);
+      else HF2D_MARCH(false, false, true);
+    } else {
+      if (want_res) HF2D_MARCH(true, true, false);
+      else if (out) HF2D_MARCH(false, true, false);
+      else HF2D_MARCH(false, false, false);
+    }
+#undef HF2D_MARCH
+    HIP_CHECK(hipGetLastError());
+    npart = nw;
+    sbuf = 1 - sbuf;
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+  } else if (euler && lean && lean_ok && lean_pipe > 0 && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
+    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 1);
+    const int ntile = T.nbi * T.nbj;
+    const unsigned G = (unsigned)std::max(1, std::min(ntile, cu_count * lean_pipe));
+    const size_t shmem = (size_t)lean_tile_fields(sg_now) * T.NC * sizeof(real);
+    if (T.NC > PIPE_SLOTS * BLOCK) throw std::runtime_error("lean_pipe: tile larger than the staging slots");
+    const bool out = step_outputs || want_res;
+#define HF2D_PIPE(R, O, S)                                                                                   \
+  hipLaunchKernelGGL((hf2d_lean_pipe<R, O, S>), dim3(G), dim3(BLOCK), shmem, st, P, L, T, ntile, m.sc, slot, slot_next, \
+                     serial, m.partials)
+    if (sg_now) {
+      if (want_res) HF2D_PIPE(true, true, true);
+      else if (out) HF2D_PIPE(false, true, true);
+      else HF2D_PIPE(false, false, true);
+    } else {
+      if (want_res) HF2D_PIPE(true, true, false);
+      else if (out) HF2D_PIPE(false, true, false);
+      else HF2D_PIPE(false, false, false);
+    }
+#undef HF2D_PIPE
+    HIP_CHECK(hipGetLastError());
+    nres = G;
+    sbuf = 1 - sbuf;
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+  } else if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
     // two cells per thread unless that leaves fewer than ~2 workgroups per CU
     // (small strips of a multi-GPU run)
@@ -1642,8 +1908,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   StepResult r;
   r.async = true;
   if (want_res) {
-    hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials, (long)nres * (BLOCK / WAVE),
-                       m.res_out);
+    hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials,
+                       npart >= 0 ? npart : (long)nres * (BLOCK / WAVE), m.res_out);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(m.res_host, m.res_out, sizeof(ResidualPack), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));

@@ -33,6 +33,12 @@ def main():
             s.solver.use_graph = False
         elif v0 == "nosg":
             s.solver.lean_sg = False
+        elif v0 == "nosgtab":
+            s.solver.lean_sgtab = False
+        elif v0.startswith("pipe"):
+            s.solver.lean_pipe = int(v0[4:])
+        elif v0.startswith("march"):
+            s.solver.lean_march = int(v0[5:])
         elif v0.startswith("cpt"):
             s.solver.lean_cpt = int(v0[3:])
         elif v0.startswith("occ"):
@@ -59,7 +65,7 @@ def main():
     cells = a.nx * a.ny
     for v, ts in res.items():
         best = min(ts)
-        print("%-8s us/step best %.2f  all %s  -> %.0f Mcells*it/s" % (v, best, " ".join("%.2f" % t for t in ts),
+        print("%-10s us/step best %.2f  all %s  -> %.0f Mcells*it/s" % (v, best, " ".join("%.2f" % t for t in ts),
                                                                       cells / best))
 
 
