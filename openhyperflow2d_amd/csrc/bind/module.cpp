@@ -80,6 +80,8 @@ py::array_t<double> field_scalar(const Field& J, const std::string& name) {
       else if (name == "R") v = c.R;
       else if (name == "CP") v = c.CP;
       else if (name == "l_min") v = c.l_min;
+      else if (name == "i_wall") v = c.i_wall;
+      else if (name == "j_wall") v = c.j_wall;
       else if (name == "y_plus") v = c.y_plus;
       else if (name == "mach") {
         const double A = std::sqrt(c.k * c.R * c.Tg + 1e-30);
@@ -193,6 +195,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_property_readonly("project", [](const Case& c) { return c.cfg.project; })
       .def_property_readonly("global_time", [](const Case& c) { return c.global_time; })
       .def_property_readonly("wall_nodes", [](const Case& c) { return c.wall_nodes; })
+      .def("set_min_distance_to_wall", &Case::set_min_distance_to_wall, py::arg("x0") = 0.0)
+      .def("set_min_distance_to_wall_bruteforce", &Case::set_min_distance_to_wall_bruteforce, py::arg("x0") = 0.0)
       .def("set_semantics", [](Case& c, const std::string& s) {
         c.cfg.semantics = (s == "serial") ? Semantics::SERIAL : Semantics::MPI;
       })

@@ -114,6 +114,8 @@ class Case {
   void set_wall_nodes();
   void collect_wall_nodes();
   void set_min_distance_to_wall(real x0 = 0.0);
+  // the reference's O(cells x walls) scan (oracle for the bucketed search)
+  void set_min_distance_to_wall_bruteforce(real x0 = 0.0);
   void recalc_y_plus();
   void set_init_boundary_layer(real delta);
   int set_non_reflected_bc();

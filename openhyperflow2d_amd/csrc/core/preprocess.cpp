@@ -20,6 +20,9 @@
 #include <sstream>
 
 #include "case.hpp"
+#include <thread>
+#include <atomic>
+#include <limits>
 #include "checkpoint.hpp"
 
 namespace hf2d {
@@ -1035,10 +1038,19 @@ void Case::collect_wall_nodes() {
     }
 }
 
-// SetMinDistanceToWall2D: brute-force nearest wall node (the reference's
-// running-min/tie rules are kept: the last equal minimum wins and the
-// min(dx,dy) clamp is applied inside the loop).
-void Case::set_min_distance_to_wall(real x0) {
+// SetMinDistanceToWall2D (deeps2d_core.cpp:4783-4832) scans every wall node
+// per cell: l = sqrt(dx^2 + dy^2); m = min(m, l); if m == l take that wall;
+// m = max(min(dx,dy), m), starting from m = L0 = max(X extent, Y extent).
+// Order-dependent as written, but its outcome has a closed form: with
+// l* = min_k l_k and theta = max(min_l, min(L0, l*)), the final l_min is
+// theta and the wall taken is the LAST k (list order) with l_k <= theta
+// (none if l* > L0).  [l* >= min_l: only walls at exactly l* can pass after
+// the last one; l* < min_l: m sits at min_l once reached and every wall with
+// l <= min_l retakes it.]  So the scan becomes a nearest-wall query plus a
+// "last index within theta" query over a uniform bucket grid -- exact (same
+// expressions, sqrt is monotone), O(cells * nearby walls), threaded over
+// columns.  set_min_distance_to_wall_bruteforce() is the literal scan.
+void Case::set_min_distance_to_wall_bruteforce(real x0) {
   const real min_l = std::min(cfg.dx, cfg.dy);
   for (int i = 0; i < J.nx; i++)
     for (int j = 0; j < J.ny; j++) {
@@ -1061,6 +1073,81 @@ void Case::set_min_distance_to_wall(real x0) {
         n.l_min = std::max(min_l, n.l_min);
       }
     }
+}
+
+void Case::set_min_distance_to_wall(real x0) {
+  if (x0 != 0.0) {   // strip-local offsets: cells may lie outside the wall bucket grid
+    set_min_distance_to_wall_bruteforce(x0);
+    return;
+  }
+  const real dx = cfg.dx, dy = cfg.dy;
+  const real min_l = std::min(dx, dy);
+  const real L0 = std::max((x0 + dx * J.nx), (dy * J.ny));
+  const int W = (int)wall_nodes.size();
+  // buckets of BS x BS grid nodes over the wall index space
+  const int BS = 16;
+  const int nbx = (J.nx + BS - 1) / BS + 1, nby = (J.ny + BS - 1) / BS + 1;
+  std::vector<std::vector<int>> bucket((size_t)nbx * nby);
+  for (int k = 0; k < W; k++) {
+    const int bx = std::min(std::max(wall_nodes[k].first / BS, 0), nbx - 1);
+    const int by = std::min(std::max(wall_nodes[k].second / BS, 0), nby - 1);
+    bucket[(size_t)bx * nby + by].push_back(k);   // ascending k within a bucket
+  }
+  const real bw = BS * dx, bh = BS * dy;   // bucket extent (m)
+  auto cell = [&](int i, int j) {
+    CellRecord& n = J.at(i, j);
+    if (!n.is(CT_NODE_IS_SET) || n.is(CT_SOLID)) return;
+    if (n.Tg != 0 && n.p == 0.) {
+      n.CT |= CT_SOLID;
+      return;
+    }
+    const real x = x0 + i * dx, y = j * dy;
+    auto dist = [&](int k) {
+      const real wx = wall_nodes[k].first * dx, wy = wall_nodes[k].second * dy;
+      return std::sqrt((x - wx) * (x - wx) + (y - wy) * (y - wy));
+    };
+    const int cbx = std::min(i / BS, nbx - 1), cby = std::min(j / BS, nby - 1);
+    // lower bound of the distance from (x, y) to any node of a bucket in
+    // Chebyshev ring r around the cell's bucket (one ring of slack)
+    auto ring_lb = [&](int r) { return r <= 2 ? 0.0 : (r - 2) * std::min(bw, bh); };
+    // 1. nearest wall (ring by ring until no closer bucket can exist)
+    real best = std::numeric_limits<real>::infinity();
+    const int rmax = std::max(nbx, nby);
+    for (int r = 0; r <= rmax; r++) {
+      if (ring_lb(r) > best) break;
+      for (int bx = cbx - r; bx <= cbx + r; bx++) {
+        if (bx < 0 || bx >= nbx) continue;
+        for (int by = cby - r; by <= cby + r; by++) {
+          if (by < 0 || by >= nby) continue;
+          if (std::max(std::abs(bx - cbx), std::abs(by - cby)) != r) continue;
+          for (int k : bucket[(size_t)bx * nby + by]) best = std::min(best, dist(k));
+        }
+      }
+    }
+    n.l_min = std::max(min_l, std::min(L0, best));
+    if (W == 0 || best > L0) return;   // the scan never takes a wall
+    // 2. the last wall (list order) with l <= theta
+    const real theta = n.l_min;
+    int last = -1;
+    const int rr = (int)std::ceil(theta / std::min(bw, bh)) + 2;
+    for (int bx = std::max(cbx - rr, 0); bx <= std::min(cbx + rr, nbx - 1); bx++)
+      for (int by = std::max(cby - rr, 0); by <= std::min(cby + rr, nby - 1); by++)
+        for (int k : bucket[(size_t)bx * nby + by])
+          if (k > last && dist(k) <= theta) last = k;
+    if (last >= 0) {
+      n.i_wall = wall_nodes[last].first;
+      n.j_wall = wall_nodes[last].second;
+    }
+  };
+  const int nth = std::max(1, std::min((int)std::thread::hardware_concurrency(), 16));
+  std::vector<std::thread> pool;
+  std::atomic<int> next{0};
+  for (int t = 0; t < nth; t++)
+    pool.emplace_back([&] {
+      for (int i; (i = next.fetch_add(1)) < J.nx;)
+        for (int j = 0; j < J.ny; j++) cell(i, j);
+    });
+  for (auto& th : pool) th.join();
 }
 
 // Recalc_y_plus (serial variant): u_tau from the nearest wall node.
