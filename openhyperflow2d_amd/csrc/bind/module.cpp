@@ -380,6 +380,7 @@ PYBIND11_MODULE(_hf2d, m) {
              s.p2p_import(v);
            })
       .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
+      .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
@@ -397,6 +398,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_property("lean_sgtab", [](const DeviceSolver& d) { return d.lean_sgtab; },
                     [](DeviceSolver& d, bool on) { d.lean_sgtab = on; d.upload(); })
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
+      .def_readonly("lean_has_cauchy_x", &DeviceSolver::lean_has_cauchy_x)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },
                     [](DeviceSolver& d, bool on) { d.set_lean_plain(on); })
       .def_readonly("lean_ok", &DeviceSolver::lean_ok)

@@ -297,13 +297,91 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
   }
 }
 
+// Halo pack: nf field columns (each ny contiguous doubles at src[f] + col*ny)
+struct ColList {
+  real* f[48];
+  int nf;
+};
+constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
+constexpr int P2P_THREADS = 512;
+
+__device__ inline double p2p_load(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
+// Multi-GPU exchange fused into the lean tile kernel (xGMI mailboxes, see
+// hf2d_p2p_xchg for the layout and the parity argument).  Step n of a rank:
+//   start  one thread per workgroup waits (bounded) until every peer has
+//          published sequence s-1; the global dt is MIN(local slot, the
+//          peers' dt of s-1); tiles at the strip edges stage their ghost
+//          column straight from the mailbox of parity s-1;
+//   end    cells of the first / last owned column store their new lean
+//          state into the neighbour's mailbox of parity s; the last
+//          workgroup to finish (completion counter) sends this rank's local
+//          dt MIN to every peer and releases flag s at system scope.
+// No exchange kernel, no pack/unpack pass, no host involvement: one kernel
+// per step.  Ghost columns of the state arrays are only refreshed by
+// hf2d_p2p_complete, which the host runs before any other consumer.
+struct FusedX {
+  real* peer_recv_l;   // left neighbour's mailbox recv base (we are its right side)
+  real* peer_recv_r;
+  const real* my_recv;
+  unsigned long long* const* peer_flags;
+  double* const* peer_dtr;
+  const unsigned long long* my_flags;
+  const double* my_dtr;
+  unsigned long long* seq;   // last published sequence number
+  unsigned* done;            // workgroups finished in this step
+  long cap;
+  int rank, nranks, sides, on;
+};
+
+__device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, DevScalars* sc) {
+  if (__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) return false;
+  for (int q = 0; q < x.nranks; q++) {
+    if (q == x.rank) continue;
+    long spins = 0;
+    while (__hip_atomic_load(&x.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > P2P_SPIN_LIMIT) {
+        atomicOr(&sc->neg_T, 2);
+        return false;
+      }
+    }
+  }
+  return true;
+}
+
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
-template <bool RES, bool OUT, bool SG, int CPT>
+template <bool RES, bool OUT, bool SG, int CPT, bool FX = false>
 __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, const LeanTile& T, DevScalars* sc,
-                                               int slot, int slot_next, int serial, ResidualPack* partials) {
+                                               int slot, int slot_next, int serial, ResidualPack* partials,
+                                               const FusedX& X = FusedX{}) {
   extern __shared__ real lds[];
-  apply_dt(P, sc, slot);
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  unsigned long long seq_prev = 0;
+  if (FX) {
+    __shared__ double s_dt;
+    seq_prev = *X.seq;
+    if (threadIdx.x == 0) {
+      double d = bits_to_d(sc->dt_bits[slot]);
+      if (seq_prev > 0 && p2p_wait_all(X, seq_prev, sc)) {
+        const int pp = (int)(seq_prev & 1);
+        for (int q = 0; q < X.nranks; q++)
+          if (q != X.rank) d = fmin(d, p2p_load(X.my_dtr + pp * X.nranks + q));
+      }
+      s_dt = d;
+      if (b == 0) sc->dt_bits[slot] = d_to_bits(d);   // global MIN (idempotent for racing readers)
+    }
+    __syncthreads();
+    apply_dt(P, sc, slot);
+    P.dt = s_dt;
+    P.dtdx = s_dt / P.dx;
+    P.dtdy = s_dt / P.dy;
+  } else {
+    apply_dt(P, sc, slot);
+  }
   if (b == 0 && threadIdx.x == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
@@ -318,7 +396,40 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     mine[q] = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i[q], &j[q], &c[q], &i0, &j0, q);
     if (mine[q]) lean_load_own<TileIO<SG>::NE>(L, (long)i[q] * P.ny + j[q], own[q]);
   }
-  lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
+  if (!FX || seq_prev == 0 || (i0 - 1 > P.i0 - 1 && i0 + T.TI < P.i1)) {
+    lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
+  } else {
+    // edge tile: the ghost column comes from the mailbox of parity seq_prev
+    constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
+    const int pp = (int)(seq_prev & 1);
+    const real* mbL = X.my_recv + ((long)pp * 2) * X.cap;
+    const real* mbR = X.my_recv + ((long)pp * 2 + 1) * X.cap;
+    const long N = L.N;
+    constexpr int NS = SG ? 4 : 4 + NCOMP;
+    constexpr int FU = SG ? 4 : 10;
+    for (int c = threadIdx.x; c < T.NC; c += BLOCK) {
+      const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
+      const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
+      const int gi = i0 + ii, gj = j0 + jj;
+      if ((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
+      const bool gl = (X.sides & 1) && gi == P.i0 - 1, gr = (X.sides & 2) && gi == P.i1;
+      if (gl || gr) {
+        const real* mb = gl ? mbL : mbR;
+#pragma unroll
+        for (int f = 0; f < NF; f++) lds[f * T.NC + c] = p2p_load(mb + (long)f * P.ny + gj);
+        continue;
+      }
+      const long g = (long)gi * P.ny + gj;
+#pragma unroll
+      for (int f = 0; f < NS; f++) lds[f * T.NC + c] = L.Sin[f * N + g];
+      if (!SG)
+#pragma unroll
+        for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * T.NC + c] = L.Pin_s[f * N + g];
+      lds[FU * T.NC + c] = L.Uin[g];
+      lds[(FU + 1) * T.NC + c] = L.Vin[g];
+      lds[(FU + 2) * T.NC + c] = L.Pin[g];
+    }
+  }
   __syncthreads();
   ResidualPack r;
   if (RES) {
@@ -333,6 +444,28 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     if (mine[q]) {
       TileIO<SG> io(L, (long)i[q] * P.ny + j[q], lds, T.NC, T.W, c[q]);
       dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, own[q], i[q], j[q], r, &neg));
+      if (FX) {
+        const bool pl = (X.sides & 1) && i[q] == P.i0, pr = (X.sides & 2) && i[q] == P.i1 - 1;
+        if (pl || pr) {   // new lean state of an edge cell -> the neighbour's mailbox of parity seq_prev + 1
+          constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
+          constexpr int NS = SG ? 4 : 4 + NCOMP;
+          const int pn = (int)((seq_prev + 1) & 1);
+          real* mb = pl ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap;
+          const long N = L.N, g = (long)i[q] * P.ny + j[q];
+          real v[NF];
+#pragma unroll
+          for (int f = 0; f < NS; f++) v[f] = L.Sout[f * N + g];
+          if (!SG)
+#pragma unroll
+            for (int f = 0; f < NCOMP; f++) v[4 + NCOMP + f] = L.Pout_s[f * N + g];
+          v[NF - 3] = L.Uout[g];
+          v[NF - 2] = L.Vout[g];
+          v[NF - 1] = L.Pout[g];
+#pragma unroll
+          for (int f = 0; f < NF; f++) mb[(long)f * P.ny + j[q]] = v[f];
+          __threadfence_system();
+        }
+      }
     }
   }
   if (RES) {
@@ -350,6 +483,23 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    if (FX) {
+      const unsigned prev = __hip_atomic_fetch_add(X.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {   // last workgroup: publish this rank's step
+        *X.done = 0;
+        const unsigned long long sn = seq_prev + 1;
+        const int pn = (int)(sn & 1);
+        const double dl = bits_to_d(__hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_ACQUIRE,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+        for (int q = 0; q < X.nranks; q++)
+          if (q != X.rank) X.peer_dtr[q][pn * X.nranks + X.rank] = dl;
+        __threadfence_system();
+        for (int q = 0; q < X.nranks; q++)
+          if (q != X.rank)
+            __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        *X.seq = sn;
+      }
+    }
   }
 }
 
@@ -360,6 +510,48 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
                                                          int slot, int slot_next, int serial,
                                                          ResidualPack* partials) {
   lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
+}
+
+// Same step with the multi-GPU exchange fused in (FusedX).
+template <bool RES, bool OUT, bool SG, int CPT>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_tile_fx(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                            int slot, int slot_next, int serial,
+                                                            ResidualPack* partials, FusedX X) {
+  lean_tile_body<RES, OUT, SG, CPT, true>(P, L, T, sc, slot, slot_next, serial, partials, X);
+}
+
+// Ghost columns + global dt after fused steps, for any other consumer: wait
+// for the peers' last publication, copy the mailbox of that parity into the
+// ghost columns of the current state, fold the dt MIN into the slot.
+__global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_complete(ColList Lc, int ghostL, int ghostR, int ny, int cnt,
+                                                                 FusedX X, DevScalars* sc, int dslot) {
+  const unsigned long long sq = *X.seq;
+  if (sq == 0) return;
+  __shared__ int ok;
+  if (threadIdx.x == 0) ok = p2p_wait_all(X, sq, sc) ? 1 : 0;
+  __syncthreads();
+  if (!ok) return;
+  const int pp = (int)(sq & 1);
+  if (X.sides & 1) {
+    const real* src = X.my_recv + ((long)pp * 2) * X.cap;
+    for (int t = threadIdx.x; t < cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      Lc.f[f][(long)ghostL * ny + j] = p2p_load(src + t);
+    }
+  }
+  if (X.sides & 2) {
+    const real* src = X.my_recv + ((long)pp * 2 + 1) * X.cap;
+    for (int t = threadIdx.x; t < cnt; t += P2P_THREADS) {
+      const int f = t / ny, j = t - f * ny;
+      Lc.f[f][(long)ghostR * ny + j] = p2p_load(src + t);
+    }
+  }
+  if (threadIdx.x == 0) {
+    double m = bits_to_d(sc->dt_bits[dslot]);
+    for (int q = 0; q < X.nranks; q++)
+      if (q != X.rank) m = fmin(m, p2p_load(X.my_dtr + pp * X.nranks + q));
+    sc->dt_bits[dslot] = d_to_bits(m);
+  }
 }
 
 template <bool RES, bool OUT, bool SG, int OCC, int CPT = 1>
@@ -606,11 +798,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_yplus(StepParams P, SoA s, long c0
   y_plus_cell(P, s, i, j, gx0);
 }
 
-// Halo pack: nf field columns (each ny contiguous doubles at src[f] + col*ny)
-struct ColList {
-  real* f[48];
-  int nf;
-};
+
 __global__ void hf2d_pack(ColList L, int col, int ny, real* buf) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= L.nf * ny) return;
@@ -671,8 +859,7 @@ __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* 
 // s+1, which is published after the unpack of s.  The sequence counter lives
 // in device memory, so the kernel replays unchanged inside step graphs.
 // ---------------------------------------------------------------------------
-constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
-constexpr int P2P_THREADS = 512;
+
 
 struct P2PArgs {
   ColList L;
@@ -690,10 +877,7 @@ struct P2PArgs {
   int dslot, fold_dt, rank, nranks;
 };
 
-__device__ inline double p2p_load(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_SYSTEM));
-}
+
 
 __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
   const unsigned long long seq = *a.seq + 1;
@@ -849,6 +1033,7 @@ struct DeviceSolver::Impl {
     char* base = nullptr;                 // fine-grained mailbox (p2p_layout)
     size_t bytes = 0, off_dtr = 0, off_recv = 0;
     unsigned long long* seq = nullptr;    // device-side exchange counter
+    unsigned* done = nullptr;             // fused tile kernel: finished workgroups
     std::vector<char*> peer_base;         // mailbox of every rank (self: base)
     std::vector<void*> opened;            // IPC mappings to close
     unsigned long long** d_flags = nullptr;
@@ -1157,6 +1342,7 @@ void DeviceSolver::set_lean_plain(bool on) {
 }
 
 void DeviceSolver::lean_materialize() {
+  p2p_complete();
   Impl& m = *impl;
   StepParams P = make_params(last_iter + iter);
   P.nx = h.nx;
@@ -1171,6 +1357,7 @@ void DeviceSolver::lean_materialize() {
 
 void DeviceSolver::download(Field& J) {
   flush_pending();
+  p2p_complete();
   HIP_CHECK(hipSetDevice(dev));
   Impl& m = *impl;
   if (lean_state) lean_materialize();
@@ -1226,6 +1413,7 @@ void DeviceSolver::trace_pop() { roctxRangePop(); }
 
 void DeviceSolver::sync_scalars() {
   flush_pending();
+  p2p_complete();
   Impl& m = *impl;
   HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
   HIP_CHECK(hipStreamSynchronize(m.stream));
@@ -1250,6 +1438,7 @@ void DeviceSolver::sync_scalars() {
 // Called at each outer-cycle boundary by the driver (time_part restarts).
 void DeviceSolver::cycle_update() {
   flush_pending();
+  p2p_complete();
   Impl& m = *impl;
   if (cs.cfg.ProblemType == SM_NS && cs.cfg.semantics != Semantics::SERIAL) {
     StepParams P = make_params(last_iter);
@@ -1388,6 +1577,7 @@ std::string DeviceSolver::p2p_export(int rank, int nranks) {
   p.base = (char*)b;
   HIP_CHECK(hipMemset(p.base, 0, p.bytes));
   p.seq = m.mem.alloc<unsigned long long>(1);
+  p.done = m.mem.alloc<unsigned>(1);
   HIP_CHECK(hipDeviceSynchronize());
   P2PDesc d{};
   d.magic = P2P_MAGIC;
@@ -1467,6 +1657,7 @@ int DeviceSolver::comm_size() const { return impl->nranks; }
 // send/recv group plus an all-reduce.
 void DeviceSolver::exchange(int group, int dt_slot) {
   Impl& m = *impl;
+  p2p_complete();
   if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
   const int ny = h.ny;
   const long N = h.N;
@@ -1583,6 +1774,49 @@ void DeviceSolver::exchange(int group, int dt_slot) {
   HIP_CHECK(hipGetLastError());
 }
 
+FusedX DeviceSolver::fused_args() const {
+  const Impl& m = *impl;
+  const Impl::P2P& p = m.p2p;
+  const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
+  FusedX X{};
+  X.peer_recv_l = has_left ? (real*)(p.peer_base[m.rank - 1] + p.off_recv) : nullptr;
+  X.peer_recv_r = has_right ? (real*)(p.peer_base[m.rank + 1] + p.off_recv) : nullptr;
+  X.my_recv = (const real*)(p.base + p.off_recv);
+  X.peer_flags = p.d_flags;
+  X.peer_dtr = p.d_dtr;
+  X.my_flags = (const unsigned long long*)p.base;
+  X.my_dtr = (const double*)(p.base + p.off_dtr);
+  X.seq = p.seq;
+  X.done = p.done;
+  X.cap = m.halo_cap;
+  X.rank = m.rank;
+  X.nranks = m.nranks;
+  X.sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
+  X.on = 1;
+  return X;
+}
+
+// After fused-exchange steps the newest ghost columns and the peers' dt live
+// only in the mailbox: materialise them before any other consumer.
+void DeviceSolver::p2p_complete() {
+  if (!fx_pending) return;
+  fx_pending = false;
+  Impl& m = *impl;
+  const long N = h.N;
+  ColList L;
+  L.nf = 0;
+  const bool sg = lean_sg && lean_sg_ok;
+  for (int k = 0; k < (sg ? 4 : 4 + NCOMP); k++) L.f[L.nf++] = m.S[sbuf] + (long)k * N;
+  if (!sg)
+    for (int k = 0; k < NCOMP; k++) L.f[L.nf++] = m.Spre[pbuf] + (long)k * N;
+  L.f[L.nf++] = m.U[pbuf];
+  L.f[L.nf++] = m.V[pbuf];
+  L.f[L.nf++] = m.P2[pbuf];
+  hipLaunchKernelGGL(hf2d_p2p_complete, dim3(1), dim3(P2P_THREADS), 0, m.stream, L, 0, h.nx - 1, h.ny, L.nf * h.ny,
+                     fused_args(), m.sc, (int)(nstep % 3));
+  HIP_CHECK(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------
 // Step graphs.  Plain steps (no residual pass, no host read-back) are queued
 // and executed GRAPH_STEPS at a time as one captured hipGraph: every kernel
@@ -1595,7 +1829,7 @@ void DeviceSolver::exchange(int group, int dt_slot) {
 namespace {
 constexpr int GRAPH_STEPS = 6;
 uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fused, bool tile, bool sg, int cpt,
-                         int tj, int march, int pipe) {
+                         int tj, int march, int pipe, int fuse) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
   mix((uint64_t)P.fpa.is_mu_t);
@@ -1610,6 +1844,7 @@ uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fu
   mix((uint64_t)tj);
   mix((uint64_t)march);
   mix((uint64_t)pipe);
+  mix((uint64_t)fuse);
   return h;
 }
 }  // namespace
@@ -1648,11 +1883,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
   const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj, lean_march, lean_pipe);
+                                       lean_cpt, lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on));
   bool same = true;
   for (const StepParams& p : pending)
     same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj, lean_march, lean_pipe) == sig;
+                                   lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on)) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -1728,6 +1963,10 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   unsigned nres = nblk;   // workgroups that wrote residual partials
   long npart = -1;        // residual partials written (-1: nres * waves per block)
   const bool sg_now = lean_sg && lean_sg_ok;
+  fx_step = false;
+  const bool tile_path = euler && lean && lean_ok && lean_march <= 0 && lean_pipe <= 0 && lean_tile &&
+                         lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ;
+  if (!tile_path) p2p_complete();
   if (euler && lean && lean_ok && lean_march > 0 && lean_state == 1) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
     const MarchGeom G = march_geom(P.i1 - P.i0, P.ny, lean_march);
@@ -1791,9 +2030,18 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     const bool sg = lean_sg && lean_sg_ok;
     const size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
     const bool out = step_outputs || want_res;
-#define HF2D_LEAN_TILE(R, O, G, C)                                                                        \
-  hipLaunchKernelGGL((hf2d_lean_tile<R, O, G, 0, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
-                     slot_next, serial, m.partials)
+    // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
+    fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
+    const FusedX X = fx_step ? fused_args() : FusedX{};
+#define HF2D_LEAN_TILE(R, O, G, C)                                                                                 \
+  do {                                                                                                               \
+    if (fx_step)                                                                                                     \
+      hipLaunchKernelGGL((hf2d_lean_tile_fx<R, O, G, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
+                         slot_next, serial, m.partials, X);                                                          \
+    else                                                                                                             \
+      hipLaunchKernelGGL((hf2d_lean_tile<R, O, G, 0, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
+                         slot_next, serial, m.partials);                                                             \
+  } while (0)
     // all variants of one step must use the cpt the tile geometry was built for
     if (sg && cpt == 2) {
       if (want_res)
@@ -1807,7 +2055,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
         HF2D_LEAN_TILE(true, true, true, 1);
       else if (out)
         HF2D_LEAN_TILE(false, true, true, 1);
-      else if (lean_occ == 6)
+      else if (lean_occ == 6 && !fx_step)
         hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                            m.sc, slot, slot_next, serial, m.partials);
       else
@@ -1895,8 +2143,11 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     pbuf = 1 - pbuf;
   }
   // new-state halo + global dt (MIN over ranks into the next slot)
-  if ((m.comm || m.local || m.p2p.on) && m.nranks > 1)
+  if (fx_step) {
+    fx_pending = true;   // exchanged inside the tile kernel
+  } else if ((m.comm || m.local || m.p2p.on) && m.nranks > 1) {
     exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
+  }
   if (!cs.cfg.isAdiabaticWall) {
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     hipLaunchKernelGGL(hf2d_wall_solid, dim3(nblk), dim3(BLOCK), 0, st, P, s, m.qdir, c0, c1);

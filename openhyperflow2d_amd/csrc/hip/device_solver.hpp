@@ -87,6 +87,10 @@ class DeviceSolver : public SolverBase {
   std::string p2p_export(int rank, int nranks);
   void p2p_import(const std::vector<std::string>& descs);
   bool p2p_active() const;
+  bool p2p_fuse = true;      // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
+  bool fx_step = false, fx_pending = false;
+  void p2p_complete();
+  struct FusedX fused_args() const;
   void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import
   int comm_rank() const;
   int comm_size() const;

@@ -118,6 +118,9 @@ class DistributedSimulation:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 1:
             self.transport = "p2p"
+            # exchange fused into the lean tile kernel (one kernel per step);
+            # HF2D_P2P_FUSE=0 keeps the separate exchange kernel
+            s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "1") != "0"
         else:
             s.p2p_active = False
             if not nccl:

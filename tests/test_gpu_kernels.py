@@ -124,7 +124,7 @@ def test_lean_bitwise_with_switches(gpu):
     np.testing.assert_array_equal(rg, rc)
 
 
-def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False):
+def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
     host thread each, halos through the in-process LocalGroup transport (or,
     p2p=True, the device-side mailbox transport: one exchange kernel per step,
@@ -147,6 +147,7 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False):
         descs = [s.p2p_export(r, nranks) for r, s in enumerate(solvers)]
         for s in solvers:
             s.p2p_import(descs)
+            s.p2p_fuse = fuse
             assert s.p2p_active
     errors = []
 
@@ -156,7 +157,10 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False):
         except Exception as e:   # pragma: no cover - reported below
             errors.append(e)
 
-    for n, res in schedule:
+    for k, (n, res) in enumerate(schedule):
+        if toggle:   # alternate fused / separate-kernel exchange between chunks
+            for s in solvers:
+                s.p2p_fuse = (k % 2 == 0)
         th = [threading.Thread(target=run, args=(s, n, res), daemon=True) for s in solvers]
         for t in th:
             t.start()
@@ -197,15 +201,20 @@ def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
 # <= 3 in-process ranks: their streams must land on distinct hardware queues
 # (GPU_MAX_HW_QUEUES=4) or a spinning exchange could sit in front of the step
 # it waits for; separate processes (the real deployment) have no such limit.
-@pytest.mark.parametrize("nranks,physics,lean", [(2, "euler", True), (3, "euler", True), (3, "kes", False)])
-def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
+@pytest.mark.parametrize("nranks,physics,lean,fuse", [(2, "euler", True, False), (3, "euler", True, False),
+                                                      (3, "kes", False, True), (2, "euler", True, True),
+                                                      (3, "euler", True, True), (3, "euler", True, "toggle")])
+def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse):
     """xGMI mailbox transport (hf2d_p2p_xchg: direct peer stores, system-scope
-    flags, device-side dt MIN) inside captured step graphs == one GPU, bit for
-    bit (in-process ranks share the device; the protocol is the multi-GPU one)."""
+    flags, device-side dt MIN; fuse: the same exchange folded into the lean
+    tile kernel, hf2d_lean_tile_fx + hf2d_p2p_complete) inside captured step
+    graphs == one GPU, bit for bit (in-process ranks share the device; the
+    protocol is the multi-GPU one)."""
     ns = physics != "euler"
     text = decks.wedge15(240, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
     schedule = [(5, True), (30, False), (7, True), (25, False)]
-    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean, p2p=True)
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean, p2p=True, fuse=fuse is True,
+                               toggle=fuse == "toggle")
     ref = gpu.Simulation(text, "gpu", lean=lean)
     for n, res in schedule:
         ref.step(n, residual=res)

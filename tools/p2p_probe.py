@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--ny", type=int, default=200)
     ap.add_argument("--steps", type=int, default=600)
     ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--nofuse", action="store_true", help="separate exchange kernel instead of the fused tile kernel")
     a = ap.parse_args()
     import openhyperflow2d_amd as hf
     from openhyperflow2d_amd.models import decks
@@ -43,6 +44,7 @@ def main():
     descs = [s.p2p_export(r, a.ranks) for r, s in enumerate(solvers)]
     for s in solvers:
         s.p2p_import(descs)
+        s.p2p_fuse = not a.nofuse
 
     def run_all(n):
         th = [threading.Thread(target=s.run_steps, args=(n, False)) for s in solvers]
