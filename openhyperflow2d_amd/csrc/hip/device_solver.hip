@@ -343,8 +343,10 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
     if (q == x.rank) continue;
     long spins = 0;
     while (__hip_atomic_load(&x.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > P2P_SPIN_LIMIT) {
+      // every workgroup of the step polls: back off harder than the
+      // single-workgroup exchange kernel so the pollers do not flood HBM
+      __builtin_amdgcn_s_sleep(16);
+      if (++spins > P2P_SPIN_LIMIT / 8) {
         atomicOr(&sc->neg_T, 2);
         return false;
       }

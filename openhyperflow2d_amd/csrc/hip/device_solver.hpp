@@ -87,7 +87,7 @@ class DeviceSolver : public SolverBase {
   std::string p2p_export(int rank, int nranks);
   void p2p_import(const std::vector<std::string>& descs);
   bool p2p_active() const;
-  bool p2p_fuse = true;      // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
+  bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
   bool fx_step = false, fx_pending = false;
   void p2p_complete();
   struct FusedX fused_args() const;

@@ -118,9 +118,11 @@ class DistributedSimulation:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 1:
             self.transport = "p2p"
-            # exchange fused into the lean tile kernel (one kernel per step);
-            # HF2D_P2P_FUSE=0 keeps the separate exchange kernel
-            s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "1") != "0"
+            # HF2D_P2P_FUSE=1 folds the exchange into the lean tile kernel; off
+            # by default: on the one-GPU proxy (tools/p2p_probe.py --tail) the
+            # fused step cost more than tile kernel + exchange kernel
+            # (profiles/p2p_fused_virtual2_kernels.md)
+            s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "0") == "1"
         else:
             s.p2p_active = False
             if not nccl:

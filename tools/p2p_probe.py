@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--steps", type=int, default=600)
     ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--nofuse", action="store_true", help="separate exchange kernel instead of the fused tile kernel")
+    ap.add_argument("--tail", type=int, default=0,
+                    help="2 ranks, the last one owning only this many columns: its kernel barely competes for "
+                         "the shared GPU, so us/step ~ rank 0's kernel + its exchange overhead")
     a = ap.parse_args()
     import openhyperflow2d_amd as hf
     from openhyperflow2d_amd.models import decks
@@ -35,6 +38,8 @@ def main():
     text = decks.wedge15(a.nx, a.ny, nmax=10 ** 9, nout=10 ** 8)
     cases = [nat.Case.from_deck(text, ".", False) for _ in range(a.ranks)]
     parts = balanced_columns(np.asarray(cases[0].field("solid")), a.ranks)
+    if a.tail:
+        parts = [(0, a.nx - a.tail), (a.nx - a.tail, a.nx)]
     group = nat.LocalGroup(a.ranks)
     solvers = []
     for r, (lo, hi) in enumerate(parts):
