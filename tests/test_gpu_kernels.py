@@ -236,7 +236,7 @@ def _p2p_proc_worker(rank, world, port, text, schedule, out):
 
     sim = DistributedSimulation(text, "gpu", rank=rank, world=world, device=0, transport="p2p")
     assert sim.transport == "p2p", sim.transport
-    sim.solver.p2p_fuse = rank == 0 or True   # fused exchange across processes (IPC-mapped mailboxes)
+    sim.solver.p2p_fuse = True   # fused exchange across processes (IPC-mapped mailboxes)
     for n, res in schedule:
         sim.step(n, residual=res)
     fields = {f: sim.gather_field(f) for f in FIELDS}
