@@ -267,6 +267,9 @@ PYBIND11_MODULE(_hf2d, m) {
         if (!py_.empty()) save_y_heat_flux(py_, c, c.J);
       });
 
+  m.def("cond_names", &cond_names, py::arg("CT"), "PrintCond: names of the set CondType2D bits");
+  m.def("turb_cond_names", &turb_cond_names, py::arg("TT"), "PrintTurbCond: names of the set TurbulenceCondType2D bits");
+
   py::class_<SolverBase>(m, "SolverBase")
       .def("run_steps", &SolverBase::run_steps, py::arg("n"), py::arg("want_residual_last") = false,
            py::call_guard<py::gil_scoped_release>())

@@ -358,4 +358,50 @@ void save_y_heat_flux(const std::string& path, const Case& cs, const Field& J) {
   for (int j = 0; j < J.ny; j++) o << j * C.dy << " " << Q[j] << "\n";
 }
 
+namespace {
+struct FlagName {
+  u64 bit;
+  const char* name;
+};
+const FlagName CT_NAMES[] = {
+    {CT_Rho_CONST, "CT_Rho_CONST_2D"}, {CT_U_CONST, "CT_U_CONST_2D"}, {CT_V_CONST, "CT_V_CONST_2D"},
+    {CT_T_CONST, "CT_T_CONST_2D"}, {CT_Y_CONST, "CT_Y_CONST_2D"}, {CT_dRhodx_NULL, "CT_dRhodx_NULL_2D"},
+    {CT_dUdx_NULL, "CT_dUdx_NULL_2D"}, {CT_dVdx_NULL, "CT_dVdx_NULL_2D"}, {CT_dTdx_NULL, "CT_dTdx_NULL_2D"},
+    {CT_dYdx_NULL, "CT_dYdx_NULL_2D"}, {CT_dRhody_NULL, "CT_dRhody_NULL_2D"}, {CT_dUdy_NULL, "CT_dUdy_NULL_2D"},
+    {CT_dVdy_NULL, "CT_dVdy_NULL_2D"}, {CT_dTdy_NULL, "CT_dTdy_NULL_2D"}, {CT_dYdy_NULL, "CT_dYdy_NULL_2D"},
+    {CT_d2Rhodx2_NULL, "CT_d2Rhodx2_NULL_2D"}, {CT_d2Udx2_NULL, "CT_d2Udx2_NULL_2D"},
+    {CT_d2Vdx2_NULL, "CT_d2Vdx2_NULL_2D"}, {CT_d2Tdx2_NULL, "CT_d2Tdx2_NULL_2D"},
+    {CT_d2Ydx2_NULL, "CT_d2Ydx2_NULL_2D"}, {CT_d2Rhody2_NULL, "CT_d2Rhody2_NULL_2D"},
+    {CT_d2Udy2_NULL, "CT_d2Udy2_NULL_2D"}, {CT_d2Vdy2_NULL, "CT_d2Vdy2_NULL_2D"},
+    {CT_d2Tdy2_NULL, "CT_d2Tdy2_NULL_2D"}, {CT_d2Ydy2_NULL, "CT_d2Ydy2_NULL_2D"},
+    {CT_NONREFLECTED, "CT_NONREFLECTED_2D"}, {CT_WALL_NO_SLIP, "CT_WALL_NO_SLIP_2D"},
+    {CT_WALL_LAW, "CT_WALL_LAW_2D"}, {CT_GAS, "CT_GAS_2D"}, {CT_BL_REFINEMENT, "CT_BL_REFINEMENT_2D"},
+    {CT_SOLID, "CT_SOLID_2D"}, {CT_NODE_IS_SET, "CT_NODE_IS_SET_2D"}, {CT_LIQUID, "CT_LIQUID_2D"},
+    {CT_TIME_DEPEND, "CT_TIME_DEPEND_2D"},
+};
+const FlagName TCT_NAMES[] = {
+    {TCT_k_CONST, "TCT_k_CONST_2D"}, {TCT_eps_CONST, "TCT_eps_CONST_2D"}, {TCT_dkdx_NULL, "TCT_dkdx_NULL_2D"},
+    {TCT_depsdx_NULL, "TCT_depsdx_NULL_2D"}, {TCT_dkdy_NULL, "TCT_dkdy_NULL_2D"},
+    {TCT_depsdy_NULL, "TCT_depsdy_NULL_2D"}, {TCT_d2kdx2_NULL, "TCT_d2kdx2_NULL_2D"},
+    {TCT_d2epsdx2_NULL, "TCT_d2epsdx2_NULL_2D"}, {TCT_d2kdy2_NULL, "TCT_d2kdy2_NULL_2D"},
+    {TCT_d2epsdy2_NULL, "TCT_d2epsdy2_NULL_2D"}, {TCT_k_eps_Model, "TCT_k_eps_Model_2D"},
+    {TCT_Prandtl_Model, "TCT_Prandtl_Model_2D"}, {TCT_Integral_Model, "TCT_Integral_Model_2D"},
+    {TCT_eps_mud2kdx2_WALL, "TCT_eps_mud2kdx2_WALL_2D"}, {TCT_eps_mud2kdy2_WALL, "TCT_eps_mud2kdy2_WALL_2D"},
+    {TCT_eps_Cmk2kXn_WALL, "TCT_eps_Cmk2kXn_WALL_2D"}, {TCT_Spalart_Allmaras_Model, "TCT_Spalart_Allmaras_Model_2D"},
+    {TCT_k_omega_Model, "TCT_k_omega_Model_2D"}, {TCT_k_omega_SST_Model, "TCT_k_omega_SST_Model_2D"},
+    {TCT_Baldwin_Lomax_Model, "TCT_Baldwin_Lomax_Model_2D"}, {TCT_nut_92_Model, "TCT_nut_92_Model_2D"},
+    {TCT_Smagorinsky_Model, "TCT_Smagorinsky_Model_2D"},
+};
+template <size_t M>
+std::string names(u64 v, const FlagName (&tab)[M], const char* none) {
+  std::string s;
+  for (const FlagName& f : tab)
+    if ((v & f.bit) == f.bit) s += (s.empty() ? "" : " | ") + std::string(f.name);
+  return s.empty() ? none : s;
+}
+}  // namespace
+
+std::string cond_names(u64 CT) { return names(CT, CT_NAMES, "CT_NO_COND_2D"); }
+std::string turb_cond_names(u64 TT) { return names(TT, TCT_NAMES, "TCT_No_Turbulence_2D"); }
+
 }  // namespace hf2d

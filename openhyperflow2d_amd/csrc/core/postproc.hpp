@@ -39,4 +39,9 @@ real calc_cv(const Case& cs, const Field& J, real x0, real y0, real dy, real p_a
 real average_pressure(const Case& cs, const Field& J, real x0, real l, real d);
 real average_temperature(const Case& cs, const Field& J, real x0, real l, real d, int mid_enthalpy);
 
+// PrintCond / PrintTurbCond (deeps2d_core.cpp:2390-2491): names of the set
+// CondType2D / TurbulenceCondType2D bits, e.g. "CT_U_CONST_2D | CT_NODE_IS_SET_2D".
+std::string cond_names(u64 CT);
+std::string turb_cond_names(u64 TT);
+
 }  // namespace hf2d

@@ -402,7 +402,20 @@ void SolverBase::failure_snapshot(const RunOptions& opt, const std::string& dir,
                            "-err.plt";
   if (opt.write_outputs) save_field_plt(dir + "/" + name, cs, cs.J, cs.global_time + cur_time_part, true);
   if (log && (r == 0 || nr > 1)) {
-    *log << "\n" << why << "\nError snapshot: " << dir << "/" << name;
+    *log << "\n" << why;
+    // the first owned active cell with Tg < 0 (deeps2d_core.cpp:1246-1316 report + PrintCond)
+    const auto own = owned_columns();
+    bool found = false;
+    for (int i = own.first; i < own.second && !found; i++)
+      for (int j = 0; j < cs.J.ny && !found; j++) {
+        const CellRecord& c = cs.J.at(i, j);
+        if (has_all(c.CT, CT_NODE_IS_SET) && !has_all(c.CT, CT_SOLID) && !(c.Tg >= 0)) {
+          *log << "\nTg=" << c.Tg << " in cell (" << i << ", " << j << ") of rank " << r << "\n  CT: "
+               << cond_names(c.CT) << "\n  TurbType: " << turb_cond_names(c.TurbType);
+          found = true;
+        }
+      }
+    *log << "\nError snapshot: " << dir << "/" << name;
     if (opt.write_checkpoint)
       *log << "; last good checkpoint (iteration " << last_iter << "): " << dir << "/" << C.swap_file;
     *log << "\n" << std::flush;

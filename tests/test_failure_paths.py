@@ -54,6 +54,7 @@ def test_nan_fault_writes_error_snapshot_and_keeps_checkpoint(hf, tmp_path, back
                 profile=str(tmp_path / "prof.json"))
     msg = str(ei.value)
     assert "unstability" in msg and "Error snapshot" in msg and "last good checkpoint (iteration 20)" in msg
+    assert "CT_NODE_IS_SET_2D" in msg and "in cell (" in msg     # PrintCond of the failing cell
     err = tmp_path / (STEM + "-err.plt")
     assert err.exists() and err.stat().st_size > 0
     meta = json.loads((tmp_path / (STEM + ".hf2d.meta")).read_text())
@@ -93,3 +94,9 @@ def test_cli_nan_fault_exit_code(hf, tmp_path):
     assert r.returncode == 3, r.stdout[-2000:] + r.stderr[-2000:]
     assert "unstability" in r.stderr
     assert (tmp_path / (STEM + "-err.plt")).exists()
+
+
+def test_cond_names(native):
+    assert native.cond_names(0) == "CT_NO_COND_2D"
+    assert native.cond_names(0x02 | 0x080000000) == "CT_U_CONST_2D | CT_NODE_IS_SET_2D"
+    assert "TCT_k_eps_Model_2D" in native.turb_cond_names(0x0400)
