@@ -76,6 +76,11 @@ py::array_t<double> field_scalar(const Field& J, const std::string& name) {
       else if (name == "p") v = c.p;
       else if (name == "T") v = c.Tg;
       else if (name == "mu_t") v = c.mu_t;
+      else if (name == "mu") v = c.mu;
+      else if (name == "lam") v = c.lam;
+      else if (name == "Diff") v = c.Diff;
+      else if (name == "dUdx") v = c.dUdx;
+      else if (name == "dTdy") v = c.dTdy;
       else if (name == "k") v = c.k;
       else if (name == "R") v = c.R;
       else if (name == "CP") v = c.CP;
@@ -267,6 +272,8 @@ PYBIND11_MODULE(_hf2d, m) {
         if (!py_.empty()) save_y_heat_flux(py_, c, c.J);
       });
 
+  m.def("sgl_eligible", [](const Case& c) { std::string w; const bool ok = sgl_eligible(c, &w); return py::make_tuple(ok, w); },
+        py::arg("case"), "single-gas laminar N-S specialisation eligibility (ok, reason)");
   m.def("cond_names", &cond_names, py::arg("CT"), "PrintCond: names of the set CondType2D bits");
   m.def("turb_cond_names", &turb_cond_names, py::arg("TT"), "PrintTurbCond: names of the set TurbulenceCondType2D bits");
 
@@ -397,6 +404,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
       .def_readwrite("lean_march", &DeviceSolver::lean_march)
+      .def_readwrite("sgl", &DeviceSolver::sgl)
+      .def_readonly("sgl_ok", &DeviceSolver::sgl_ok)
+      .def_readonly("sgl_why", &DeviceSolver::sgl_why)
       .def_readwrite("lean_pipe", &DeviceSolver::lean_pipe)
       .def_property("lean_sgtab", [](const DeviceSolver& d) { return d.lean_sgtab; },
                     [](DeviceSolver& d, bool on) { d.lean_sgtab = on; d.upload(); })

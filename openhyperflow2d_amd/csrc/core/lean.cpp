@@ -34,6 +34,42 @@ bool lean_eligible(const Case& cs, std::string* why) {
   return true;
 }
 
+// Single-gas laminar N-S specialisation of the generic stepper (fill_cell /
+// predict_cell_t <SGL>): only equations 0..3 and the fields the next step
+// reads move through memory.  Requires species +0 everywhere, no species
+// sources, no turbulence model, mu_t = lam_t = 0, Y = (0,0,0,1) and (with
+// chemistry on) R = R_air everywhere -- then the generic stepper leaves every
+// skipped field unchanged.
+bool sgl_eligible(const Case& cs, std::string* why) {
+  auto no = [&](const char* w) {
+    if (why) *why = w;
+    return false;
+  };
+  const Config& C = cs.cfg;
+  if (C.ProblemType != SM_NS) return no("inviscid problem");
+  if (!C.sources.empty()) return no("gas sources");
+  if (C.chem_model == CRM_ARRENIUS) return no("finite-rate chemistry sources");
+  if (!lean_single_gas(cs)) return no("species present");
+  const real Rair = C.species.R[H_AIR];
+  // boundary-condition bits alone leave turb_model() a no-op; the model bits
+  // (or an initial-reset pass on any TurbType, which sets mu_t = 5 mu) do not
+  const u64 model = TCT_k_eps_Model | TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
+                    TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model | TCT_nut_92_Model |
+                    TCT_Smagorinsky_Model;
+  for (const CellRecord& c : cs.J.c) {
+    if ((c.TurbType & model) != 0) return no("turbulence model");
+    if (c.TurbType != 0 && C.isTurbulenceReset) return no("turbulence reset pass");
+    if (c.is(CT_SOLID)) continue;
+    if (c.mu_t != 0. || c.lam_t != 0.) return no("non-zero eddy viscosity");
+    for (int k = 4; k < 4 + NCOMP; k++)
+      if (c.Src[k] != 0.) return no("species sources");
+    if (!(c.Y[0] == 0. && c.Y[1] == 0. && c.Y[2] == 0. && c.Y[3] == 1.)) return no("mixture fractions");
+    if (C.chem_model != NO_REACTIONS && std::memcmp(&c.R, &Rair, sizeof(real)) != 0) return no("R != R_air");
+  }
+  if (why) why->clear();
+  return true;
+}
+
 bool lean_single_gas(const Case& cs) {
   static const real zero = 0.0;
   for (const CellRecord& c : cs.J.c)

@@ -545,6 +545,21 @@ HF_HD inline void chemistry_zeldovich(N& n, const SpeciesProps& sp, int sm, int 
   }
 }
 
+// chemistry_zeldovich() for a viscous node whose fuel/oxidiser/product
+// partial densities are +0: every zero-fraction term of the mixture sums is
+// +0, so R = R_air, Cp/lam/mu = table_air(T) * 1 and Y = (0, 0, 0, 1) exactly
+// (the species S stay +0).  Used by the single-gas laminar N-S path.
+template <class N>
+HF_HD inline void chemistry_single_gas_ns(N& n, const SpeciesProps& sp) {
+  const real T = n.Tg;
+  n.R = ((sp.R[H_FU] * 0. + sp.R[H_OX] * 0.) + sp.R[H_CP] * 0.) + sp.R[H_AIR] * 1.;
+  n.CP = table_eval(sp.Cp[H_AIR], T) * 1.;
+  n.lam = table_eval(sp.lam[H_AIR], T) * 1.;
+  n.mu = table_eval(sp.mu[H_AIR], T) * 1.;
+  n.Y[0] = n.Y[1] = n.Y[2] = 0.;
+  n.Y[3] = 1.;
+}
+
 // Finite-rate global H2/air reaction (new; the reference declares the
 // CRM_ARRENIUS slot without implementing it): 2 H2 + O2 -> 2 H2O with
 // W = A exp(-Ta/T) [H2]^a [O2]^b (default: the one-step global rate with

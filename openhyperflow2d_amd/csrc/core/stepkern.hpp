@@ -319,9 +319,11 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
   }
 }
 
-// Accessor over the full SoA arrays (fluxes loaded).
+// Accessor over the full SoA arrays (fluxes loaded).  NEF < NEQ: only the
+// first NEF equations are touched (single-gas laminar specialisation).
+template <int NEF = NEQ>
 struct SoAPredictIO {
-  static constexpr int NE = NEQ;
+  static constexpr int NE = NEF;
   const SoA& in;
   const SoA& out;
   long N, idx, iL, iR, iU, iD;
@@ -355,15 +357,16 @@ struct SoAPredictIO {
   uint8_t gf = 0xff;
 };
 
-template <bool RES>
+template <bool RES, bool SGL = false>
 HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
                                  ResidualPack& res) {
+  constexpr int NEF = SGL ? 4 : NEQ;
   const long N = in.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = in.CT[idx];
   const uint8_t gf = in.gf ? in.gf[idx] : (uint8_t)0xff;
   if (!is_active(CT)) {
-    for (int k = 0; k < NEQ; k++) {
+    for (int k = 0; k < NEF; k++) {
       out.S[k * N + idx] = in.S[k * N + idx];
       if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
       if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
@@ -374,7 +377,7 @@ HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& 
   const uint8_t nbm = in.nb[idx];
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-  SoAPredictIO io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
+  SoAPredictIO<NEF> io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
   predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
 }
 
@@ -395,15 +398,24 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
 // and written to `out` (the same arrays except A/B in the fused Euler path).
 // Returns the local dt (1.0 when the cell does not limit dt); sets *neg_T.
 // ---------------------------------------------------------------------------
+// SGL (single-gas laminar N-S, sgl_eligible() on the host): the species
+// partial densities are +0 and stay so, mu_t = lam_t = 0, no turbulence
+// equations -- only equations 0..3 and the fields the next step reads are
+// loaded and stored (S, A, B, F, Src, SrcAdd of 0..3; U, V, Tg, p, k, CP,
+// lam, mu; R only if it changed), chemistry reduces to chemistry_single_gas();
+// output-only fields (Diff, grad, Y, ...) are written when store_grad (the
+// host reads the record after this step).  Fields equal the generic path.
+template <bool SGL = false>
 HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
                             int* neg_T, bool store_grad) {
   const long N = sin.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = sin.CT[idx];
+  constexpr int NEF = SGL ? 4 : NEQ;
   CellLocal c;
-  for (int k = 0; k < NEQ; k++) c.S[k] = sin.S[k * N + idx];
+  for (int k = 0; k < NEQ; k++) c.S[k] = (k < NEF) ? sin.S[k * N + idx] : 0.0;
   if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
-    for (int k = 0; k < NEQ; k++) out.S[k * N + idx] = c.S[k];
+    for (int k = 0; k < NEF; k++) out.S[k * N + idx] = c.S[k];
     return 1.0;
   }
   const bool active = !has_all(CT, NT_FC);
@@ -413,11 +425,12 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   c.CT = CT;
   c.TurbType = sin.TT[idx];
   for (int k = 0; k < NEQ; k++) {
-    c.A[k] = sin.A[k * N + idx];
-    c.B[k] = sin.B[k * N + idx];
-    c.F[k] = axi ? sin.F[k * N + idx] : 0.0;
-    c.Src[k] = ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) ? sin.Src[k * N + idx] : 0.0;
-    c.SrcAdd[k] = (gf & GF_SRCADD) ? sin.SrcAdd[k * N + idx] : 0.0;
+    const bool ld = k < NEF;
+    c.A[k] = ld ? sin.A[k * N + idx] : 0.0;
+    c.B[k] = ld ? sin.B[k * N + idx] : 0.0;
+    c.F[k] = (axi && ld) ? sin.F[k * N + idx] : 0.0;
+    c.Src[k] = (ld && ((k >= 4 + NCOMP && ns) || (gf & GF_SRC))) ? sin.Src[k * N + idx] : 0.0;
+    c.SrcAdd[k] = (ld && (gf & GF_SRCADD)) ? sin.SrcAdd[k * N + idx] : 0.0;
     c.RX[k] = c.RY[k] = 0;
   }
   c.U = prim_old.U[idx];
@@ -429,19 +442,26 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   c.CP = sin.CP[idx];
   c.lam = sin.lam[idx];
   c.mu = sin.mu[idx];
-  c.Diff = sin.Diff[idx];
-  c.mu_t = sin.mu_t[idx];
-  c.lam_t = sin.lam_t[idx];
-  c.l_min = sin.l_min[idx];
-  c.y_plus = sin.y_plus[idx];
-  c.Re_local = sin.Re_local[idx];
-  c.BGX = sin.BGX[idx];
-  c.BGY = sin.BGY[idx];
-  c.Tf = sin.Tf[idx];
+  const bool wall = has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW);
+  if (SGL) {   // recomputed before use, zero, or turbulence/chemistry-only
+    c.Diff = c.mu_t = c.lam_t = c.l_min = c.y_plus = c.Re_local = c.Tf = 0.0;
+    c.BGX = wall ? sin.BGX[idx] : 0.0;
+    c.BGY = wall ? sin.BGY[idx] : 0.0;
+  } else {
+    c.Diff = sin.Diff[idx];
+    c.mu_t = sin.mu_t[idx];
+    c.lam_t = sin.lam_t[idx];
+    c.l_min = sin.l_min[idx];
+    c.y_plus = sin.y_plus[idx];
+    c.Re_local = sin.Re_local[idx];
+    c.BGX = sin.BGX[idx];
+    c.BGY = sin.BGY[idx];
+    c.Tf = sin.Tf[idx];
+  }
   c.Uw = c.Vw = 0;
   c.y = (j + 0.5) * P.dy;
   for (int s = 0; s < NSPEC; s++) {
-    c.Y[s] = sin.Y[s * N + idx];
+    c.Y[s] = SGL ? (s == NCOMP ? 1.0 : 0.0) : sin.Y[s * N + idx];
     c.droYdx[s] = c.droYdy[s] = 0;
   }
   if (!(active && ns)) {   // velocity/temperature gradients are recomputed below for active viscous nodes
@@ -452,10 +472,14 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     c.dTdx = sin.grad[G_DTDX * N + idx];
     c.dTdy = sin.grad[G_DTDY * N + idx];
   }
-  c.dkdx = sin.grad[G_DKDX * N + idx];
-  c.dkdy = sin.grad[G_DKDY * N + idx];
-  c.depsdx = sin.grad[G_DEDX * N + idx];
-  c.depsdy = sin.grad[G_DEDY * N + idx];
+  if (SGL) {
+    c.dkdx = c.dkdy = c.depsdx = c.depsdy = 0.0;
+  } else {
+    c.dkdx = sin.grad[G_DKDX * N + idx];
+    c.dkdy = sin.grad[G_DKDY * N + idx];
+    c.depsdx = sin.grad[G_DEDX * N + idx];
+    c.depsdy = sin.grad[G_DEDY * N + idx];
+  }
 
   if (active && P.sm == SM_NS) {
     const uint8_t nbm = sin.nb[idx];
@@ -468,7 +492,9 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     real aR = sin.S[iR], aL = sin.S[iL], aU = sin.S[iU], aD = sin.S[iD];
     c.droYdx[NCOMP] = c.droYdy[NCOMP] = 0.;
     const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
-    for (int k = 4; k < 4 + NCOMP; k++) {
+    // SGL: species partial densities are +0, so aR - 0 - 0 - 0 == aR and the
+    // species gradients are (0 - 0) * d == +0
+    for (int k = 4; k < (SGL ? 4 : 4 + NCOMP); k++) {
       const long o = k * N;
       if (!nx0) {
         c.droYdx[k - 4] = (sin.S[o + iR] - sin.S[o + iL]) * dx_1_n;
@@ -529,7 +555,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     fp.is_mu_t = P.ffc.is_mu_t;
     fp.is_init = P.ffc.is_init;
   }
-  fill_node(c, fp);
+  const bool filled = fill_node(c, fp);
 
   real dt_local = 1.0;
   if (active) {
@@ -542,15 +568,23 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
         const real nu_eff = (c.mu + c.mu_t) / c.S[I_RHO];
         if (nu_eff > 0) dt_local = hf_min(dt_local, P.visc_cfl / (nu_eff * (1.0 / (P.dx * P.dx) + 1.0 / (P.dy * P.dy))));
       }
-      if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
-      if (P.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, *P.species, P.dt);
+      if (SGL) {
+        if (P.chem_model != NO_REACTIONS) chemistry_single_gas_ns(c, *P.species);
+      } else {
+        if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
+        if (P.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, *P.species, P.dt);
+      }
     }
   }
-  for (int k = 0; k < NEQ; k++) {
+  // SGL: a skipped node (fill_node returned false) keeps its stored fluxes
+  const bool wflux = !SGL || filled;
+  for (int k = 0; k < NEF; k++) {
     out.S[k * N + idx] = c.S[k];
-    out.A[k * N + idx] = c.A[k];
-    out.B[k * N + idx] = c.B[k];
-    if (axi) out.F[k * N + idx] = c.F[k];
+    if (wflux) {
+      out.A[k * N + idx] = c.A[k];
+      out.B[k * N + idx] = c.B[k];
+      if (axi) out.F[k * N + idx] = c.F[k];
+    }
     if ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) out.Src[k * N + idx] = c.Src[k];
     if (gf & GF_SRCADD) out.SrcAdd[k * N + idx] = c.SrcAdd[k];
   }
@@ -559,15 +593,17 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   out.Tg[idx] = c.Tg;
   out.p[idx] = c.p;
   out.kk[idx] = c.k;
-  out.R[idx] = c.R;
+  if (!SGL) out.R[idx] = c.R;   // SGL: R_air, never changes
   out.CP[idx] = c.CP;
   out.lam[idx] = c.lam;
   out.mu[idx] = c.mu;
-  out.Diff[idx] = c.Diff;
-  out.mu_t[idx] = c.mu_t;
-  out.lam_t[idx] = c.lam_t;
-  out.Re_local[idx] = c.Re_local;
-  for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
+  if (!SGL || store_grad) out.Diff[idx] = c.Diff;
+  if (!SGL) {
+    out.mu_t[idx] = c.mu_t;
+    out.lam_t[idx] = c.lam_t;
+    out.Re_local[idx] = c.Re_local;
+    for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
+  }
   if (store_grad && active && P.sm == SM_NS) {
     out.grad[G_DUDX * N + idx] = c.dUdx;
     out.grad[G_DUDY * N + idx] = c.dUdy;
@@ -575,6 +611,8 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     out.grad[G_DVDY * N + idx] = c.dVdy;
     out.grad[G_DTDX * N + idx] = c.dTdx;
     out.grad[G_DTDY * N + idx] = c.dTdy;
+  }
+  if (!SGL && store_grad && active && P.sm == SM_NS) {   // turbulence gradients (never read by SGL)
     out.grad[G_DKDX * N + idx] = c.dkdx;
     out.grad[G_DKDY * N + idx] = c.dkdy;
     out.grad[G_DEDX * N + idx] = c.depsdx;

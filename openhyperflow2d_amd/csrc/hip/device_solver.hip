@@ -125,7 +125,7 @@ __device__ inline void shfl_merge(ResidualPack& r, int off) {
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-template <bool RES>
+template <bool RES, bool SGL = false>
 __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA out, long c0, long c1,
                                                        DevScalars* sc, int slot, int slot_next, int serial,
                                                        ResidualPack* partials) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
   }
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    predict_cell_t<RES>(P, in, out, i, j, r);
+    predict_cell_t<RES, SGL>(P, in, out, i, j, r);
   }
   if (RES) {
 #pragma unroll
@@ -175,15 +175,17 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
   }
 }
 
+template <bool SGL = false>
 __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
-                                                    DevScalars* sc, int slot, int slot_next, int serial) {
+                                                    DevScalars* sc, int slot, int slot_next, int serial,
+                                                    int store_grad) {
   apply_dt(P, sc, slot);
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   double dtl = 1.0;
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    dtl = fill_cell(P, sin, pold, out, i, j, &neg, true);
+    dtl = fill_cell<SGL>(P, sin, pold, out, i, j, &neg, store_grad != 0);
   }
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
   __shared__ double sdt[BLOCK / WAVE];
@@ -1286,6 +1288,7 @@ void DeviceSolver::upload() {
   compute_generic_flags(cs, h);
   cp(m.gf, h.gf.data(), N);
   lean_ok = lean_eligible(cs, &lean_why);
+  sgl_ok = sgl_eligible(cs, &sgl_why);
   lean_sg_ok = lean_ok && lean_single_gas(cs);
   lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
   if (lean_ok) {
@@ -1831,7 +1834,7 @@ void DeviceSolver::p2p_complete() {
 namespace {
 constexpr int GRAPH_STEPS = 6;
 uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fused, bool tile, bool sg, int cpt,
-                         int tj, int march, int pipe, int fuse) {
+                         int tj, int march, int pipe, int fuse, int sglf) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
   mix((uint64_t)P.fpa.is_mu_t);
@@ -1847,6 +1850,7 @@ uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fu
   mix((uint64_t)march);
   mix((uint64_t)pipe);
   mix((uint64_t)fuse);
+  mix((uint64_t)sglf);
   return h;
 }
 }  // namespace
@@ -1885,11 +1889,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
   const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on));
+                                       lean_cpt, lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok));
   bool same = true;
   for (const StepParams& p : pending)
     same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on)) == sig;
+                                   lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok)) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -2128,18 +2132,33 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (lean_state) lean_materialize();
     SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
     SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
-    if (want_res)
-      hipLaunchKernelGGL(hf2d_predict<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next,
-                         serial, m.partials);
-    else
-      hipLaunchKernelGGL(hf2d_predict<false>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next,
-                         serial, m.partials);
+    // single-gas laminar N-S: only equations 0..3 and the live fields move
+    const bool sgl_now = sgl && sgl_ok && P.sm == SM_NS;
+    if (want_res) {
+      if (sgl_now)
+        hipLaunchKernelGGL((hf2d_predict<true, true>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+      else
+        hipLaunchKernelGGL((hf2d_predict<true, false>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+    } else {
+      if (sgl_now)
+        hipLaunchKernelGGL((hf2d_predict<false, true>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+      else
+        hipLaunchKernelGGL((hf2d_predict<false, false>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
+                           slot_next, serial, m.partials);
+    }
     HIP_CHECK(hipGetLastError());
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
     SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
-    hipLaunchKernelGGL(hf2d_fill, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot, slot_next,
-                       serial);
+    if (sgl_now)   // gradients / Diff only when the host reads the record (or y+ follows)
+      hipLaunchKernelGGL(hf2d_fill<true>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+                         slot_next, serial, (step_outputs || want_res) ? 1 : 0);
+    else
+      hipLaunchKernelGGL(hf2d_fill<false>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+                         slot_next, serial, 1);
     HIP_CHECK(hipGetLastError());
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;

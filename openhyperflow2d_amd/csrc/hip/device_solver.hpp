@@ -120,6 +120,9 @@ class DeviceSolver : public SolverBase {
   void set_lean_plain(bool on);
   bool lean_ok = false;
   std::string lean_why;
+  bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
+  bool sgl_ok = false;
+  std::string sgl_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)

@@ -361,3 +361,26 @@ def test_march_kernel_bitwise_equals_tile(gpu, deck, march, sg):
     # residual sums are accumulated per wave instead of per workgroup
     np.testing.assert_allclose(a.summary()["rms"], b.summary()["rms"], rtol=1e-12, atol=0)
     assert a.records() == b.records()
+
+
+@pytest.mark.parametrize("deck", ["step", "step_ref_ns"])
+def test_sgl_ns_specialisation_equals_generic(gpu, deck):
+    """Single-gas laminar N-S path (fill_cell/predict_cell_t <SGL>: equations
+    0..3 and live fields only) == the generic split kernels on every field
+    (+-0 of never-read species fluxes aside), dt and time."""
+    from tests.conftest import read_deck
+
+    text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5) if deck == "step" else \
+        decks.set_key(read_deck("Step.dat"), "ProblemType", 1)   # reference deck, laminar N-S
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    b.solver.sgl = False
+    assert a.solver.sgl_ok, a.solver.sgl_why
+    for n, res in [(4, True), (30, False), (6, True), (19, False)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+    assert a.summary()["dt"] == b.summary()["dt"]
+    assert a.summary()["time"] == b.summary()["time"]
+    np.testing.assert_array_equal(a.summary()["rms"], b.summary()["rms"])
+    for f in FIELDS + ["k", "R", "CP", "mu", "lam", "dUdx", "dTdy"]:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
