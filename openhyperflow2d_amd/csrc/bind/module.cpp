@@ -272,8 +272,8 @@ PYBIND11_MODULE(_hf2d, m) {
         if (!py_.empty()) save_y_heat_flux(py_, c, c.J);
       });
 
-  m.def("sgl_eligible", [](const Case& c) { std::string w; const bool ok = sgl_eligible(c, &w); return py::make_tuple(ok, w); },
-        py::arg("case"), "single-gas laminar N-S specialisation eligibility (ok, reason)");
+  m.def("sk_eligible", [](const Case& c) { std::string w; const int md = sk_eligible(c, &w); return py::make_tuple(md, w); },
+        py::arg("case"), "split-kernel specialisation (0 generic, 1 single-gas laminar, 2 single-gas turbulent; reason)");
   m.def("cond_names", &cond_names, py::arg("CT"), "PrintCond: names of the set CondType2D bits");
   m.def("turb_cond_names", &turb_cond_names, py::arg("TT"), "PrintTurbCond: names of the set TurbulenceCondType2D bits");
 
@@ -407,6 +407,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("sgl", &DeviceSolver::sgl)
       .def_readonly("sgl_ok", &DeviceSolver::sgl_ok)
       .def_readonly("sgl_why", &DeviceSolver::sgl_why)
+      .def_readonly("sk_mode", &DeviceSolver::sk_mode)
       .def_readwrite("lean_pipe", &DeviceSolver::lean_pipe)
       .def_property("lean_sgtab", [](const DeviceSolver& d) { return d.lean_sgtab; },
                     [](DeviceSolver& d, bool on) { d.lean_sgtab = on; d.upload(); })

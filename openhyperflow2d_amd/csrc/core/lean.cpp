@@ -40,10 +40,10 @@ bool lean_eligible(const Case& cs, std::string* why) {
 // sources, no turbulence model, mu_t = lam_t = 0, Y = (0,0,0,1) and (with
 // chemistry on) R = R_air everywhere -- then the generic stepper leaves every
 // skipped field unchanged.
-bool sgl_eligible(const Case& cs, std::string* why) {
+int sk_eligible(const Case& cs, std::string* why) {
   auto no = [&](const char* w) {
     if (why) *why = w;
-    return false;
+    return (int)SK_GENERIC;
   };
   const Config& C = cs.cfg;
   if (C.ProblemType != SM_NS) return no("inviscid problem");
@@ -56,18 +56,18 @@ bool sgl_eligible(const Case& cs, std::string* why) {
   const u64 model = TCT_k_eps_Model | TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
                     TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model | TCT_nut_92_Model |
                     TCT_Smagorinsky_Model;
+  bool laminar = true;
   for (const CellRecord& c : cs.J.c) {
-    if ((c.TurbType & model) != 0) return no("turbulence model");
-    if (c.TurbType != 0 && C.isTurbulenceReset) return no("turbulence reset pass");
+    if ((c.TurbType & model) != 0 || (c.TurbType != 0 && C.isTurbulenceReset)) laminar = false;
     if (c.is(CT_SOLID)) continue;
-    if (c.mu_t != 0. || c.lam_t != 0.) return no("non-zero eddy viscosity");
+    if (c.mu_t != 0. || c.lam_t != 0.) laminar = false;
     for (int k = 4; k < 4 + NCOMP; k++)
       if (c.Src[k] != 0.) return no("species sources");
     if (!(c.Y[0] == 0. && c.Y[1] == 0. && c.Y[2] == 0. && c.Y[3] == 1.)) return no("mixture fractions");
     if (C.chem_model != NO_REACTIONS && std::memcmp(&c.R, &Rair, sizeof(real)) != 0) return no("R != R_air");
   }
-  if (why) why->clear();
-  return true;
+  if (why) *why = laminar ? "" : "turbulent: SK_SGT";
+  return laminar ? SK_SGL : SK_SGT;
 }
 
 bool lean_single_gas(const Case& cs) {

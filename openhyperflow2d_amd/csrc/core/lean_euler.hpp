@@ -180,6 +180,7 @@ HF_HD inline void lean_load_own(const LeanSoA& L, long idx, LeanOwn& o) {
 // memory, addressed by the global indices idx / iL / iR / iU / iD.
 struct LeanIOCommon {
   static constexpr int NE = 4 + NCOMP;
+  static constexpr bool skip(int) { return false; }
   const LeanSoA& L;
   long N, idx, iL, iR, iU, iD;
   uint8_t lb = 0;

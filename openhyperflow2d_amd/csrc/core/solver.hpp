@@ -153,7 +153,7 @@ void install_signal_handlers();
 // lean inviscid path (lean.cpp)
 bool lean_eligible(const Case& cs, std::string* why);
 bool lean_single_gas(const Case& cs);
-bool sgl_eligible(const Case& cs, std::string* why);
+int sk_eligible(const Case& cs, std::string* why);   // SK_* mode of the split kernels
 bool lean_any_cauchy_x(const Case& cs);
 // per-cell GF_* flags of the generic stepper (from the uploaded host arrays)
 void compute_generic_flags(const Case& cs, HostArrays& h);

@@ -223,6 +223,7 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
   const bool axi = P.fpa.FT != 0;
 #pragma unroll
   for (int k = 0; k < IO::NE; k++) {
+    if (IO::skip(k)) continue;   // equation not stored by this accessor (single-gas species)
     real s = io.S(k);
     const EqFlags f = PLAIN ? EqFlags{true, true, true, false, false} : eq_flags(k, CT, TT, P.sm);
     if (!PLAIN &&
@@ -319,11 +320,23 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
   }
 }
 
-// Accessor over the full SoA arrays (fluxes loaded).  NEF < NEQ: only the
-// first NEF equations are touched (single-gas laminar specialisation).
-template <int NEF = NEQ>
+// Specialisations of the generic (split) stepper, selected on the host:
+//   SK_GENERIC  every field of the reference record
+//   SK_SGL      single-gas laminar N-S: equations 0..3 only
+//   SK_SGT      single-gas N-S with a turbulence model: equations 0..3, 7, 8
+// Species partial densities are +0 and stay so in both specialisations (the
+// argument of the lean single-gas path), so their equations, fluxes, mixture
+// fractions and R need not move through memory (sk_eligible on the host).
+enum { SK_GENERIC = 0, SK_SGL = 1, SK_SGT = 2 };
+HF_HD constexpr bool sk_live(int mode, int k) {
+  return mode == SK_GENERIC || k < 4 || (mode == SK_SGT && k >= 4 + NCOMP);
+}
+
+// Accessor over the full SoA arrays (fluxes loaded).
+template <int MODE = SK_GENERIC>
 struct SoAPredictIO {
-  static constexpr int NE = NEF;
+  static constexpr int NE = MODE == SK_SGL ? 4 : NEQ;
+  static constexpr bool skip(int k) { return !sk_live(MODE, k); }
   const SoA& in;
   const SoA& out;
   long N, idx, iL, iR, iU, iD;
@@ -357,16 +370,16 @@ struct SoAPredictIO {
   uint8_t gf = 0xff;
 };
 
-template <bool RES, bool SGL = false>
+template <bool RES, int MODE = SK_GENERIC>
 HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
                                  ResidualPack& res) {
-  constexpr int NEF = SGL ? 4 : NEQ;
   const long N = in.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = in.CT[idx];
   const uint8_t gf = in.gf ? in.gf[idx] : (uint8_t)0xff;
   if (!is_active(CT)) {
-    for (int k = 0; k < NEF; k++) {
+    for (int k = 0; k < NEQ; k++) {
+      if (!sk_live(MODE, k)) continue;
       out.S[k * N + idx] = in.S[k * N + idx];
       if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
       if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
@@ -377,7 +390,7 @@ HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& 
   const uint8_t nbm = in.nb[idx];
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-  SoAPredictIO<NEF> io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
+  SoAPredictIO<MODE> io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
   predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
 }
 
@@ -398,24 +411,24 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
 // and written to `out` (the same arrays except A/B in the fused Euler path).
 // Returns the local dt (1.0 when the cell does not limit dt); sets *neg_T.
 // ---------------------------------------------------------------------------
-// SGL (single-gas laminar N-S, sgl_eligible() on the host): the species
-// partial densities are +0 and stay so, mu_t = lam_t = 0, no turbulence
-// equations -- only equations 0..3 and the fields the next step reads are
-// loaded and stored (S, A, B, F, Src, SrcAdd of 0..3; U, V, Tg, p, k, CP,
-// lam, mu; R only if it changed), chemistry reduces to chemistry_single_gas();
-// output-only fields (Diff, grad, Y, ...) are written when store_grad (the
-// host reads the record after this step).  Fields equal the generic path.
-template <bool SGL = false>
+// MODE (SK_*, see SoAPredictIO): the specialisations load and store only the
+// live equations and the fields the next step reads (S, A, B, F, Src, SrcAdd
+// of live equations; U, V, Tg, p, k, CP, lam, mu; SGT also the turbulence
+// fields); chemistry reduces to chemistry_single_gas_ns(); output-only fields
+// (SGL: Diff, grad) are written when store_grad (the host reads the record
+// after this step).  Every field equals the generic path (GPU tests).
+template <int MODE = SK_GENERIC>
 HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
                             int* neg_T, bool store_grad) {
   const long N = sin.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = sin.CT[idx];
-  constexpr int NEF = SGL ? 4 : NEQ;
+  constexpr bool SGL = MODE == SK_SGL, SG = MODE != SK_GENERIC;
   CellLocal c;
-  for (int k = 0; k < NEQ; k++) c.S[k] = (k < NEF) ? sin.S[k * N + idx] : 0.0;
+  for (int k = 0; k < NEQ; k++) c.S[k] = sk_live(MODE, k) ? sin.S[k * N + idx] : 0.0;
   if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
-    for (int k = 0; k < NEF; k++) out.S[k * N + idx] = c.S[k];
+    for (int k = 0; k < NEQ; k++)
+      if (sk_live(MODE, k)) out.S[k * N + idx] = c.S[k];
     return 1.0;
   }
   const bool active = !has_all(CT, NT_FC);
@@ -425,7 +438,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   c.CT = CT;
   c.TurbType = sin.TT[idx];
   for (int k = 0; k < NEQ; k++) {
-    const bool ld = k < NEF;
+    const bool ld = sk_live(MODE, k);
     c.A[k] = ld ? sin.A[k * N + idx] : 0.0;
     c.B[k] = ld ? sin.B[k * N + idx] : 0.0;
     c.F[k] = (axi && ld) ? sin.F[k * N + idx] : 0.0;
@@ -461,7 +474,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   c.Uw = c.Vw = 0;
   c.y = (j + 0.5) * P.dy;
   for (int s = 0; s < NSPEC; s++) {
-    c.Y[s] = SGL ? (s == NCOMP ? 1.0 : 0.0) : sin.Y[s * N + idx];
+    c.Y[s] = SG ? (s == NCOMP ? 1.0 : 0.0) : sin.Y[s * N + idx];
     c.droYdx[s] = c.droYdy[s] = 0;
   }
   if (!(active && ns)) {   // velocity/temperature gradients are recomputed below for active viscous nodes
@@ -494,7 +507,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
     // SGL: species partial densities are +0, so aR - 0 - 0 - 0 == aR and the
     // species gradients are (0 - 0) * d == +0
-    for (int k = 4; k < (SGL ? 4 : 4 + NCOMP); k++) {
+    for (int k = 4; k < (SG ? 4 : 4 + NCOMP); k++) {
       const long o = k * N;
       if (!nx0) {
         c.droYdx[k - 4] = (sin.S[o + iR] - sin.S[o + iL]) * dx_1_n;
@@ -568,7 +581,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
         const real nu_eff = (c.mu + c.mu_t) / c.S[I_RHO];
         if (nu_eff > 0) dt_local = hf_min(dt_local, P.visc_cfl / (nu_eff * (1.0 / (P.dx * P.dx) + 1.0 / (P.dy * P.dy))));
       }
-      if (SGL) {
+      if (SG) {
         if (P.chem_model != NO_REACTIONS) chemistry_single_gas_ns(c, *P.species);
       } else {
         if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
@@ -577,8 +590,9 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     }
   }
   // SGL: a skipped node (fill_node returned false) keeps its stored fluxes
-  const bool wflux = !SGL || filled;
-  for (int k = 0; k < NEF; k++) {
+  const bool wflux = !SG || filled;
+  for (int k = 0; k < NEQ; k++) {
+    if (!sk_live(MODE, k)) continue;
     out.S[k * N + idx] = c.S[k];
     if (wflux) {
       out.A[k * N + idx] = c.A[k];
@@ -593,7 +607,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   out.Tg[idx] = c.Tg;
   out.p[idx] = c.p;
   out.kk[idx] = c.k;
-  if (!SGL) out.R[idx] = c.R;   // SGL: R_air, never changes
+  if (!SG) out.R[idx] = c.R;   // single gas: R_air, never changes
   out.CP[idx] = c.CP;
   out.lam[idx] = c.lam;
   out.mu[idx] = c.mu;
@@ -602,8 +616,9 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     out.mu_t[idx] = c.mu_t;
     out.lam_t[idx] = c.lam_t;
     out.Re_local[idx] = c.Re_local;
-    for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
   }
+  if (!SG)
+    for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
   if (store_grad && active && P.sm == SM_NS) {
     out.grad[G_DUDX * N + idx] = c.dUdx;
     out.grad[G_DUDY * N + idx] = c.dUdy;

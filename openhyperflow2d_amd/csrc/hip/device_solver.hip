@@ -125,7 +125,7 @@ __device__ inline void shfl_merge(ResidualPack& r, int off) {
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-template <bool RES, bool SGL = false>
+template <bool RES, int MODE = SK_GENERIC>
 __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA out, long c0, long c1,
                                                        DevScalars* sc, int slot, int slot_next, int serial,
                                                        ResidualPack* partials) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
   }
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    predict_cell_t<RES, SGL>(P, in, out, i, j, r);
+    predict_cell_t<RES, MODE>(P, in, out, i, j, r);
   }
   if (RES) {
 #pragma unroll
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
   }
 }
 
-template <bool SGL = false>
+template <int MODE = SK_GENERIC>
 __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
                                                     DevScalars* sc, int slot, int slot_next, int serial,
                                                     int store_grad) {
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA po
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    dtl = fill_cell<SGL>(P, sin, pold, out, i, j, &neg, store_grad != 0);
+    dtl = fill_cell<MODE>(P, sin, pold, out, i, j, &neg, store_grad != 0);
   }
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
   __shared__ double sdt[BLOCK / WAVE];
@@ -1288,7 +1288,8 @@ void DeviceSolver::upload() {
   compute_generic_flags(cs, h);
   cp(m.gf, h.gf.data(), N);
   lean_ok = lean_eligible(cs, &lean_why);
-  sgl_ok = sgl_eligible(cs, &sgl_why);
+  sk_mode = sk_eligible(cs, &sgl_why);
+  sgl_ok = sk_mode != SK_GENERIC;
   lean_sg_ok = lean_ok && lean_single_gas(cs);
   lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
   if (lean_ok) {
@@ -2132,32 +2133,35 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (lean_state) lean_materialize();
     SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
     SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
-    // single-gas laminar N-S: only equations 0..3 and the live fields move
-    const bool sgl_now = sgl && sgl_ok && P.sm == SM_NS;
+    // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT)
+    const int mode = (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+#define HF2D_PRED(R, M)                                                                                     \
+  hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
+                     serial, m.partials)
     if (want_res) {
-      if (sgl_now)
-        hipLaunchKernelGGL((hf2d_predict<true, true>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else
-        hipLaunchKernelGGL((hf2d_predict<true, false>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
+      if (mode == SK_SGL) HF2D_PRED(true, SK_SGL);
+      else if (mode == SK_SGT) HF2D_PRED(true, SK_SGT);
+      else HF2D_PRED(true, SK_GENERIC);
     } else {
-      if (sgl_now)
-        hipLaunchKernelGGL((hf2d_predict<false, true>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else
-        hipLaunchKernelGGL((hf2d_predict<false, false>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
+      if (mode == SK_SGL) HF2D_PRED(false, SK_SGL);
+      else if (mode == SK_SGT) HF2D_PRED(false, SK_SGT);
+      else HF2D_PRED(false, SK_GENERIC);
     }
+#undef HF2D_PRED
     HIP_CHECK(hipGetLastError());
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
     SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
-    if (sgl_now)   // gradients / Diff only when the host reads the record (or y+ follows)
-      hipLaunchKernelGGL(hf2d_fill<true>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
-                         slot_next, serial, (step_outputs || want_res) ? 1 : 0);
+    // SGL: gradients / Diff only when the host reads the record (or y+ follows)
+    const int sg_out = (step_outputs || want_res) ? 1 : 0;
+    if (mode == SK_SGL)
+      hipLaunchKernelGGL(hf2d_fill<SK_SGL>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+                         slot_next, serial, sg_out);
+    else if (mode == SK_SGT)
+      hipLaunchKernelGGL(hf2d_fill<SK_SGT>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+                         slot_next, serial, 1);
     else
-      hipLaunchKernelGGL(hf2d_fill<false>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+      hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
                          slot_next, serial, 1);
     HIP_CHECK(hipGetLastError());
     dsbuf = 1 - dsbuf;

@@ -122,6 +122,7 @@ class DeviceSolver : public SolverBase {
   std::string lean_why;
   bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
   bool sgl_ok = false;
+  int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)
   std::string sgl_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
   std::vector<uint8_t> lean_bytes;

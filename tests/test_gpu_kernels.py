@@ -363,24 +363,31 @@ def test_march_kernel_bitwise_equals_tile(gpu, deck, march, sg):
     assert a.records() == b.records()
 
 
-@pytest.mark.parametrize("deck", ["step", "step_ref_ns"])
-def test_sgl_ns_specialisation_equals_generic(gpu, deck):
-    """Single-gas laminar N-S path (fill_cell/predict_cell_t <SGL>: equations
-    0..3 and live fields only) == the generic split kernels on every field
-    (+-0 of never-read species fluxes aside), dt and time."""
+@pytest.mark.parametrize("deck,mode", [("step", 1), ("step_ref_ns", 1), ("resonator", 2), ("wedge_keps", 2)])
+def test_single_gas_ns_specialisation_equals_generic(gpu, deck, mode):
+    """Single-gas N-S split kernels (fill_cell/predict_cell_t <SK_SGL> laminar:
+    equations 0..3 only; <SK_SGT> turbulent: 0..3 + k, eps) == the generic
+    split kernels on every field (+-0 of never-read species fluxes aside),
+    dt, time and residuals."""
     from tests.conftest import read_deck
 
-    text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5) if deck == "step" else \
-        decks.set_key(read_deck("Step.dat"), "ProblemType", 1)   # reference deck, laminar N-S
+    if deck == "step":
+        text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5)
+    elif deck == "step_ref_ns":
+        text = decks.set_key(read_deck("Step.dat"), "ProblemType", 1)   # reference deck, laminar N-S
+    elif deck == "resonator":
+        text = decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
+    else:
+        text = decks.wedge15(200, 60, navier_stokes=True, turbulence=4, nmax=10 ** 6, nout=10 ** 5)
     a = gpu.Simulation(text, "gpu")
     b = gpu.Simulation(text, "gpu")
     b.solver.sgl = False
-    assert a.solver.sgl_ok, a.solver.sgl_why
+    assert a.solver.sk_mode == mode, a.solver.sgl_why
     for n, res in [(4, True), (30, False), (6, True), (19, False)]:
         a.step(n, residual=res)
         b.step(n, residual=res)
     assert a.summary()["dt"] == b.summary()["dt"]
     assert a.summary()["time"] == b.summary()["time"]
     np.testing.assert_array_equal(a.summary()["rms"], b.summary()["rms"])
-    for f in FIELDS + ["k", "R", "CP", "mu", "lam", "dUdx", "dTdy"]:
+    for f in FIELDS + ["k", "R", "CP", "mu", "lam", "mu_t", "dUdx", "dTdy", "Diff", "S7", "S8"]:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
