@@ -911,39 +911,56 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
   for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
     if (q != a.rank) __hip_atomic_store(&a.peer_flags[q][a.rank], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   const bool failed = __hip_atomic_load(&a.sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2;
+  __shared__ double s_dt[P2P_THREADS];
+  double dmin = mydt;   // each polling thread folds the dt of the peers it waited for
   for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS) {
     if (q == a.rank || failed) continue;   // after one timeout, stop waiting (the host reports it)
     long spins = 0;
+    bool ok = true;
     while (__hip_atomic_load(&a.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > P2P_SPIN_LIMIT) {
         atomicOr(&a.sc->neg_T, 2);
+        ok = false;
         break;
       }
     }
+    if (ok) dmin = fmin(dmin, p2p_load(a.my_dtr + par * a.nranks + q));
   }
+  s_dt[threadIdx.x] = dmin;
   __syncthreads();
-  // 4. unpack this rank's mailbox into the ghost columns
-  if (a.sides & 1) {
-    const real* src = a.my_recv + ((long)par * 2) * a.cap;
-    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
-      const int f = t / ny, j = t - f * ny;
-      a.L.f[f][(long)a.ghostL * ny + j] = p2p_load(src + t);
+  // 4. unpack this rank's mailbox into the ghost columns: all loads of a
+  // thread first, then its stores (the stores may alias nothing the loads
+  // read, but the compiler cannot know that)
+  constexpr int PER = 8;   // (2 sides * 48 fields * ny) / P2P_THREADS slots for ny <= 42; loop otherwise
+  const int total = ((a.sides & 1) ? a.cnt : 0) + ((a.sides & 2) ? a.cnt : 0);
+  for (int base = 0; base < total; base += PER * P2P_THREADS) {
+    real v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int t = base + u * P2P_THREADS + threadIdx.x;
+      if (t < total) {
+        const bool right = !(a.sides & 1) || t >= a.cnt;
+        const int tt = (a.sides & 1) && right ? t - a.cnt : t;
+        v[u] = p2p_load(a.my_recv + ((long)par * 2 + (right ? 1 : 0)) * a.cap + tt);
+      }
     }
-  }
-  if (a.sides & 2) {
-    const real* src = a.my_recv + ((long)par * 2 + 1) * a.cap;
-    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
-      const int f = t / ny, j = t - f * ny;
-      a.L.f[f][(long)a.ghostR * ny + j] = p2p_load(src + t);
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int t = base + u * P2P_THREADS + threadIdx.x;
+      if (t < total) {
+        const bool right = !(a.sides & 1) || t >= a.cnt;
+        const int tt = (a.sides & 1) && right ? t - a.cnt : t;
+        const int f = tt / ny, j = tt - f * ny;
+        a.L.f[f][(long)(right ? a.ghostR : a.ghostL) * ny + j] = v[u];
+      }
     }
   }
   // 5. global dt: MIN over ranks (exact in any order)
   if (threadIdx.x == 0) {
     if (a.fold_dt) {
       double m = mydt;
-      for (int q = 0; q < a.nranks; q++)
-        if (q != a.rank) m = fmin(m, p2p_load(a.my_dtr + par * a.nranks + q));
+      for (int q = 0; q < a.nranks && q < P2P_THREADS; q++) m = fmin(m, s_dt[q]);
       a.sc->dt_bits[a.dslot] = d_to_bits(m);
     }
     *a.seq = seq;
