@@ -409,8 +409,6 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("sgl_why", &DeviceSolver::sgl_why)
       .def_readonly("sk_mode", &DeviceSolver::sk_mode)
       .def_readwrite("lean_pipe", &DeviceSolver::lean_pipe)
-      .def_property("lean_sgtab", [](const DeviceSolver& d) { return d.lean_sgtab; },
-                    [](DeviceSolver& d, bool on) { d.lean_sgtab = on; d.upload(); })
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_readonly("lean_has_cauchy_x", &DeviceSolver::lean_has_cauchy_x)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },

@@ -43,56 +43,8 @@ namespace hf2d {
 // PLAIN) -- set on the host by lean_flags().
 enum : uint8_t { LB_DX_OUT = 16, LB_DY_OUT = 32, LB_PLAIN = 64 };
 
-// Single-gas Cp(T) of the inert component, carried by value in the kernel
-// arguments: evaluated with a branch-free scan over uniform (scalar-register)
-// breakpoints instead of a per-lane linear search through global memory,
-// which put several dependent memory round trips on every cell's critical
-// path.  Same interval and arithmetic as table_eval() for strictly
-// increasing breakpoints (sg_table_set() checks; otherwise n = 0 and the
-// global table is used).
-constexpr int SG_TABLE_PTS = 16;
-struct SGTable {
-  int n = 0;
-  real R_air = 0;
-  real x[SG_TABLE_PTS];
-  real y[SG_TABLE_PTS];
-};
-inline SGTable sg_table_set(const SpeciesProps& sp) {
-  SGTable t;
-  const TableData& c = sp.Cp[H_AIR];
-  t.R_air = sp.R[H_AIR];
-  for (int q = 0; q < SG_TABLE_PTS; q++) t.x[q] = t.y[q] = 0;
-  bool ok = c.n >= 2 && c.n <= SG_TABLE_PTS;
-  for (int q = 1; ok && q < c.n; q++) ok = c.x[q] > c.x[q - 1];
-  if (!ok) return t;   // n = 0: fall back to table_eval
-  t.n = c.n;
-  for (int q = 0; q < c.n; q++) {
-    t.x[q] = c.x[q];
-    t.y[q] = c.y[q];
-  }
-  return t;
-}
-HF_HD inline real sg_table_eval(const SGTable& t, real xv) {
-  // table_eval: i = 1 below x[0], n-1 above x[n-1], else x[i-1] <= xv < x[i]
-  int i = 1;
-#pragma unroll
-  for (int q = 2; q < SG_TABLE_PTS; q++)
-    if (q < t.n && xv >= t.x[q - 1]) i = q;
-  real xi = t.x[1], xm = t.x[0], yi = t.y[1], ym = t.y[0];
-#pragma unroll
-  for (int q = 2; q < SG_TABLE_PTS; q++)
-    if (q == i) {
-      xi = t.x[q];
-      xm = t.x[q - 1];
-      yi = t.y[q];
-      ym = t.y[q - 1];
-    }
-  return yi + (ym - yi) * (xv - xi) / (xm - xi);
-}
-
 struct LeanSoA {
   long N = 0;
-  SGTable sgt;         // single-gas Cp(T) (n = 0: use P.species)
   const real* Sin;     // [NEQ*N] committed state (equations 0..6 used)
   real* Sout;
   const real* Pin_s;   // [NCOMP*N] pre-chemistry species of the last fill
@@ -276,12 +228,13 @@ struct LeanChemNode {
 // chemistry_zeldovich() evaluated for a node whose species partial densities
 // are +0: Y = (0, 0, 0, 1), R = R_air, Cp = Cp_air(T) (each zero-fraction term
 // of the mixture sums is +0, so the sums reduce to the air term exactly).
+// (A copy of the air Cp table in the kernel arguments, scanned branch-free,
+// cost 95 SGPR spills in the tile kernel and ~9 % of its time: measured and
+// removed.)
 template <class N>
-HF_HD inline void chemistry_single_gas(N& n, const SpeciesProps& sp, const SGTable& t) {
-  // (+0 + +0) + +0 + R_air * 1 == R_air exactly: the kernel-argument copy
-  // avoids a dependent global load
-  n.R = t.n ? t.R_air : ((sp.R[H_FU] * 0. + sp.R[H_OX] * 0.) + sp.R[H_CP] * 0.) + sp.R[H_AIR] * 1.;
-  n.CP = (t.n ? sg_table_eval(t, n.Tg) : table_eval(sp.Cp[H_AIR], n.Tg)) * 1.;
+HF_HD inline void chemistry_single_gas(N& n, const SpeciesProps& sp) {
+  n.R = ((sp.R[H_FU] * 0. + sp.R[H_OX] * 0.) + sp.R[H_CP] * 0.) + sp.R[H_AIR] * 1.;
+  n.CP = table_eval(sp.Cp[H_AIR], n.Tg) * 1.;
   n.Y[0] = n.Y[1] = n.Y[2] = 0.;
   n.Y[3] = 1.;
 }
@@ -421,7 +374,7 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
         c.CT = CT;
         c.lam = c.mu = 0.;
         if (SG)
-          chemistry_single_gas(c, *P.species, L.sgt);
+          chemistry_single_gas(c, *P.species);
         else
           chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
         if (c.R != own.R) L.R[idx] = c.R;   // constant for a frozen mixture

@@ -637,7 +637,6 @@ void CpuSolver::download(Field& J) {
 LeanSoA CpuSolver::lean_view(bool fromg) {
   LeanSoA L;
   L.N = h.N;
-  L.sgt = sg_table_set(cs.cfg.species);
   L.Sin = h.S[0].data();
   L.Sout = h.S[1].data();
   L.Pin_s = Spre[pbuf].data();

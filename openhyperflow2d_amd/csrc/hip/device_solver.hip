@@ -1061,11 +1061,9 @@ struct DeviceSolver::Impl {
     double** d_dtr = nullptr;
   } p2p;
 
-  SGTable sgt;   // single-gas Cp table (kernel argument copy)
   LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
     LeanSoA L;
     L.N = h.N;
-    L.sgt = sgt;
     L.Sin = S[sb];
     L.Sout = S[1 - sb];
     L.Pin_s = Spre[pb];
@@ -1319,8 +1317,6 @@ void DeviceSolver::upload() {
   cp(m.iw, h.iw.data(), N * sizeof(int32_t));
   cp(m.jw, h.jw.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
-  m.sgt = sg_table_set(cs.cfg.species);
-  if (!lean_sgtab) m.sgt.n = 0;
   scen_host.cfl = cs.cfg.CFL_Scenario.pack();
   scen_host.beta = cs.cfg.beta_Scenario.pack();
   scen_host.CFL = cs.cfg.CFL;

@@ -111,7 +111,6 @@ class DeviceSolver : public SolverBase {
   int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
   int lean_cpt = 2;
-  bool lean_sgtab = true;  // single-gas Cp table in kernel arguments (lean_euler.hpp SGTable)
   int lean_march = 0;
   int lean_pipe = 0;       // > 0: software-pipelined persistent tile kernel, this many workgroups per CU      // > 0: register-marching kernel with chunks of this many columns
   int cu_count = 256;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)

@@ -33,8 +33,6 @@ def main():
             s.solver.use_graph = False
         elif v0 == "nosg":
             s.solver.lean_sg = False
-        elif v0 == "nosgtab":
-            s.solver.lean_sgtab = False
         elif v0.startswith("pipe"):
             s.solver.lean_pipe = int(v0[4:])
         elif v0.startswith("march"):
