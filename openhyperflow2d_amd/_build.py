@@ -67,6 +67,14 @@ def _ninja_file() -> str:
         "  command = $hipcc --offload-arch=" + ARCH + " $in -o $out $ldflags",
         "rule link_gxx",
         "  command = g++ $in -o $out",
+        # host AddressSanitizer / UBSan build of the CPU CLI (host code only)
+        "rule gxx_asan",
+        "  command = g++ -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -std=c++17 -fPIC -I" + CSRC
+        + " -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "rule link_gxx_asan",
+        "  command = g++ -fsanitize=address,undefined $in -o $out",
     ]
     objs = []
     for s in CORE_SRCS:
@@ -89,10 +97,27 @@ def _ninja_file() -> str:
     lines.append(f"build {ext_path()}: link_so {' '.join(objs + hobjs)} bind_module.o")
     lines.append(f"build {os.path.join(HERE, 'bin', 'hf2d')}: link_exe {' '.join(objs + hobjs)} main.o")
     lines.append(f"build {os.path.join(HERE, 'bin', 'hf2d_cpu')}: link_gxx {' '.join(gobjs)}")
+    aobjs = []
+    for s in CORE_SRCS + ["hf2d_main.cpp"]:
+        o = f"asan_{s[:-4]}.o"
+        lines.append(f"build {o}: gxx_asan {os.path.join(CSRC, 'core', s)}")
+        aobjs.append(o)
+    lines.append(f"build {asan_path()}: link_gxx_asan {' '.join(aobjs)}")
+    lines.append(f"default {ext_path()} {os.path.join(HERE, 'bin', 'hf2d')} {os.path.join(HERE, 'bin', 'hf2d_cpu')}")
     return "\n".join(lines) + "\n"
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> str:
+def asan_path() -> str:
+    return os.path.join(HERE, "bin", "hf2d_cpu_asan")
+
+
+def build_asan(verbose: bool = False) -> str:
+    """Host ASan/UBSan build of the CPU CLI (not part of the default build)."""
+    build(verbose=verbose, targets=[asan_path()])
+    return asan_path()
+
+
+def build(verbose: bool = False, jobs: int | None = None, targets=None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
     nf = os.path.join(BUILD, "build.ninja")
@@ -110,7 +135,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         except Exception as e:  # pragma: no cover
             raise RuntimeError("ninja not found") from e
     jobs = jobs or min(8, os.cpu_count() or 4)
-    cmd = [ninja, "-C", BUILD, f"-j{jobs}"]
+    cmd = [ninja, "-C", BUILD, f"-j{jobs}"] + list(targets or [])
     if verbose:
         cmd.append("-v")
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
