@@ -772,6 +772,17 @@ __global__ __launch_bounds__(MARCH_BLOCK) void hf2d_lean_march(StepParams P, Lea
   }
 }
 
+// K8 monitors: p and Tg of the probe cells this rank owns (idx < 0: not
+// owned) gathered on the device, so an output step moves 16 bytes per probe
+// instead of the whole state.
+__global__ void hf2d_probe_gather(const long* idx, int n, const real* p, const real* T, real* out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const long c = idx[t];
+  out[2 * t] = c >= 0 ? p[c] : 0.0;
+  out[2 * t + 1] = c >= 0 ? T[c] : 0.0;
+}
+
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, LeanSoA L, SoA g, long c0, long c1) {
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   if (c >= c1) return;
@@ -1035,6 +1046,8 @@ struct DeviceSolver::Impl {
   int32_t *iw, *jw;
   SpeciesProps* species = nullptr;
   ScenarioTables* scen = nullptr;
+  long* probe_idx = nullptr;   // K8 monitor probes (sample_monitors)
+  real* probe_out = nullptr;
   DevScalars* sc = nullptr;
   DevScalars* sc_host = nullptr;   // pinned
   ResidualPack* partials = nullptr;
@@ -1416,6 +1429,49 @@ void DeviceSolver::download(Field& J) {
 }
 
 void DeviceSolver::on_cycle_roll() { time_offset = last_dev_time; }
+
+void DeviceSolver::sample_monitors(std::vector<MonitorPoint>& mp) {
+  if (mp.empty()) return;
+  flush_pending();
+  p2p_complete();
+  Impl& m = *impl;
+  const int n = (int)mp.size();
+  std::vector<long> idx(n, -1);
+  for (int q = 0; q < n; q++) {
+    const int i = (int)(mp[q].x / cs.cfg.dx), j = (int)(mp[q].y / cs.cfg.dy);
+    if (cs.J.in(i, j) && i >= gi0 && i < gi1) idx[q] = (long)(i - gi0 + l_off) * h.ny + j;
+  }
+  if ((int)probe_idx_host.size() != n) {
+    probe_idx_host.assign(n, -2);
+    probe_buf_host.assign(2 * n, 0.0);
+    impl->probe_idx = m.mem.alloc<long>(n);
+    impl->probe_out = m.mem.alloc<real>(2 * n);
+    HIP_CHECK(hipDeviceSynchronize());
+  }
+  if (idx != probe_idx_host) {
+    probe_idx_host = idx;
+    HIP_CHECK(hipMemcpyAsync(m.probe_idx, probe_idx_host.data(), n * sizeof(long), hipMemcpyHostToDevice, m.stream));
+  }
+  // current pressure: the lean arrays while they are authoritative
+  const real* p = lean_state ? m.P2[pbuf] : m.p;
+  hipLaunchKernelGGL(hf2d_probe_gather, dim3((n + 63) / 64), dim3(64), 0, m.stream, m.probe_idx, n, p, m.Tg[pbuf],
+                     m.probe_out);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(probe_buf_host.data(), m.probe_out, 2 * n * sizeof(real), hipMemcpyDeviceToHost, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  for (int q = 0; q < n; q++) {
+    real pv = probe_buf_host[2 * q], Tv = probe_buf_host[2 * q + 1];
+    const int i = (int)(mp[q].x / cs.cfg.dx), j = (int)(mp[q].y / cs.cfg.dy);
+    if (comm->size() > 1) {   // exactly one rank owns the probe
+      pv = comm->allreduce_sum(pv);
+      Tv = comm->allreduce_sum(Tv);
+    } else if (!cs.J.in(i, j)) {
+      continue;
+    }
+    mp[q].p = pv;
+    mp[q].T = Tv;
+  }
+}
 
 void DeviceSolver::poison_cell(int gi, int j) {
   flush_pending();

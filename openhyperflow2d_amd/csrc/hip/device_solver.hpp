@@ -69,6 +69,9 @@ class DeviceSolver : public SolverBase {
   void sync_scalars() override;
   void on_cycle_roll() override;
   void poison_cell(int gi, int j) override;
+  void sample_monitors(std::vector<MonitorPoint>& mp) override;
+  std::vector<long> probe_idx_host;
+  std::vector<real> probe_buf_host;
   void trace_push(const char* name) override;
   void trace_pop() override;
   double time_offset = 0.0, last_dev_time = 0.0;

@@ -47,3 +47,19 @@ def test_sigint_finishes_cycle_and_checkpoints(hf, tmp_path):
     assert (tmp_path / "Wedge15_200x60.hf2d").exists()
     meta = json.loads((tmp_path / "Wedge15_200x60.hf2d.meta").read_text())
     assert meta["iteration"] > 0
+
+
+def test_launcher_script_one_and_two_ranks(hf, tmp_path):
+    """bin/OpenHyperFLOW2D.sh <Project> [n]: the reference's launcher contract
+    (Project -> Project.dat, outputs next to the deck), n ranks via torchrun."""
+    from openhyperflow2d_amd.models import decks
+
+    (tmp_path / "W.dat").write_text(decks.wedge15(60, 20, nmax=10, nout=5))
+    sh = os.path.join(ROOT, "openhyperflow2d_amd", "bin", "OpenHyperFLOW2D.sh")
+    for n in ("1", "2"):
+        r = subprocess.run([sh, "W", n, "--backend", "cpu", "--cycles", "1", "--no-checkpoint"], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, HF2D_MASTER_PORT=str(29700 + int(n))))
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        assert "Computation finished" in r.stdout
+    assert (tmp_path / "Wedge15_60x20.plt").exists()

@@ -391,3 +391,28 @@ def test_single_gas_ns_specialisation_equals_generic(gpu, deck, mode):
     np.testing.assert_array_equal(a.summary()["rms"], b.summary()["rms"])
     for f in FIELDS + ["k", "R", "CP", "mu", "lam", "mu_t", "dUdx", "dTdy", "Diff", "S7", "S8"]:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("physics", ["euler", "ns"])
+def test_monitor_probes_device_gather(gpu, tmp_path, physics):
+    """K8: monitor probes gathered on the device (hf2d_probe_gather, 16 B per
+    probe instead of a full download) == the CPU driver's Monitors-<P>.plt."""
+    ns = physics == "ns"
+    text = decks.wedge15(200, 40, navier_stokes=ns, nmax=20, nout=5)
+    text = decks.set_key(text, "NumMonitorPoints", 3)
+    for q, (x, y) in enumerate([(0.05, 0.02), (0.15, 0.035), (0.199, 0.001)]):
+        text = decks.set_key(text, "Point-%d.X" % (q + 1), x)
+        text = decks.set_key(text, "Point-%d.Y" % (q + 1), y)
+    text = decks.set_key(text, "MonitorIndex", 1)
+    text = decks.set_key(text, "ExitMonitorValue", 1e-30)
+    out = {}
+    for be in ("gpu", "cpu"):
+        d = tmp_path / be
+        d.mkdir()
+        s = gpu.Simulation(text, be, workdir=str(d))
+        s.run(max_cycles=2, outdir=str(d), checkpoint=False, verbose=False)
+        mon = [f for f in d.iterdir() if f.name.startswith("Monitors-")]
+        assert mon, list(d.iterdir())
+        out[be] = np.loadtxt(mon[0], comments="#")
+    assert out["gpu"].shape == out["cpu"].shape and out["gpu"].shape[0] >= 4
+    np.testing.assert_allclose(out["gpu"], out["cpu"], rtol=1e-10, atol=0)
