@@ -138,7 +138,11 @@ def build(verbose: bool = False, jobs: int | None = None, targets=None) -> str:
     cmd = [ninja, "-C", BUILD, f"-j{jobs}"] + list(targets or [])
     if verbose:
         cmd.append("-v")
-    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    import fcntl
+
+    with open(os.path.join(BUILD, ".lock"), "w") as lk:   # concurrent callers (pytest -n) share one build dir
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         sys.stderr.write((r.stdout or "") + (r.stderr or ""))
         raise RuntimeError("native build failed")

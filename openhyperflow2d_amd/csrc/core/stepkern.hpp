@@ -434,14 +434,20 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   const bool active = !has_all(CT, NT_FC);
   const uint8_t gf = sin.gf ? sin.gf[idx] : (uint8_t)0xff;
   const bool axi = P.fpa.FT != 0;   // F is only read by the axisymmetric predictor
+  const bool inplace = sin.A == out.A && sin.B == out.B && sin.F == out.F;
   const bool ns = P.sm == SM_NS;    // turbulence sources live in Src[I_K], Src[I_EPS]
   c.CT = CT;
   c.TurbType = sin.TT[idx];
   for (int k = 0; k < NEQ; k++) {
     const bool ld = sk_live(MODE, k);
-    c.A[k] = ld ? sin.A[k * N + idx] : 0.0;
-    c.B[k] = ld ? sin.B[k * N + idx] : 0.0;
-    c.F[k] = (axi && ld) ? sin.F[k * N + idx] : 0.0;
+    // fill_node() rewrites A, B (and F) of the flow and species equations of
+    // every node it does not skip, so those are loaded only when the fluxes
+    // are not updated in place (fused Euler ping-pong); a skipped node keeps
+    // the stored ones (see the store below)
+    const bool fld = ld && (!inplace || k >= 4 + NCOMP);
+    c.A[k] = fld ? sin.A[k * N + idx] : 0.0;
+    c.B[k] = fld ? sin.B[k * N + idx] : 0.0;
+    c.F[k] = (axi && fld) ? sin.F[k * N + idx] : 0.0;
     c.Src[k] = (ld && ((k >= 4 + NCOMP && ns) || (gf & GF_SRC))) ? sin.Src[k * N + idx] : 0.0;
     c.SrcAdd[k] = (ld && (gf & GF_SRCADD)) ? sin.SrcAdd[k * N + idx] : 0.0;
     c.RX[k] = c.RY[k] = 0;
@@ -590,11 +596,10 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     }
   }
   // SGL: a skipped node (fill_node returned false) keeps its stored fluxes
-  const bool wflux = !SG || filled;
   for (int k = 0; k < NEQ; k++) {
     if (!sk_live(MODE, k)) continue;
     out.S[k * N + idx] = c.S[k];
-    if (wflux) {
+    if (filled || !inplace || k >= 4 + NCOMP) {
       out.A[k * N + idx] = c.A[k];
       out.B[k * N + idx] = c.B[k];
       if (axi) out.F[k * N + idx] = c.F[k];
