@@ -103,3 +103,44 @@ def test_two_strip_driver_outputs_match_single_rank(hf, tmp_path):
     r1 = (one / "RMS-Wedge15_90x30.plt").read_text().split()
     r2 = (two / "RMS-Wedge15_90x30.plt").read_text().split()
     assert len(r1) == len(r2)
+
+
+def _fault_worker(rank, world, port, text, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from openhyperflow2d_amd.parallel.dist import DistributedSimulation
+
+        sim = DistributedSimulation(text, "cpu", rank=rank, world=world, workdir=outdir)
+        try:
+            sim.run(max_cycles=3, outdir=outdir, checkpoint=True, verbose=True, fault="step:27,rank:1")
+            msg = "no error"
+        except RuntimeError as e:
+            msg = str(e)
+        with open(os.path.join(outdir, "msg%d.txt" % rank), "w") as f:
+            f.write(msg)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_fault_on_one_rank_stops_every_rank(hf, tmp_path):
+    """A NaN fault injected on rank 1 makes every rank stop with the Tg < 0
+    error (the flag is MAX-reduced), each rank writes its own
+    rank-<r>-<P>-err.plt, and the checkpoint of the last completed cycle stays."""
+    text = decks.wedge15(90, 30, nmax=20, nout=5)
+    text = decks.set_key(text, "MonitorIndex", 1)
+    text = decks.set_key(text, "ExitMonitorValue", 1e-30)
+    mp.start_processes(_fault_worker, args=(2, _free_port(), text, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    for r in (0, 1):
+        msg = (tmp_path / ("msg%d.txt" % r)).read_text()
+        assert "unstability" in msg, msg
+        assert (tmp_path / ("rank-%d-Wedge15_90x30-err.plt" % r)).exists()
+    assert "in cell (" in (tmp_path / "msg1.txt").read_text()   # the poisoned rank names the cell
+    import json
+
+    assert json.loads((tmp_path / "Wedge15_90x30.hf2d.meta").read_text())["iteration"] == 20
