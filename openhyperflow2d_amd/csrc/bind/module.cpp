@@ -193,6 +193,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_property_readonly("ny", [](const Case& c) { return c.J.ny; })
       .def_property_readonly("dt0", [](const Case& c) { return c.dt0; })
       .def_property_readonly("dx", [](const Case& c) { return c.cfg.dx; })
+      .def_property_readonly("thread_block_size", [](const Case& c) { return c.cfg.ThreadBlockSize; })
       .def_property_readonly("dy", [](const Case& c) { return c.cfg.dy; })
       .def_property_readonly("problem_type", [](const Case& c) { return c.cfg.ProblemType; })
       .def_property_readonly("flow_type", [](const Case& c) { return c.cfg.FT; })
@@ -394,6 +395,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("autotune", &DeviceSolver::autotune, py::arg("steps") = 120, py::call_guard<py::gil_scoped_release>())
       .def_readwrite("fused", &DeviceSolver::fused)
       .def_readwrite("lean", &DeviceSolver::lean)
       .def_readwrite("lean_tile", &DeviceSolver::lean_tile)

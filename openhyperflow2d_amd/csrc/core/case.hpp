@@ -51,6 +51,9 @@ struct Config {
   // new key (not in the reference): viscous time-step bound for N-S,
   // dt <= ViscousCFL * rho / ((mu + mu_t) (1/dx^2 + 1/dy^2)); 0 = off (reference)
   real ViscousCFL = 0;
+  // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
+  // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
+  int ThreadBlockSize = 0;
   Table CFL_Scenario, beta_Scenario;
   int NSaveStep = 1, Nmax = 1, NOutStep = 1;
   int isAlternateRMS = 0, isIgnoreUnsetNodes = 0, MonitorIndex = 0;

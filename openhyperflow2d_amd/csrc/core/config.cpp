@@ -25,6 +25,7 @@ void Config::load_globals(InputDeck& d) {
   CFL = d.get_float("CFL");
   CFL_Scenario = d.get_table("CFL_Scenario");
   ViscousCFL = d.get_float_or("ViscousCFL", 0.0);
+  ThreadBlockSize = d.get_int_or("ThreadBlockSize", 0);
   NSaveStep = d.get_int("NSaveStep");
   Nmax = d.get_int("Nmax");
   NOutStep = d.get_int_or("NOutStep", 1);

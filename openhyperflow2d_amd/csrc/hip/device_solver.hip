@@ -23,6 +23,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -2267,6 +2268,73 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
 void DeviceSolver::synchronize() {
   flush_pending();
   HIP_CHECK(hipStreamSynchronize(impl->stream));
+}
+
+// ThreadBlockSize = 0 ("auto-calibrate", UG p.20): time the lean tile
+// kernel's geometry choices (cells per thread, tile height) on this device
+// and strip, keep the fastest.  Every candidate computes the same bits; the
+// state (device arrays and host bookkeeping) is restored afterwards, so the
+// run is unaffected apart from its speed.  Only before the first step.
+std::string DeviceSolver::autotune(int steps) {
+  if (!lean_ok || cs.cfg.ProblemType == SM_NS || !lean_tile || nstep != 0 || iter != 0) return "";
+  flush_pending();
+  const real s_dt = dt, s_dtr = dt_running, s_cur = cur_time_part, s_gt = cs.global_time;
+  const long s_iter = iter, s_last = last_iter;
+  const int s_cycle = cycle;
+  const bool s_src = isSrcAdd, s_out = step_outputs;
+  const ResidualSummary s_res = last_res;
+  const bool s_resv = last_res_valid;
+  struct Cand {
+    int cpt, tj;
+  };
+  std::vector<Cand> cands;
+  for (int cpt : {2, 1})
+    for (int tj : {0, 16, 20, 25, 32, 40, 50, 64})
+      if (tj == 0 || tj <= h.ny) cands.push_back({cpt, tj});
+  double best = 1e30;
+  Cand win{lean_cpt, lean_tj};
+  char b[160];
+  std::string log;
+  for (const Cand& c : cands) {
+    lean_cpt = c.cpt;
+    lean_tj = c.tj;
+    graph.reset();
+    upload();
+    run_steps(12);   // first lean step + graph capture
+    synchronize();
+    double us = 1e30;
+    for (int rep = 0; rep < 2; rep++) {   // best of two: the candidates differ by a few %
+      const auto t0 = std::chrono::steady_clock::now();
+      run_steps(steps);
+      synchronize();
+      us = std::min(us, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / steps * 1e6);
+    }
+    std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
+    log += b;
+    if (us < best) {
+      best = us;
+      win = c;
+    }
+  }
+  lean_cpt = win.cpt;
+  lean_tj = win.tj;
+  graph.reset();
+  upload();
+  dt = s_dt;
+  dt_running = s_dtr;
+  cur_time_part = s_cur;
+  cs.global_time = s_gt;
+  iter = s_iter;
+  last_iter = s_last;
+  cycle = s_cycle;
+  isSrcAdd = s_src;
+  step_outputs = s_out;
+  last_res = s_res;
+  last_res_valid = s_resv;
+  upload();   // device scalars from the restored host state
+  graph_launches = 0;
+  std::snprintf(b, sizeof b, "best cpt=%d tj=%d (%.2f us/step)", win.cpt, win.tj, best);
+  return log + b;
 }
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device) {

@@ -76,6 +76,8 @@ class DeviceSolver : public SolverBase {
   void trace_pop() override;
   double time_offset = 0.0, last_dev_time = 0.0;
   void synchronize();
+  // ThreadBlockSize = 0: time the lean tile geometries, keep the fastest (before the first step)
+  std::string autotune(int steps = 120);
   void* stream() const;
 
   // Multi-GPU: RCCL communicator over the strip ranks.

@@ -13,6 +13,15 @@ from typing import Optional
 import numpy as np
 
 
+def maybe_autotune(case, solver) -> str:
+    """Deck key ThreadBlockSize = 0 (the reference's "auto-calibrate") tunes
+    the lean kernel geometry on the device before the first step
+    (DeviceSolver.autotune; results are unaffected).  HF2D_AUTOTUNE=0 skips."""
+    if case.thread_block_size != 0 or os.environ.get("HF2D_AUTOTUNE", "1") == "0":
+        return ""
+    return solver.autotune()
+
+
 def parse_fault(spec: str):
     """``step:N[,rank:R][,kind:nan|kill]`` -> (N, R, kind); "" -> (-1, 0, "nan").
 
@@ -51,6 +60,7 @@ class Simulation:
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
             self.solver.lean = True if lean is None else bool(lean)
+            self.autotune_log = maybe_autotune(self.case, self.solver)
         elif backend == "cpu":
             self.solver = hf.CpuSolver(self.case, gi0, gi1)
             self.solver.lean = False if lean is None else bool(lean)

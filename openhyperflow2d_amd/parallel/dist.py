@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ..models.simulation import parse_fault
+from ..models.simulation import maybe_autotune, parse_fault
 from .strips import balanced_columns
 
 
@@ -58,6 +58,7 @@ class DistributedSimulation:
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
             self.solver.lean = lean
+            self.autotune_log = maybe_autotune(self.case, self.solver)
             if world > 1:
                 self._wire_gpu(transport or os.environ.get("HF2D_TRANSPORT", "p2p"))
         elif backend == "cpu":

@@ -416,3 +416,21 @@ def test_monitor_probes_device_gather(gpu, tmp_path, physics):
         out[be] = np.loadtxt(mon[0], comments="#")
     assert out["gpu"].shape == out["cpu"].shape and out["gpu"].shape[0] >= 4
     np.testing.assert_allclose(out["gpu"], out["cpu"], rtol=1e-10, atol=0)
+
+
+def test_autotune_thread_block_size_zero(gpu, monkeypatch):
+    """ThreadBlockSize = 0 (reference: auto-calibrate) times the lean tile
+    geometries on the device before the first step; the run is unchanged."""
+    text = decks.wedge15(300, 60, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    assert "best cpt=" in a.autotune_log, a.autotune_log
+    monkeypatch.setenv("HF2D_AUTOTUNE", "0")
+    b = gpu.Simulation(text, "gpu")
+    assert b.autotune_log == ""
+    for n, res in [(5, True), (40, False), (7, True)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+    assert a.summary()["dt"] == b.summary()["dt"] and a.summary()["iteration"] == b.summary()["iteration"]
+    assert a.summary()["time"] == b.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
