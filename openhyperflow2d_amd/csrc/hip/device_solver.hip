@@ -2295,19 +2295,26 @@ std::string DeviceSolver::autotune(int steps) {
   Cand win{lean_cpt, lean_tj};
   char b[160];
   std::string log;
+  // same work per candidate whatever the grid (~50 M cell-steps): big grids get fewer steps
+  const long cells = std::max(1L, (long)(gi1 - gi0) * h.ny);
+  steps = (int)std::max(12L, std::min((long)steps, 50000000L / cells));
   for (const Cand& c : cands) {
     lean_cpt = c.cpt;
     lean_tj = c.tj;
-    graph.reset();
-    upload();
-    run_steps(12);   // first lean step + graph capture
-    synchronize();
+    graph.reset();   // the state just keeps marching; it is restored once at the end
     double us = 1e30;
-    for (int rep = 0; rep < 2; rep++) {   // best of two: the candidates differ by a few %
-      const auto t0 = std::chrono::steady_clock::now();
-      run_steps(steps);
+    try {
+      run_steps(12);   // (first candidate: first lean step) + graph capture
       synchronize();
-      us = std::min(us, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / steps * 1e6);
+      for (int rep = 0; rep < 2; rep++) {   // best of two: the candidates differ by a few %
+        const auto t0 = std::chrono::steady_clock::now();
+        run_steps(steps);
+        synchronize();
+        us = std::min(us, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / steps * 1e6);
+      }
+    } catch (const std::exception& e) {   // e.g. the transient went unstable: stop tuning, keep the best so far
+      log += std::string("stopped: ") + e.what() + "; ";
+      break;
     }
     std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
     log += b;
@@ -2319,7 +2326,6 @@ std::string DeviceSolver::autotune(int steps) {
   lean_cpt = win.cpt;
   lean_tj = win.tj;
   graph.reset();
-  upload();
   dt = s_dt;
   dt_running = s_dtr;
   cur_time_part = s_cur;
