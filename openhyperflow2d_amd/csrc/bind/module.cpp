@@ -234,6 +234,12 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("y_force", [](const Case& c, double x0, double y0, double dx, double dy) {
         return y_force(c, c.J, x0, y0, dx, dy);
       })
+      .def("x_force_ysym", [](const Case& c, double x0, double l, double d) {
+        return x_force_ysym(c, c.J, x0, l, d);
+      })
+      .def("mid_section_area", [](const Case& c, double x0, double y0, double dx, double dy) {
+        return mid_section_area(c, c.J, x0, y0, dx, dy);
+      })
       .def("cx", [](const Case& c, double x0, double y0, double dx, double dy, int flow) {
         return calc_cx(c, c.J, x0, y0, dx, dy, c.flows2d.at(flow - 1));
       })
@@ -275,6 +281,12 @@ PYBIND11_MODULE(_hf2d, m) {
 
   m.def("sk_eligible", [](const Case& c) { std::string w; const int md = sk_eligible(c, &w); return py::make_tuple(md, w); },
         py::arg("case"), "split-kernel specialisation (0 generic, 1 single-gas laminar, 2 single-gas turbulent; reason)");
+  m.def("smooth", [](py::array_t<double, py::array::c_style> a, int axis) {
+        if (a.ndim() != 2) throw std::runtime_error("smooth: (nx, ny) array expected");
+        auto buf = a.mutable_data();
+        if (axis == 0) smooth_x(buf, (int)a.shape(0), (int)a.shape(1));
+        else smooth_y(buf, (int)a.shape(0), (int)a.shape(1));
+      }, py::arg("a"), py::arg("axis"), "SmoothX (axis 0) / SmoothY (axis 1), in place");
   m.def("cond_names", &cond_names, py::arg("CT"), "PrintCond: names of the set CondType2D bits");
   m.def("turb_cond_names", &turb_cond_names, py::arg("TT"), "PrintTurbCond: names of the set TurbulenceCondType2D bits");
 

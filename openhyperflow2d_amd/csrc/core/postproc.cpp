@@ -195,6 +195,65 @@ real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy)
   return Fp + Fd;
 }
 
+// CalcXForceYSym2D (out_cfd_param.cpp:199-254): x force on the wall cells of
+// x in [x0, x0+l], j <= d/dy; axisymmetric areas use the cell's y (not j+0.5).
+real x_force_ysym(const Case& cs, const Field& J, real x0, real l, real d) {
+  const Config& C = cs.cfg;
+  real Fp = 0, Fd = 0;
+  const int i0 = (int)(x0 / C.dx), i1 = (int)((l + x0) / C.dx), j1 = (int)(d / C.dy);
+  for (int i = 0; i < J.nx; i++)
+    for (int j = 0; j < J.ny; j++) {
+      const CellRecord& n = J.at(i, j);
+      if (!((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && i >= i0 && i <= i1 && j <= j1)) continue;
+      const real Sp = (C.FT == FT_FLAT) ? C.dy : 2 * M_PI * n.y * C.dy;
+      const real Sd = (C.FT == FT_FLAT) ? C.dx : 2 * M_PI * n.y * C.dx;
+      if (i > 0 && J.at(i - 1, j).is(CT_SOLID))
+        Fp -= Sp * n.p;
+      else if (i < J.nx - 1 && J.at(i + 1, j).is(CT_SOLID))
+        Fp += Sp * n.p;
+      const real tau = -Sd * (n.mu + n.mu_t) * std::fabs(n.dUdy);
+      if (j < J.ny - 1 && !J.at(i, j + 1).is(CT_SOLID))
+        Fd += J.at(i, j + 1).U > 0 ? tau : -tau;
+      else if (j > 0 && !J.at(i, j - 1).is(CT_SOLID))
+        Fd += J.at(i, j - 1).U > 0 ? tau : -tau;
+    }
+  return Fp + Fd;
+}
+
+// GetFmid (out_cfd_param.cpp:391-429): frontal (mid-section) area of the wall
+// rows inside the box -- dy per row (flat) or the 2*pi*(j+0.5)*dy^2 ring.
+real mid_section_area(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  const Config& C = cs.cfg;
+  real F = 0;
+  for (int j = 0; j < J.ny; j++) {
+    bool hit = false;
+    for (int i = 0; i < J.nx; i++) {
+      const CellRecord& n = J.at(i, j);
+      if ((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy)) hit = true;
+    }
+    if (hit) F += (C.FT == FT_FLAT) ? C.dy : 2 * M_PI * (j + 0.5) * C.dy * C.dy;
+  }
+  return F;
+}
+
+// SmoothX / SmoothY (out_cfd_param.cpp:500-522): in place, in the reference's
+// j-outer / i-inner order, so a smoothed value feeds the next cell.
+void smooth_y(real* A, int nx, int ny) {
+  for (int j = 1; j < ny - 1; j++)
+    for (int i = 0; i < nx; i++) {
+      real* c = A + (size_t)i * ny;
+      if (c[j + 1] > 0. && c[j - 1] > 0.) c[j] = 0.5 * (c[j + 1] + c[j - 1]);
+    }
+}
+void smooth_x(real* A, int nx, int ny) {
+  for (int j = 0; j < ny; j++)
+    for (int i = 1; i < nx - 1; i++) {
+      real& c = A[(size_t)i * ny + j];
+      const real l = A[(size_t)(i - 1) * ny + j], r = A[(size_t)(i + 1) * ny + j];
+      if (r > 0. && l > 0.) c = 0.5 * (r + l);
+    }
+}
+
 static real wall_span_x(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
   const Config& C = cs.cfg;
   real S = 0;

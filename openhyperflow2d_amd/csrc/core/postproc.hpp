@@ -31,6 +31,10 @@ real mass_flow_rate_x(const Case& cs, const Field& J, real x0, real y0, real dy)
 real calc_area(const Case& cs, const Field& J, real x0, real y0, real dy);
 real x_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy);
 real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy);
+real x_force_ysym(const Case& cs, const Field& J, real x0, real l, real d);
+real mid_section_area(const Case& cs, const Field& J, real x0, real y0, real dx, real dy);
+void smooth_x(real* A, int nx, int ny);   // x-major (nx, ny) array, in place
+void smooth_y(real* A, int nx, int ny);
 real calc_cx(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f);
 real calc_cy(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f);
 real calc_cp(const CellRecord& n, const GasFlow& f);

@@ -6,7 +6,7 @@ The solver kernels themselves live in csrc/hip (device) and csrc/core
 total-state and schlieren fields) and derived fields for Python users.
 """
 from .postproc import (average_pressure, average_temperature, cd, cv, cx, cy, derived_field, force,
-                       mach, mass_flow_x, vorticity)
+                       mach, mass_flow_x, mid_section_area, smooth, vorticity, x_force_ysym)
 
 __all__ = ["average_pressure", "average_temperature", "cd", "cv", "cx", "cy", "derived_field", "force", "mach",
-           "mass_flow_x", "vorticity"]
+           "mass_flow_x", "mid_section_area", "smooth", "vorticity", "x_force_ysym"]

@@ -23,6 +23,26 @@ def force(sim, x0: float, y0: float, dx: float, dy: float):
     return c.x_force(x0, y0, dx, dy), c.y_force(x0, y0, dx, dy)
 
 
+def x_force_ysym(sim, x0: float, l: float, d: float) -> float:
+    """x force on the wall cells of x in [x0, x0+l] below y = d (CalcXForceYSym2D)."""
+    return _case(sim).x_force_ysym(x0, l, d)
+
+
+def mid_section_area(sim, x0, y0, dx, dy) -> float:
+    """Frontal area of the body rows inside the box (GetFmid)."""
+    return _case(sim).mid_section_area(x0, y0, dx, dy)
+
+
+def smooth(a: np.ndarray, axis: int) -> np.ndarray:
+    """SmoothX (axis=0) / SmoothY (axis=1) of an x-major (nx, ny) field: a cell
+    whose two neighbours along the axis are > 0 becomes their mean, in place in
+    the reference's sweep order.  Returns a smoothed copy."""
+    from .. import native
+    out = np.ascontiguousarray(a, dtype=np.float64).copy()
+    native().smooth(out, int(axis))
+    return out
+
+
 def cx(sim, x0, y0, dx, dy, flow: int = 1) -> float:
     """Drag coefficient against Flow2D-<flow> (Calc_Cx_2D)."""
     return _case(sim).cx(x0, y0, dx, dy, flow)

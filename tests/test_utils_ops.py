@@ -40,3 +40,63 @@ def test_ops(hf):
     assert w.shape == p.shape and np.isfinite(w).all()
     fx, fy = ops.force(s, 0.0, 0.0, 0.12, 0.04)
     assert np.isfinite(fx) and np.isfinite(fy)
+
+
+def _wall_mask(rec):
+    from openhyperflow2d_amd.utils import RECORD_DTYPE  # noqa: F401
+    CT = rec["CT"].astype(np.uint64)
+    wall = ((CT & np.uint64(0x4000000)) == np.uint64(0x4000000)) | ((CT & np.uint64(0x8000000)) == np.uint64(0x8000000))
+    solid = (CT & np.uint64(0x40000000)) == np.uint64(0x40000000)
+    return wall, solid
+
+
+def test_ops_ysym_fmid_smooth(hf):
+    """CalcXForceYSym2D, GetFmid and SmoothX/SmoothY (out_cfd_param.cpp:199-254,
+    391-429, 500-522) against literal numpy/Python loops over the records."""
+    from openhyperflow2d_amd import ops
+    from openhyperflow2d_amd.utils import RECORD_DTYPE
+
+    nx, ny = 120, 40
+    s = hf.Simulation(decks.wedge15(nx, ny, nmax=100, nout=50), "cpu")
+    s.step(40)
+    dx = dy = 1e-3
+    x0, l, d = 0.02, 0.08, 0.03
+    got = ops.x_force_ysym(s, x0, l, d)
+    rec = np.frombuffer(s.records(), dtype=RECORD_DTYPE).reshape(nx, ny)
+    wall, solid = _wall_mask(rec)
+    assert wall.any()
+    Fp = Fd = 0.0
+    for i in range(nx):
+        for j in range(ny):
+            if not (wall[i, j] and int(x0 / dx) <= i <= int((l + x0) / dx) and j <= int(d / dy)):
+                continue
+            n = rec[i, j]
+            if i > 0 and solid[i - 1, j]:
+                Fp -= dy * n["p"]
+            elif i < nx - 1 and solid[i + 1, j]:
+                Fp += dy * n["p"]
+            tau = -dx * (n["mu"] + n["mu_t"]) * abs(n["dUdy"])
+            if j < ny - 1 and not solid[i, j + 1]:
+                Fd += tau if rec[i, j + 1]["U"] > 0 else -tau
+            elif j > 0 and not solid[i, j - 1]:
+                Fd += tau if rec[i, j - 1]["U"] > 0 else -tau
+    assert got == Fp + Fd
+    assert got != 0.0
+
+    box = (0.0, 0.0, 0.12, 0.04)
+    rows = {j for i in range(nx) for j in range(ny)
+            if wall[i, j] and int(box[0] / dx) <= i <= int((box[0] + box[2]) / dx)
+            and int(box[1] / dy) <= j <= int((box[1] + box[3]) / dy)}
+    assert abs(ops.mid_section_area(s, *box) - len(rows) * dy) < 1e-15
+
+    rng = np.random.default_rng(3)
+    a = rng.standard_normal((9, 7))
+    for axis in (0, 1):
+        ref = a.copy()
+        for j in range(7):
+            for i in range(9):
+                if axis == 1 and 0 < j < 6 and ref[i, j + 1] > 0 and ref[i, j - 1] > 0:
+                    ref[i, j] = 0.5 * (ref[i, j + 1] + ref[i, j - 1])
+                if axis == 0 and 0 < i < 8 and ref[i + 1, j] > 0 and ref[i - 1, j] > 0:
+                    ref[i, j] = 0.5 * (ref[i + 1, j] + ref[i - 1, j])
+        np.testing.assert_array_equal(ops.smooth(a, axis), ref)
