@@ -314,18 +314,29 @@ __device__ inline double p2p_load(const double* p) {
 }
 
 // Multi-GPU exchange fused into the lean tile kernel (xGMI mailboxes, see
-// hf2d_p2p_xchg for the layout and the parity argument).  Step n of a rank:
-//   start  one thread per workgroup waits (bounded) until every peer has
-//          published sequence s-1; the global dt is MIN(local slot, the
-//          peers' dt of s-1); tiles at the strip edges stage their ghost
-//          column straight from the mailbox of parity s-1;
+// hf2d_p2p_xchg for the layout and the parity argument).  Step s of a rank:
+//   start  the dt slot already holds the global MIN (folded by the previous
+//          kernel's last workgroup); tiles at the strip edges stage their
+//          ghost column straight from the mailbox of parity s-1;
 //   end    cells of the first / last owned column store their new lean
-//          state into the neighbour's mailbox of parity s; the last
-//          workgroup to finish (completion counter) sends this rank's local
-//          dt MIN to every peer and releases flag s at system scope.
-// No exchange kernel, no pack/unpack pass, no host involvement: one kernel
-// per step.  Ghost columns of the state arrays are only refreshed by
+//          state into the neighbour's mailbox of parity s with
+//          system-coherent stores and wait for their completion (vmcnt);
+//          the last workgroup to finish (completion counter) sends this
+//          rank's local dt MIN to every peer, publishes flag s, waits
+//          (bounded) for the peers' flag s and folds their dt into the slot.
+// One kernel per step and a single waiting workgroup, at the tail: no
+// exchange kernel, no pack/unpack pass, no host involvement, and no
+// system-scope fence (L2 writeback / invalidate) in the other workgroups.
+// Ghost columns of the state arrays are only refreshed by
 // hf2d_p2p_complete, which the host runs before any other consumer.
+__device__ inline void p2p_store(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// outstanding vector-memory operations of this wave (stores included on gfx9)
+// have completed: the ordering point for the relaxed system-coherent stores
+__device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 struct FusedX {
   real* peer_recv_l;   // left neighbour's mailbox recv base (we are its right side)
   real* peer_recv_r;
@@ -366,27 +377,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   extern __shared__ real lds[];
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   unsigned long long seq_prev = 0;
-  if (FX) {
-    __shared__ double s_dt;
-    seq_prev = *X.seq;
-    if (threadIdx.x == 0) {
-      double d = bits_to_d(sc->dt_bits[slot]);
-      if (seq_prev > 0 && p2p_wait_all(X, seq_prev, sc)) {
-        const int pp = (int)(seq_prev & 1);
-        for (int q = 0; q < X.nranks; q++)
-          if (q != X.rank) d = fmin(d, p2p_load(X.my_dtr + pp * X.nranks + q));
-      }
-      s_dt = d;
-      if (b == 0) sc->dt_bits[slot] = d_to_bits(d);   // global MIN (idempotent for racing readers)
-    }
-    __syncthreads();
-    apply_dt(P, sc, slot);
-    P.dt = s_dt;
-    P.dtdx = s_dt / P.dx;
-    P.dtdy = s_dt / P.dy;
-  } else {
-    apply_dt(P, sc, slot);
-  }
+  if (FX) seq_prev = *X.seq;
+  apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
@@ -467,8 +459,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
           v[NF - 2] = L.Vout[g];
           v[NF - 1] = L.Pout[g];
 #pragma unroll
-          for (int f = 0; f < NF; f++) mb[(long)f * P.ny + j[q]] = v[f];
-          __threadfence_system();
+          for (int f = 0; f < NF; f++) p2p_store(mb + (long)f * P.ny + j[q], v[f]);
+          vm_drain();
         }
       }
     }
@@ -489,19 +481,35 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     if (serial) m = fmin(m, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
     if (FX) {
-      const unsigned prev = __hip_atomic_fetch_add(X.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {   // last workgroup: publish this rank's step
-        *X.done = 0;
+      // the barrier above drained every wave's mailbox stores; drain the
+      // dt atomic before counting this workgroup as done
+      vm_drain();
+      const unsigned prev = __hip_atomic_fetch_add(X.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {   // last workgroup: publish this rank's step, then fold the peers'
+        __hip_atomic_store(X.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long sn = seq_prev + 1;
         const int pn = (int)(sn & 1);
-        const double dl = bits_to_d(__hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_ACQUIRE,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
+        double d = bits_to_d(__hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         for (int q = 0; q < X.nranks; q++)
-          if (q != X.rank) X.peer_dtr[q][pn * X.nranks + X.rank] = dl;
-        __threadfence_system();
+          if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
+        vm_drain();
         for (int q = 0; q < X.nranks; q++)
-          if (q != X.rank)
-            __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bool ok = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
+        for (int q = 0; q < X.nranks && ok; q++) {
+          if (q == X.rank) continue;
+          long spins = 0;
+          while (__hip_atomic_load(&X.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sn) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > P2P_SPIN_LIMIT) {
+              atomicOr(&sc->neg_T, 2);
+              ok = false;
+              break;
+            }
+          }
+          if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
+        }
+        __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *X.seq = sn;
       }
     }

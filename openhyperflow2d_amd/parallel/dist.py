@@ -119,11 +119,12 @@ class DistributedSimulation:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 1:
             self.transport = "p2p"
-            # HF2D_P2P_FUSE=1 folds the exchange into the lean tile kernel; off
-            # by default: on the one-GPU proxy (tools/p2p_probe.py --tail) the
-            # fused step cost more than tile kernel + exchange kernel
-            # (profiles/p2p_fused_virtual2_kernels.md)
-            s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "0") == "1"
+            # the exchange is folded into the lean tile kernel (one kernel per
+            # step, the last workgroup publishes and waits); HF2D_P2P_FUSE=0
+            # selects tile kernel + hf2d_p2p_xchg.  One-GPU proxy
+            # (tools/p2p_probe.py --tail): 18.6 vs 21.7 us/step for a 250-column
+            # strip (profiles/p2p_fused_virtual2_kernels.md)
+            s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "1") == "1"
         else:
             s.p2p_active = False
             if not nccl:

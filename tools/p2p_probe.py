@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--tail", type=int, default=0,
                     help="2 ranks, the last one owning only this many columns: its kernel barely competes for "
                          "the shared GPU, so us/step ~ rank 0's kernel + its exchange overhead")
+    ap.add_argument("--autotune", action="store_true", help="DeviceSolver.autotune() on every strip first")
     a = ap.parse_args()
     import openhyperflow2d_amd as hf
     from openhyperflow2d_amd.models import decks
@@ -45,6 +46,8 @@ def main():
     for r, (lo, hi) in enumerate(parts):
         s = nat.DeviceSolver(cases[r], 0, lo, hi)
         s.init_local(group, r)
+        if a.autotune:
+            print("rank %d autotune: %s" % (r, s.autotune().strip().splitlines()[-1]), flush=True)
         solvers.append(s)
     descs = [s.p2p_export(r, a.ranks) for r, s in enumerate(solvers)]
     for s in solvers:
