@@ -874,10 +874,16 @@ __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* 
 //   recv[2][2][cap] f64  halo columns for parity 0/1 from the left/right
 // One single-workgroup kernel per exchange replaces pack + RCCL group +
 // unpack: it stores this rank's boundary columns straight into the
-// neighbours' mailboxes and its dt into every peer's, releases its flag at
-// system scope, waits (bounded) for every peer's flag of the same sequence
-// number, then unpacks its own mailbox into the ghost columns and folds the
-// MIN of all dt into the next dt slot -- bitwise the RCCL path's result.
+// neighbours' mailboxes and its dt into every peer's, publishes its flag,
+// waits (bounded) for every peer's flag of the same sequence number, then
+// unpacks its own mailbox into the ghost columns and folds the MIN of all dt
+// into the next dt slot -- bitwise the RCCL path's result.
+// Ordering without system-scope fences: mailbox data and flags are written
+// with system-coherent stores (p2p_store: they bypass the non-coherent L2),
+// and a wave's stores are complete (s_waitcnt vmcnt(0)) before any flag is
+// stored; a reader issues its system-coherent data loads only after it has
+// seen the flag.  A __threadfence_system() would also write back the whole
+// L2 of the XCD (buffer_wbl2), which cost ~3 us per step in the fused kernel.
 // Parity double buffering is safe without a second handshake: a peer writes
 // parity p again only at sequence s+2, after it has seen this rank's flag
 // s+1, which is published after the unpack of s.  The sequence counter lives
@@ -912,24 +918,26 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
     real* dst = a.peer_recv_l + ((long)par * 2 + 1) * a.cap;   // left neighbour receives "from right"
     for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
       const int f = t / ny, j = t - f * ny;
-      dst[t] = a.L.f[f][(long)a.first * ny + j];
+      p2p_store(dst + t, a.L.f[f][(long)a.first * ny + j]);
     }
   }
   if (a.sides & 2) {
     real* dst = a.peer_recv_r + ((long)par * 2) * a.cap;       // right neighbour receives "from left"
     for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
       const int f = t / ny, j = t - f * ny;
-      dst[t] = a.L.f[f][(long)a.last * ny + j];
+      p2p_store(dst + t, a.L.f[f][(long)a.last * ny + j]);
     }
   }
   const double mydt = bits_to_d(a.sc->dt_bits[a.dslot]);
   for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
-    if (q != a.rank) a.peer_dtr[q][par * a.nranks + a.rank] = mydt;
-  __threadfence_system();
+    if (q != a.rank) p2p_store(a.peer_dtr[q] + par * a.nranks + a.rank, mydt);
+  // system-coherent stores drained (vmcnt) in every wave before the flag:
+  // no L2 writeback needed, nothing of this kernel sits dirty in the L2
+  vm_drain();
   __syncthreads();
   // 2. publish, 3. wait for every peer's publication of the same sequence
   for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
-    if (q != a.rank) __hip_atomic_store(&a.peer_flags[q][a.rank], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (q != a.rank) __hip_atomic_store(&a.peer_flags[q][a.rank], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const bool failed = __hip_atomic_load(&a.sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2;
   __shared__ double s_dt[P2P_THREADS];
   double dmin = mydt;   // each polling thread folds the dt of the peers it waited for
@@ -937,7 +945,7 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
     if (q == a.rank || failed) continue;   // after one timeout, stop waiting (the host reports it)
     long spins = 0;
     bool ok = true;
-    while (__hip_atomic_load(&a.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    while (__hip_atomic_load(&a.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > P2P_SPIN_LIMIT) {
         atomicOr(&a.sc->neg_T, 2);
