@@ -408,12 +408,16 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("autotune", &DeviceSolver::autotune, py::arg("steps") = 120, py::call_guard<py::gil_scoped_release>())
+      .def("trace_tile", &DeviceSolver::trace_tile, py::arg("steps") = 20,
+           "one phase-traced lean tile step: per workgroup [entry, staged, wave0 computed, reduced, dt atomic done "
+           "(s_memrealtime, 100 MHz), HW_ID, XCC_ID, blockIdx]")
       .def_readwrite("fused", &DeviceSolver::fused)
       .def_readwrite("lean", &DeviceSolver::lean)
       .def_readwrite("lean_tile", &DeviceSolver::lean_tile)
       .def_readwrite("lean_sg", &DeviceSolver::lean_sg)
       .def_readwrite("lean_tj", &DeviceSolver::lean_tj)
       .def_readwrite("lean_occ", &DeviceSolver::lean_occ)
+      .def_readwrite("lean_wgcu", &DeviceSolver::lean_wgcu)
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)

@@ -370,11 +370,21 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
 }
 
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
-template <bool RES, bool OUT, bool SG, int CPT, bool FX = false>
+// In-kernel phase trace (TR): thread 0 of every workgroup records the
+// 100 MHz s_memrealtime clock at entry, after the LDS staging barrier, when
+// its own wave finished computing, after the block dt reduction barrier and
+// after the dt atomic, plus the HW_ID / XCC_ID registers (DeviceSolver::trace_tile).
+constexpr int TILE_TRACE_WORDS = 8;
+constexpr int LDS_PER_CU = 160 * 1024;
+__device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <bool RES, bool OUT, bool SG, int CPT, bool FX = false, bool TR = false>
 __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, const LeanTile& T, DevScalars* sc,
                                                int slot, int slot_next, int serial, ResidualPack* partials,
-                                               const FusedX& X = FusedX{}) {
+                                               const FusedX& X = FusedX{}, unsigned long long* trace = nullptr) {
   extern __shared__ real lds[];
+  unsigned long long tr[5];
+  if (TR) tr[0] = rt_clock();
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
@@ -428,6 +438,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     }
   }
   __syncthreads();
+  if (TR) tr[1] = rt_clock();
   ResidualPack r;
   if (RES) {
     residual_reset(r);
@@ -465,6 +476,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       }
     }
   }
+  if (TR) tr[2] = rt_clock();
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
@@ -475,11 +487,22 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
   if (neg) atomicOr(&sc->neg_T, 1);
   __syncthreads();
+  if (TR) tr[3] = rt_clock();
   if (threadIdx.x == 0) {
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    if (TR) {
+      vm_drain();
+      tr[4] = rt_clock();
+      unsigned long long* o = trace + (long)b * TILE_TRACE_WORDS;
+#pragma unroll
+      for (int q = 0; q < 5; q++) o[q] = tr[q];
+      o[5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave/SIMD/CU/SE
+      o[6] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+      o[7] = blockIdx.x;
+    }
     if (FX) {
       // the barrier above drained every wave's mailbox stores; drain the
       // dt atomic before counting this workgroup as done
@@ -523,6 +546,14 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L,
                                                          int slot, int slot_next, int serial,
                                                          ResidualPack* partials) {
   lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
+}
+
+// Phase-traced plain step (profiling only, DeviceSolver::trace_tile).
+template <bool SG, int CPT>
+__global__ __launch_bounds__(BLOCK) void hf2d_lean_tile_tr(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                            int slot, int slot_next, int serial,
+                                                            ResidualPack* partials, unsigned long long* trace) {
+  lean_tile_body<false, false, SG, CPT, false, true>(P, L, T, sc, slot, slot_next, serial, partials, FusedX{}, trace);
 }
 
 // Same step with the multi-GPU exchange fused in (FusedX).
@@ -1976,11 +2007,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
   const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok));
+                                       lean_cpt, lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok));
   bool same = true;
   for (const StepParams& p : pending)
     same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok)) == sig;
+                                   lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok)) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -2121,14 +2152,19 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, cpt);
     const unsigned ntile = (unsigned)(T.nbi * T.nbj);
     const bool sg = lean_sg && lean_sg_ok;
-    const size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
+    size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
+    if (lean_wgcu > 0)   // cap the resident workgroups per CU through the LDS request (160 KB per CU)
+      shmem = std::max(shmem, (size_t)((LDS_PER_CU / lean_wgcu - 1024) & ~255));
     const bool out = step_outputs || want_res;
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
 #define HF2D_LEAN_TILE(R, O, G, C)                                                                                 \
   do {                                                                                                               \
-    if (fx_step)                                                                                                     \
+    if (tile_trace && !R && !O && !fx_step)                                                                          \
+      hipLaunchKernelGGL((hf2d_lean_tile_tr<G, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,       \
+                         slot_next, serial, m.partials, tile_trace);                                                 \
+    else if (fx_step)                                                                                                \
       hipLaunchKernelGGL((hf2d_lean_tile_fx<R, O, G, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
                          slot_next, serial, m.partials, X);                                                          \
     else                                                                                                             \
@@ -2148,7 +2184,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
         HF2D_LEAN_TILE(true, true, true, 1);
       else if (out)
         HF2D_LEAN_TILE(false, true, true, 1);
-      else if (lean_occ == 6 && !fx_step)
+      else if (lean_occ == 6 && !fx_step && !tile_trace)
         hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                            m.sc, slot, slot_next, serial, m.partials);
       else
@@ -2291,6 +2327,35 @@ void DeviceSolver::synchronize() {
 // and strip, keep the fastest.  Every candidate computes the same bits; the
 // state (device arrays and host bookkeeping) is restored afterwards, so the
 // run is unaffected apart from its speed.  Only before the first step.
+// One traced lean tile step (after `steps` untraced ones): per workgroup the
+// phase clocks of lean_tile_body<TR> (TILE_TRACE_WORDS words each, tile order).
+std::vector<unsigned long long> DeviceSolver::trace_tile(int steps) {
+  if (!lean_ok || cs.cfg.ProblemType == SM_NS || !lean_tile) throw std::runtime_error("trace_tile: lean tile steps only");
+  flush_pending();
+  const bool g = use_graph;
+  use_graph = false;
+  if (steps > 0) run_steps(steps);
+  const int cpt = lean_cpt == 2 ? 2 : 1;
+  const LeanTile T = lean_tile_geom(gi1 - gi0, h.ny, BLOCK, lean_tj, cpt);
+  const long n = (long)T.nbi * T.nbj * TILE_TRACE_WORDS * 2;   // room for either cpt
+  tile_trace = impl->mem.alloc<unsigned long long>(n);
+  try {
+    run_steps(2);   // the last step of run_steps stores the output fields (not traced)
+    synchronize();
+  } catch (...) {
+    tile_trace = nullptr;
+    use_graph = g;
+    throw;
+  }
+  std::vector<unsigned long long> out(n);
+  HIP_CHECK(hipMemcpy(out.data(), tile_trace, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  tile_trace = nullptr;
+  use_graph = g;
+  while (!out.empty() && out.back() == 0) out.pop_back();
+  out.resize((out.size() + TILE_TRACE_WORDS - 1) / TILE_TRACE_WORDS * TILE_TRACE_WORDS);
+  return out;
+}
+
 std::string DeviceSolver::autotune(int steps) {
   if (!lean_ok || cs.cfg.ProblemType == SM_NS || !lean_tile || nstep != 0 || iter != 0) return "";
   flush_pending();

@@ -78,6 +78,8 @@ class DeviceSolver : public SolverBase {
   void synchronize();
   // ThreadBlockSize = 0: time the lean tile geometries, keep the fastest (before the first step)
   std::string autotune(int steps = 120);
+  std::vector<unsigned long long> trace_tile(int steps = 20);
+  unsigned long long* tile_trace = nullptr;   // set only inside trace_tile
   void* stream() const;
 
   // Multi-GPU: RCCL communicator over the strip ranks.
@@ -114,6 +116,7 @@ class DeviceSolver : public SolverBase {
   bool lean_plain = false; // flag-free predictor fast path (measured slower: off)
   bool lean_sg = true;     // single-gas specialisation (lean_euler.hpp) if eligible
   int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
+  int lean_wgcu = 0;       // >0: at most this many tile workgroups resident per CU (LDS request)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
   int lean_cpt = 2;
   int lean_march = 0;
