@@ -11,6 +11,7 @@
 #include "../core/checkpoint.hpp"
 #include "../core/postproc.hpp"
 #include "../core/solver.hpp"
+#include "../hip/chem_mech.hpp"
 #include "../hip/device_solver.hpp"
 
 namespace py = pybind11;
@@ -122,6 +123,31 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
+  // K12 MFMA mechanism chemistry (csrc/hip/chem_mech.hip); rhoY is [ns][ncell], updated in place.
+  m.def(
+      "chem_mech_run",
+      [](py::array_t<double, py::array::c_style | py::array::forcecast> nmat,
+         py::array_t<double, py::array::c_style | py::array::forcecast> arr,
+         py::array_t<int, py::array::c_style | py::array::forcecast> rsp,
+         py::array_t<int, py::array::c_style | py::array::forcecast> rord,
+         py::array_t<double, py::array::c_style | py::array::forcecast> W, py::array_t<double, py::array::c_style> rhoY,
+         py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub, int repeats) {
+        const int ns = (int)W.size(), R = (int)(arr.size() / 3);
+        const int ncell = (int)T.size();
+        if (nmat.size() != (py::ssize_t)16 * R || rsp.size() != (py::ssize_t)3 * R || rord.size() != (py::ssize_t)3 * R ||
+            rhoY.size() != (py::ssize_t)ns * ncell)
+          throw std::runtime_error("chem_mech_run: inconsistent array sizes");
+        double ms;
+        {
+          py::gil_scoped_release nogil;
+          ms = chem_mech_run_host(nmat.data(), arr.data(), rsp.data(), rord.data(), W.data(), ns, R,
+                                  rhoY.mutable_data(), T.data(), ncell, dt, nsub, repeats);
+        }
+        return ms;
+      },
+      py::arg("nmat"), py::arg("arr"), py::arg("rsp"), py::arg("rord"), py::arg("W"), py::arg("rhoY"), py::arg("T"),
+      py::arg("dt"), py::arg("nsub") = 1, py::arg("repeats") = 1);
+  m.attr("CHEM_MECH_MAX_REACTIONS") = chem_mech_max_reactions();
   m.def("request_stop", &request_stop, "ask a running driver to finish the cycle, write outputs and return");
   m.def("stop_requested", &stop_requested);
   m.def("clear_stop", &clear_stop);

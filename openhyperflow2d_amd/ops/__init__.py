@@ -5,8 +5,9 @@ The solver kernels themselves live in csrc/hip (device) and csrc/core
 (libOutCFD/out_cfd_param.cpp: integral forces and coefficients, mass flow,
 total-state and schlieren fields) and derived fields for Python users.
 """
+from . import chemistry
 from .postproc import (average_pressure, average_temperature, cd, cv, cx, cy, derived_field, force,
                        mach, mass_flow_x, mid_section_area, smooth, vorticity, x_force_ysym)
 
-__all__ = ["average_pressure", "average_temperature", "cd", "cv", "cx", "cy", "derived_field", "force", "mach",
+__all__ = ["chemistry", "average_pressure", "average_temperature", "cd", "cv", "cx", "cy", "derived_field", "force", "mach",
            "mass_flow_x", "mid_section_area", "smooth", "vorticity", "x_force_ysym"]
