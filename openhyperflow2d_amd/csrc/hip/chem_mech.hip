@@ -15,7 +15,8 @@
 //   * rates   Omega(16 species x 16 cells) = N(16 x R) . Q(R x 16 cells)   R/4 MFMAs
 //   * Jacobian J_c(16 x 16)                = N(16 x R) . D_c(R x 16)       R/4 MFMAs per cell
 // and the 16x16 systems are solved by Gauss-Jordan with partial pivoting, 16 lanes
-// per cell (lane = row), 4 cells at a time, rows staged in LDS.
+// per cell (lane = row, held in registers), 4 cells at a time, staged through LDS.
+// The 4 Jacobians of a round are independent MFMA chains (latency hiding).
 //
 // f64 MFMA operand maps (cdna_hip_programming.md): A[row=l&15][k=l>>4],
 // B[k=l>>4][col=l&15], C/D col=l&15, row=(l>>4)+4*i.
@@ -32,13 +33,13 @@ namespace {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TILE = 16;     // cells per wavefront (MFMA N dimension)
-constexpr int MAXR = 64;     // reactions (kf table in LDS)
+constexpr int MAXR = 64;     // reactions per mechanism
 constexpr int LD = 18;       // row stride of the staged systems (16 cols + rhs + pad)
 
-__device__ __forceinline__ double ipow(double x, int o) {
-  double p = 1.0;
-  for (int t = 0; t < o; t++) p *= x;
-  return p;
+// x^o for o in 0..3 without branches
+__device__ __forceinline__ double pw3(double x, int o) {
+  const double x2 = x * x;
+  return o == 0 ? 1.0 : (o == 1 ? x : (o == 2 ? x2 : x2 * x));
 }
 
 __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ nmat,   // [16][R]
@@ -49,15 +50,21 @@ __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ 
                                                      int ns, int R, int ncell, double* __restrict__ rhoY,
                                                      const double* __restrict__ T, double dt, int nsub) {
   __shared__ double c_s[TILE][TILE + 1];        // [cell][species]
-  __shared__ double kf_s[TILE][MAXR + 1];       // [cell][reaction]
   __shared__ double m_s[4][TILE][LD];           // 4 systems in flight: [cell][row][col | rhs]
-  __shared__ int piv_s[4][TILE];
+  __shared__ double x_s[4][TILE];
+  __shared__ int rx_s[MAXR];                    // packed reactants: 3 x (species 4 bits, order 2 bits)
+  extern __shared__ double kf_dyn[];            // [cell][R + 1] rate constants (sized per mechanism)
 
   const int l = threadIdx.x, col = l & 15, quad = l >> 4;
   const int cell0 = blockIdx.x * TILE;
   const int mycell = cell0 + col;
   const bool live = mycell < ncell;
 
+  for (int r = l; r < R; r += 64) {
+    int pk = 0;
+    for (int t = 0; t < 3; t++) pk |= (rsp[r * 3 + t] | (rord[r * 3 + t] << 4)) << (6 * t);
+    rx_s[r] = pk;
+  }
   for (int i = 0; i < 4; i++) {
     const int s = quad + 4 * i;
     c_s[col][s] = (live && s < ns) ? rhoY[(size_t)s * ncell + mycell] / W[s] : 0.0;
@@ -65,81 +72,98 @@ __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ 
   {
     const double Tc = live ? T[mycell] : 300.0;
     const double lnT = log(Tc), rT = 1.0 / Tc;
-    for (int r = quad; r < R; r += 4) kf_s[col][r] = arr[r] * exp(arr[R + r] * lnT - arr[2 * R + r] * rT);
+    for (int r = quad; r < R; r += 4) kf_dyn[col * (R + 1) + r] = arr[r] * exp(arr[R + r] * lnT - arr[2 * R + r] * rT);
   }
   const double h = dt / nsub;
 
   for (int sub = 0; sub < nsub; sub++) {
     __syncthreads();
-    // Omega[s][cell] = sum_r N[s][r] q[r][cell]
+    // Omega[s][cell] = sum_r N[s][r] q[r][cell]; lane (quad, col): Omega[quad + 4 i][col]
     d4 om = {0.0, 0.0, 0.0, 0.0};
     for (int r0 = 0; r0 < R; r0 += 4) {
-      const int r = r0 + quad;
-      double q = kf_s[col][r];
+      const int r = r0 + quad, pk = rx_s[r];
+      double q = kf_dyn[col * (R + 1) + r];
 #pragma unroll
-      for (int t = 0; t < 3; t++) q *= ipow(c_s[col][rsp[r * 3 + t]], rord[r * 3 + t]);
+      for (int t = 0; t < 3; t++) q *= pw3(c_s[col][(pk >> (6 * t)) & 15], (pk >> (6 * t + 4)) & 3);
       om = __builtin_amdgcn_mfma_f64_16x16x4f64(nmat[col * R + r], q, om, 0, 0, 0);
     }
-    for (int g = 0; g < 4; g++) {
-      for (int qq = 0; qq < 4; qq++) {
-        const int cc = 4 * g + qq;
-        // D_cc[r][j = col]
-        d4 jac = {0.0, 0.0, 0.0, 0.0};
-        for (int r0 = 0; r0 < R; r0 += 4) {
-          const int r = r0 + quad;
-          double d = kf_s[cc][r];
-          bool hit = false;
 #pragma unroll
-          for (int t = 0; t < 3; t++) {
-            const int sp = rsp[r * 3 + t], o = rord[r * 3 + t];
-            const double cv = c_s[cc][sp];
-            if (sp == col && o > 0) {
-              d *= o * ipow(cv, o - 1);
-              hit = true;
-            } else {
-              d *= ipow(cv, o);
-            }
-          }
-          jac = __builtin_amdgcn_mfma_f64_16x16x4f64(nmat[col * R + r], hit ? d : 0.0, jac, 0, 0, 0);
-        }
-        for (int i = 0; i < 4; i++) {
-          const int s = quad + 4 * i;
-          m_s[qq][s][col] = (s == col ? 1.0 : 0.0) - h * jac[i];
+    for (int g = 0; g < 4; g++) {
+      // Jacobians of cells 4g..4g+3 as 4 independent MFMA chains:
+      // J_cc = N D_cc, B operand D_cc[r = r0 + quad][j = col].
+      d4 jac[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; qq++) jac[qq] = d4{0.0, 0.0, 0.0, 0.0};
+      for (int r0 = 0; r0 < R; r0 += 4) {
+        const int r = r0 + quad, pk = rx_s[r];
+        const double nv = nmat[col * R + r];
+        const int s0 = pk & 15, o0 = (pk >> 4) & 3, s1 = (pk >> 6) & 15, o1 = (pk >> 10) & 3, s2 = (pk >> 12) & 15,
+                  o2 = (pk >> 16) & 3;
+        const bool h0 = s0 == col && o0 > 0, h1 = s1 == col && o1 > 0, h2 = s2 == col && o2 > 0;
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+          const int cc = 4 * g + qq;
+          const double c0 = c_s[cc][s0], c1 = c_s[cc][s1], c2 = c_s[cc][s2];
+          const double p0 = pw3(c0, o0), p1 = pw3(c1, o1), p2 = pw3(c2, o2);
+          const double kf = kf_dyn[cc * (R + 1) + r];
+          double d = 0.0;
+          if (h0) d = kf * (o0 * pw3(c0, o0 - 1)) * p1 * p2;
+          if (h1) d = kf * p0 * (o1 * pw3(c1, o1 - 1)) * p2;
+          if (h2) d = kf * p0 * p1 * (o2 * pw3(c2, o2 - 1));
+          jac[qq] = __builtin_amdgcn_mfma_f64_16x16x4f64(nv, d, jac[qq], 0, 0, 0);
         }
       }
+#pragma unroll
+      for (int qq = 0; qq < 4; qq++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int s = quad + 4 * i;
+          m_s[qq][s][col] = (s == col ? 1.0 : 0.0) - h * jac[qq][i];
+        }
       if ((col >> 2) == g)
         for (int i = 0; i < 4; i++) m_s[col & 3][quad + 4 * i][TILE] = h * om[i];
       __syncthreads();
+      double row[TILE + 1];
+#pragma unroll
+      for (int j = 0; j <= TILE; j++) row[j] = m_s[quad][col][j];
 
-      // Gauss-Jordan, group `quad` solves cell 4g+quad, lane `col` owns row col.
-      double* M = &m_s[quad][0][0];
+      // Gauss-Jordan, group `quad` solves cell 4g+quad; lane `col` holds row col in
+      // registers (k, j unrolled), the pivot row is read with in-group shuffles.
       bool used = false;
+      int kk = 0;
+      double diag = 1.0;
+#pragma unroll
       for (int k = 0; k < TILE; k++) {
-        double v = used ? -1.0 : fabs(M[col * LD + k]);
+        double v = used ? -1.0 : fabs(row[k]);
         int idx = col;
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
-          const double ov = __shfl_xor(v, off);
-          const int oi = __shfl_xor(idx, off);
+          const double ov = __shfl_xor(v, off, 16);
+          const int oi = __shfl_xor(idx, off, 16);
           if (ov > v || (ov == v && oi < idx)) {
             v = ov;
             idx = oi;
           }
         }
         const int p = idx;
-        if (col == p) used = true;
-        if (col == 0) piv_s[quad][k] = p;
-        if (col != p) {
-          const double f = M[col * LD + k] / M[p * LD + k];
-          for (int j = k; j <= TILE; j++) M[col * LD + j] -= f * M[p * LD + j];
+        const double pk = __shfl(row[k], p, 16);
+        const bool me = col == p;
+        const double f = me ? 0.0 : row[k] / pk;
+        if (me) {
+          used = true;
+          kk = k;
+          diag = row[k];
+        } else {
+          row[k] = 0.0;
         }
-        __syncthreads();
+#pragma unroll
+        for (int j = k + 1; j <= TILE; j++) row[j] -= f * __shfl(row[j], p, 16);
       }
+      x_s[quad][kk] = row[TILE] / diag;
+      __syncthreads();
       {
-        const int p = piv_s[quad][col];
-        const double dx = M[p * LD + TILE] / M[p * LD + col];
         const int cc = 4 * g + quad;
-        if (col < ns) c_s[cc][col] = fmax(c_s[cc][col] + dx, 0.0);
+        if (col < ns) c_s[cc][col] = fmax(c_s[cc][col] + x_s[quad][col], 0.0);
       }
       __syncthreads();
     }
@@ -164,7 +188,8 @@ int chem_mech_launch(const ChemMechDev& m, double* rhoY, const double* T, int nc
   if (m.ns < 1 || m.ns > TILE || m.R < 4 || m.R % 4 != 0 || m.R > MAXR || ncell < 1 || nsub < 1)
     return (int)hipErrorInvalidValue;
   const int blocks = (ncell + TILE - 1) / TILE;
-  hipLaunchKernelGGL(hf2d_chem_mech, dim3(blocks), dim3(64), 0, stream, m.nmat, m.arr, m.rsp, m.rord, m.W, m.ns,
+  const size_t lds = sizeof(double) * TILE * (m.R + 1);
+  hipLaunchKernelGGL(hf2d_chem_mech, dim3(blocks), dim3(64), lds, stream, m.nmat, m.arr, m.rsp, m.rord, m.W, m.ns,
                      m.R, ncell, rhoY, T, dt, nsub);
   return (int)hipGetLastError();
 }
