@@ -42,6 +42,10 @@ __device__ __forceinline__ double pw3(double x, int o) {
   return o == 0 ? 1.0 : (o == 1 ? x : (o == 2 ? x2 : x2 * x));
 }
 
+// NSP: system size (ns rounded up to a multiple of 4).  Rows/columns >= ns carry an
+// identity block (no reaction touches them), so only the NSP x NSP block and the rhs
+// are eliminated.
+template <int NSP>
 __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ nmat,   // [16][R]
                                                      const double* __restrict__ arr,    // A[R], b[R], Ta[R]
                                                      const int* __restrict__ rsp,       // [R][3]
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ 
       int kk = 0;
       double diag = 1.0;
 #pragma unroll
-      for (int k = 0; k < TILE; k++) {
+      for (int k = 0; k < NSP; k++) {
         double v = used ? -1.0 : fabs(row[k]);
         int idx = col;
 #pragma unroll
@@ -157,9 +161,10 @@ __global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ 
           row[k] = 0.0;
         }
 #pragma unroll
-        for (int j = k + 1; j <= TILE; j++) row[j] -= f * __shfl(row[j], p, 16);
+        for (int j = k + 1; j <= TILE; j++)
+          if (j < NSP || j == TILE) row[j] -= f * __shfl(row[j], p, 16);
       }
-      x_s[quad][kk] = row[TILE] / diag;
+      if (used) x_s[quad][kk] = row[TILE] / diag;
       __syncthreads();
       {
         const int cc = 4 * g + quad;
@@ -189,8 +194,16 @@ int chem_mech_launch(const ChemMechDev& m, double* rhoY, const double* T, int nc
     return (int)hipErrorInvalidValue;
   const int blocks = (ncell + TILE - 1) / TILE;
   const size_t lds = sizeof(double) * TILE * (m.R + 1);
-  hipLaunchKernelGGL(hf2d_chem_mech, dim3(blocks), dim3(64), lds, stream, m.nmat, m.arr, m.rsp, m.rord, m.W, m.ns,
-                     m.R, ncell, rhoY, T, dt, nsub);
+#define HF2D_CHEM_LAUNCH(N)                                                                                  \
+  hipLaunchKernelGGL(hf2d_chem_mech<N>, dim3(blocks), dim3(64), lds, stream, m.nmat, m.arr, m.rsp, m.rord, m.W, \
+                     m.ns, m.R, ncell, rhoY, T, dt, nsub)
+  switch ((m.ns + 3) / 4) {
+    case 1: HF2D_CHEM_LAUNCH(4); break;
+    case 2: HF2D_CHEM_LAUNCH(8); break;
+    case 3: HF2D_CHEM_LAUNCH(12); break;
+    default: HF2D_CHEM_LAUNCH(16); break;
+  }
+#undef HF2D_CHEM_LAUNCH
   return (int)hipGetLastError();
 }
 

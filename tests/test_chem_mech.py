@@ -74,3 +74,38 @@ def test_chem_mech_gpu_closed_form_and_padding():
     got, _ = ch.mech_step_gpu(m, Y, T, 0.01, nsub=5)
     np.testing.assert_allclose(got[0], Y[0] / (1 + 50.0 * 0.002) ** 5, rtol=1e-13)
     np.testing.assert_allclose(got.sum(0), Y.sum(0), rtol=1e-13)
+
+
+def _random_mech(ns, nr, seed):
+    rng = np.random.default_rng(seed)
+    sp = ["S%d" % i for i in range(ns)]
+    rx = []
+    for _ in range(nr):
+        k = int(rng.integers(1, 4))
+        reac = {sp[i]: int(rng.integers(1, 3)) for i in rng.choice(ns, size=k, replace=False)}
+        prod = {sp[i]: 1 for i in rng.choice(ns, size=int(rng.integers(1, 3)), replace=False)}
+        rx.append(ch.Reaction(reac, prod, float(10 ** rng.uniform(0, 3)), float(rng.uniform(-1, 1)),
+                              float(rng.uniform(0, 3000))))
+    return ch.Mechanism(sp, 0.001 + 0.05 * rng.random(ns), rx)
+
+
+def test_random_mechanism_reference_runs():
+    m = _random_mech(13, 21, 5)
+    assert m.packed()[0].shape == (16, 24)
+    Y = np.random.default_rng(1).random((13, 40)) * 0.05
+    out = ch.reference_step(m, Y, np.full(40, 1500.0), 1e-4, nsub=2)
+    assert np.isfinite(out).all() and (out >= 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ns,nr", [(3, 5), (10, 17), (13, 21), (16, 40)])
+def test_chem_mech_gpu_random_mechanisms(ns, nr):
+    """Every padded system size (4, 12, 16) and reaction padding against the FP64 reference."""
+    m = _random_mech(ns, nr, ns)
+    rng = np.random.default_rng(ns + nr)
+    n = 16 * 9 + 7
+    Y = rng.random((ns, n)) * 0.05
+    T = 900.0 + 1500.0 * rng.random(n)
+    ref = ch.reference_step(m, Y, T, 1e-4, nsub=2)
+    got, _ = ch.mech_step_gpu(m, Y, T, 1e-4, nsub=2)
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-10
