@@ -14,7 +14,8 @@ implemented.  This module supplies that slot as a standalone operator:
   ``c <- max(c + dc, 0)`` at frozen temperature;
 * :func:`mech_step_gpu` - the same update on the MFMA matrix cores
   (``csrc/hip/chem_mech.hip``: rates and per-cell Jacobians as
-  ``v_mfma_f64_16x16x4_f64`` products, 16x16 solves in LDS).
+  ``v_mfma_f64_16x16x4_f64`` products; the ns x ns point-implicit systems are
+  solved by Gauss-Jordan in registers, 16 lanes per cell).
 
 Species are carried as ``rhoY`` in a species-major ``[ns, ncell]`` array (the
 solver's SoA layout).  Heat release enters the caller's energy balance through
@@ -50,12 +51,39 @@ class Mechanism:
         ns = len(self.species)
         if not 1 <= ns <= MAX_SPECIES or self.W.shape != (ns,):
             raise ValueError("mechanism needs 1..16 species with one molar mass each")
+        if len(self.reactions) > 64:
+            raise ValueError("at most 64 reactions (the kernel's reactant table)")
         for r in self.reactions:
             if len(r.reactants) > 3 or any(not 0 <= o <= 3 for o in r.reactants.values()):
                 raise ValueError("at most 3 distinct reactants of order 0..3 per reaction")
             for s in list(r.reactants) + list(r.products):
                 if s not in self.species:
                     raise ValueError("unknown species %r" % s)
+
+    def to_dict(self) -> dict:
+        return {"species": list(self.species), "W": [float(w) for w in self.W],
+                "reactions": [{"reactants": r.reactants, "products": r.products, "A": r.A, "b": r.b, "Ta": r.Ta}
+                              for r in self.reactions]}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "Mechanism":
+        return cls(list(d["species"]), np.asarray(d["W"], dtype=np.float64),
+                   [Reaction(dict(r["reactants"]), dict(r["products"]), float(r["A"]), float(r.get("b", 0.0)),
+                             float(r.get("Ta", 0.0))) for r in d["reactions"]])
+
+    def save(self, path: str) -> None:
+        """JSON mechanism file (SI units: A in (m^3/mol)^(order-1)/s, Ta = Ea/Ru in K)."""
+        import json
+
+        with open(path, "w") as f:
+            json.dump(self.to_dict(), f, indent=1)
+
+    @classmethod
+    def load(cls, path: str) -> "Mechanism":
+        import json
+
+        with open(path) as f:
+            return cls.from_dict(json.load(f))
 
     @property
     def ns(self) -> int:

@@ -109,3 +109,13 @@ def test_chem_mech_gpu_random_mechanisms(ns, nr):
     ref = ch.reference_step(m, Y, T, 1e-4, nsub=2)
     got, _ = ch.mech_step_gpu(m, Y, T, 1e-4, nsub=2)
     assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-10
+
+
+def test_mechanism_json_roundtrip(tmp_path):
+    m = ch.h2_air_demo()
+    p = str(tmp_path / "mech.json")
+    m.save(p)
+    m2 = ch.Mechanism.load(p)
+    for a, b in zip(m.packed(), m2.packed()):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(m.W, m2.W)
