@@ -46,7 +46,7 @@ __device__ __forceinline__ double pw3(double x, int o) {
 // identity block (no reaction touches them), so only the NSP x NSP block and the rhs
 // are eliminated.
 template <int NSP>
-__global__ __launch_bounds__(64) void hf2d_chem_mech(const double* __restrict__ nmat,   // [16][R]
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf2d_chem_mech(const double* __restrict__ nmat,   // [16][R]
                                                      const double* __restrict__ arr,    // A[R], b[R], Ta[R]
                                                      const int* __restrict__ rsp,       // [R][3]
                                                      const int* __restrict__ rord,      // [R][3]
