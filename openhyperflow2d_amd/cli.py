@@ -125,6 +125,21 @@ def _cmd_build(a) -> int:
     return 0
 
 
+def _cmd_chem(a) -> int:
+    """K12 multi-reaction chemistry on the GPU: time one call on a synthetic field, check vs FP64 reference."""
+    import json
+
+    from .ops import chemistry as ch
+
+    m = ch.Mechanism.load(a.mech) if a.mech else ch.h2_air_demo()
+    if a.save_demo:
+        ch.h2_air_demo().save(a.save_demo)
+        return 0
+    res = ch.benchmark(m, a.nx * a.ny, a.dt, a.nsub, a.repeats)
+    print(json.dumps(res))
+    return 0 if res["rel_err_vs_torch_fp64"] < 1e-10 else 1
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m openhyperflow2d_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -150,8 +165,16 @@ def main(argv=None) -> int:
     i = sub.add_parser("info", help="pre-process a deck and print a summary")
     i.add_argument("deck")
     sub.add_parser("build", help="build the native extension and CLIs")
+    c = sub.add_parser("chem", help="run/benchmark a multi-reaction mechanism on the MFMA chemistry kernel (K12)")
+    c.add_argument("--mech", help="mechanism JSON (default: demo 8-species H2-air set)")
+    c.add_argument("--save-demo", dest="save_demo", metavar="PATH", help="write the demo mechanism as JSON and exit")
+    c.add_argument("--nx", type=int, default=6000)
+    c.add_argument("--ny", type=int, default=400)
+    c.add_argument("--nsub", type=int, default=4)
+    c.add_argument("--dt", type=float, default=1e-7)
+    c.add_argument("--repeats", type=int, default=10)
     a = ap.parse_args(argv)
-    return {"run": _cmd_run, "deck": _cmd_deck, "info": _cmd_info, "build": _cmd_build}[a.cmd](a)
+    return {"run": _cmd_run, "deck": _cmd_deck, "info": _cmd_info, "build": _cmd_build, "chem": _cmd_chem}[a.cmd](a)
 
 
 if __name__ == "__main__":

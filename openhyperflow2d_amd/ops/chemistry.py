@@ -204,9 +204,26 @@ def mech_step_gpu(mech: Mechanism, rhoY: np.ndarray, T: np.ndarray, dt: float, n
     return out, ms
 
 
+def benchmark(mech: Mechanism, ncell: int, dt: float = 1e-7, nsub: int = 4, repeats: int = 10,
+              check_cells: int = 4096, seed: int = 11) -> dict:
+    """Time the K12 kernel on ``ncell`` synthetic states and check a cell subset against
+    :func:`reference_step`.  Returns a JSON-able dict (``rel_err_vs_torch_fp64`` included)."""
+    Y, T = demo_state(mech, ncell, seed=seed)
+    got, ms = mech_step_gpu(mech, Y, T, dt, nsub, repeats=repeats)
+    sel = np.random.default_rng(0).choice(ncell, size=min(ncell, check_cells), replace=False)
+    ref = reference_step(mech, Y[:, sel], T[sel], dt, nsub)
+    err = float(np.abs(got[:, sel] - ref).max() / np.abs(ref).max())
+    R = mech.packed()[0].shape[1]
+    # MFMA work issued: per 16-cell tile and substep, (1 + 16) chains of R/4 16x16x4 f64 MFMAs
+    mfma_flop = (ncell / 16) * nsub * 17 * (R / 4) * (2 * 16 * 16 * 4)
+    return {"metric": "K12 mechanism chemistry", "cells": ncell, "species": mech.ns, "reactions": len(mech.reactions),
+            "nsub": nsub, "dt": dt, "ms_per_call": ms, "Mcells_per_s": ncell / ms / 1e3,
+            "mfma_f64_tflops": mfma_flop / ms / 1e9, "rel_err_vs_torch_fp64": err}
+
+
 def element_mass(mech: Mechanism, rhoY: np.ndarray) -> np.ndarray:
     """Total mass per cell (sum of rhoY); conserved by a balanced mechanism before clipping."""
     return np.asarray(rhoY).sum(axis=0)
 
 
-__all__ = ["Mechanism", "Reaction", "h2_air_demo", "demo_state", "reference_step", "mech_step_gpu", "element_mass"]
+__all__ = ["Mechanism", "Reaction", "h2_air_demo", "demo_state", "reference_step", "mech_step_gpu", "benchmark", "element_mass"]

@@ -119,3 +119,24 @@ def test_mechanism_json_roundtrip(tmp_path):
     for a, b in zip(m.packed(), m2.packed()):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(m.W, m2.W)
+
+
+def test_cli_chem_save_demo(tmp_path):
+    from openhyperflow2d_amd import cli
+
+    p = str(tmp_path / "demo.json")
+    assert cli.main(["chem", "--save-demo", p]) == 0
+    assert ch.Mechanism.load(p).species == ch.h2_air_demo().species
+
+
+@pytest.mark.gpu
+def test_cli_chem_runs_json_mechanism(tmp_path, capsys):
+    import json
+
+    from openhyperflow2d_amd import cli
+
+    p = str(tmp_path / "m.json")
+    _random_mech(6, 9, 2).save(p)
+    assert cli.main(["chem", "--mech", p, "--nx", "40", "--ny", "10", "--repeats", "2", "--dt", "1e-4"]) == 0
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert res["cells"] == 400 and res["species"] == 6 and res["rel_err_vs_torch_fp64"] < 1e-10

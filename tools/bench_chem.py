@@ -6,8 +6,6 @@ import json
 import os
 import sys
 
-import numpy as np
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from openhyperflow2d_amd.ops import chemistry as ch  # noqa: E402
@@ -20,20 +18,12 @@ def main():
     ap.add_argument("--nsub", type=int, default=4)
     ap.add_argument("--dt", type=float, default=1e-7)
     ap.add_argument("--repeats", type=int, default=10)
+    ap.add_argument("--mech", help="mechanism JSON (Mechanism.save format); default: demo H2-air set")
     a = ap.parse_args()
-    m = ch.h2_air_demo()
-    n = a.nx * a.ny
-    Y, T = ch.demo_state(m, n, seed=11)
-    got, ms = ch.mech_step_gpu(m, Y, T, a.dt, a.nsub, repeats=a.repeats)
-    sel = np.random.default_rng(0).choice(n, size=min(n, 4096), replace=False)
-    ref = ch.reference_step(m, Y[:, sel], T[sel], a.dt, a.nsub)
-    err = float(np.abs(got[:, sel] - ref).max() / np.abs(ref).max())
-    R = m.packed()[0].shape[1]
-    # MFMA work actually issued: per 16-cell tile and substep, (1 + 16) chains of R/4 16x16x4 f64 MFMAs
-    mfma_flop = (n / 16) * a.nsub * 17 * (R / 4) * (2 * 16 * 16 * 4)
-    print(json.dumps({"metric": "K12 mechanism chemistry", "cells": n, "species": m.ns, "reactions": len(m.reactions),
-                      "nsub": a.nsub, "ms_per_call": ms, "Mcells_per_s": n / ms / 1e3,
-                      "mfma_f64_tflops": mfma_flop / ms / 1e9, "rel_err_vs_torch_fp64": err}))
+    m = ch.Mechanism.load(a.mech) if a.mech else ch.h2_air_demo()
+    res = ch.benchmark(m, a.nx * a.ny, a.dt, a.nsub, a.repeats)
+    print(json.dumps(res))
+    err = res["rel_err_vs_torch_fp64"]
     if not err < 1e-10:
         raise SystemExit("mismatch vs reference: %g" % err)
 
