@@ -138,18 +138,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
       double diag = 1.0;
 #pragma unroll
       for (int k = 0; k < NSP; k++) {
-        double v = used ? -1.0 : fabs(row[k]);
-        int idx = col;
+        // Pivot = max |M[i][k]| over unused rows, ties to the lower row: one 64-bit key per
+        // lane (|v|'s bits, monotone for v >= 0, low 4 mantissa bits replaced by 15 - row).
+        unsigned long long key =
+            used ? 0ull : ((unsigned long long)__double_as_longlong(fabs(row[k])) & ~15ull) | (unsigned)(15 - col);
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
-          const double ov = __shfl_xor(v, off, 16);
-          const int oi = __shfl_xor(idx, off, 16);
-          if (ov > v || (ov == v && oi < idx)) {
-            v = ov;
-            idx = oi;
-          }
+          const unsigned long long ok = __shfl_xor(key, off, 16);
+          key = ok > key ? ok : key;
         }
-        const int p = idx;
+        const int p = 15 - (int)(key & 15ull);
         const double pk = __shfl(row[k], p, 16);
         const bool me = col == p;
         const double f = me ? 0.0 : row[k] / pk;
