@@ -14,7 +14,7 @@ test: build       ## CPU suite (reference decks, steppers, distributed gloo, CLI
 	$(PY) -m pytest tests -x -q -m "not gpu"
 
 gputest: build    ## GPU suite on an MI355X box
-	$(GPURUN) --timeout 900 -- 'bash tools/gpu_round_check.sh'
+	$(GPURUN) --timeout 900 -- 'bash tools/gpu_suite.sh all'
 
 bench: build      ## headline benchmark, one GPU
 	$(PY) bench.py
