@@ -1,3 +1,4 @@
+#include <algorithm>
 // Python bindings (pybind11) for the native hf2d runtime.
 #include <pybind11/functional.h>
 #include <pybind11/numpy.h>
@@ -234,7 +235,32 @@ PYBIND11_MODULE(_hf2d, m) {
       })
       .def("set_chem_model", [](Case& c, int m) { c.cfg.chem_model = m; })
       .def("partition", &Case::partition_columns)
-      .def("field", [](const Case& c, const std::string& n) { return field_scalar(c.J, n); })
+      .def("field", [](const Case& c, const std::string& n) {
+        // mechanism mode: "Y:<species>" mass fraction, "rhoY:<species>" partial density
+        if ((n.rfind("Y:", 0) == 0 || n.rfind("rhoY:", 0) == 0) && c.cfg.mech_mode()) {
+          const bool frac = n[0] == 'Y';
+          const std::string sp = n.substr(n.find(':') + 1);
+          const auto& names = c.cfg.mech->species;
+          const auto it = std::find(names.begin(), names.end(), sp);
+          if (it == names.end()) throw std::runtime_error("unknown species " + sp);
+          const long q = it - names.begin(), NG = (long)c.J.nx * c.J.ny;
+          py::array_t<double> a({c.J.nx, c.J.ny});
+          auto m = a.mutable_unchecked<2>();
+          for (int i = 0; i < c.J.nx; i++)
+            for (int j = 0; j < c.J.ny; j++) {
+              const double r = c.mech_rhoY[(size_t)q * NG + (long)i * c.J.ny + j];
+              const double rho = c.J.at(i, j).S[I_RHO];
+              m(i, j) = frac ? (rho != 0 ? r / rho : 0.0) : r;
+            }
+          return a;
+        }
+        return field_scalar(c.J, n);
+      })
+      .def_property_readonly("mech_mode", [](const Case& c) { return c.cfg.mech_mode(); })
+      .def_property_readonly("mech_species", [](const Case& c) {
+        return c.cfg.mech ? c.cfg.mech->species : std::vector<std::string>{};
+      })
+      .def_property_readonly("mech_name", [](const Case& c) { return c.cfg.mech ? c.cfg.mech->name : std::string(); })
       .def("records", [](const Case& c) {
         return py::bytes((const char*)c.J.c.data(), c.J.c.size() * sizeof(CellRecord));
       })
@@ -408,6 +434,58 @@ PYBIND11_MODULE(_hf2d, m) {
              s.unpack_column(g, li, a.data());
            })
       .def("set_exchange", [](CpuSolver& s, std::function<void(CpuSolver&, int)> f) { s.halo_exchange = f; });
+
+  // --- mechanism (mechanism.hpp) host references ---------------------------
+  m.def("mech_load", [](const std::string& name) {
+    auto mi = load_mechanism(name);
+    py::dict d;
+    d["name"] = mi->name;
+    d["species"] = mi->species;
+    d["nr"] = mi->data.nr;
+    d["W"] = std::vector<double>(mi->data.W, mi->data.W + mi->data.ns);
+    return d;
+  });
+  m.def("mech_chem_host", [](const std::string& name, py::array_t<double, py::array::c_style | py::array::forcecast> rhoY,
+                             py::array_t<double, py::array::c_style | py::array::forcecast> rho,
+                             py::array_t<double, py::array::c_style | py::array::forcecast> e,
+                             py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub) {
+    // [ns, ncell] partial densities at constant (rho, e): the scalar point-implicit
+    // integrator the device kernels are checked against; returns (rhoY, T)
+    auto mi = load_mechanism(name);
+    const MechData& md = mi->data;
+    const long n = (long)rho.size();
+    if (rhoY.ndim() != 2 || rhoY.shape(0) != md.ns || rhoY.shape(1) != n || e.size() != n || T.size() != n)
+      throw std::runtime_error("mech_chem_host: shapes [ns, n], [n], [n], [n]");
+    py::array_t<double> out({(long)md.ns, n});
+    py::array_t<double> Tout(n);
+    auto R = rhoY.unchecked<2>();
+    auto O = out.mutable_unchecked<2>();
+    auto TO = Tout.mutable_unchecked<1>();
+    for (long q = 0; q < n; q++) {
+      double y[MECH_MAXSP];
+      for (int s = 0; s < md.ns; s++) y[s] = R(s, q);
+      double Tq = T.data()[q];
+      mech_chem_cell<MECH_MAXSP>(md, rho.data()[q], e.data()[q], y, &Tq, dt, nsub);
+      for (int s = 0; s < md.ns; s++) O(s, q) = y[s];
+      TO(q) = Tq;
+    }
+    return py::make_tuple(out, Tout);
+  });
+  m.def("mech_thermo_host", [](const std::string& name, std::vector<double> Y, double T) {
+    auto mi = load_mechanism(name);
+    double e, cv, R, cp, mu, lam;
+    mech_mix_thermo<MECH_MAXSP>(mi->data, Y.data(), T, &e, &cv, &R, &cp);
+    mech_transport<MECH_MAXSP>(mi->data, Y.data(), T, &mu, &lam);
+    py::dict d;
+    d["e"] = e;
+    d["cv"] = cv;
+    d["R"] = R;
+    d["cp"] = cp;
+    d["mu"] = mu;
+    d["lam"] = lam;
+    d["T_from_e"] = mech_T_from_e<MECH_MAXSP>(mi->data, Y.data(), e, 1000.0);
+    return d;
+  });
 
   py::class_<RefSolver, SolverBase>(m, "RefSolver").def(py::init<Case&>(), py::keep_alive<1, 2>());
 

@@ -8,6 +8,7 @@
 #pragma once
 
 #include <functional>
+#include <memory>
 #include <ostream>
 #include <string>
 #include <utility>
@@ -17,6 +18,7 @@
 #include "deck.hpp"
 #include "gasdyn.hpp"
 #include "physics.hpp"
+#include "mechanism_io.hpp"
 
 namespace hf2d {
 
@@ -77,6 +79,16 @@ struct Config {
   // runtime options (not in decks; defaults reproduce the reference MPI build)
   Semantics semantics = Semantics::MPI;
   int chem_model = CRM_ZELDOVICH;
+  // detailed finite-rate chemistry (new keys): ChemicalReactionsModel = 2 and
+  // Mechanism = <built-in name | file.mech> select mechanism mode; the
+  // ChemSubsteps point-implicit substeps run per flow step in every cell
+  // hotter than ChemTmin [K]
+  std::string mechanism;
+  std::shared_ptr<MechInfo> mech;
+  int chem_nsub = 1;
+  real chem_tmin = 300.0;
+  bool mech_mode() const { return chem_model == CRM_ARRENIUS && mech != nullptr; }
+  int mech_ns() const { return mech ? mech->data.ns : 0; }
 
   void load_globals(InputDeck& d);   // InitSharedData
   FillParams fill_params() const;    // static FlowNode2D parameters
@@ -106,6 +118,9 @@ class Case {
   long restart_iter = 0;     // iteration count from the .hf2d.meta sidecar of a preloaded checkpoint
   std::string swap_path;     // resolved checkpoint path ("" = none)
   std::ostream* log = nullptr;
+  // mechanism mode: species partial densities, species-major [ns][MaxX*MaxY]
+  std::vector<real> mech_rhoY;
+  std::string species_path() const { return swap_path + ".species"; }
 
   // Build the whole problem from a deck.  workdir is where <Project>.hf2d is
   // looked up; checkpoint=false ignores any existing swap file.
@@ -125,6 +140,11 @@ class Case {
   void scan_area(int num_parts);
   void set_sources(int iter = 0);
   std::vector<std::pair<int, int>> partition_columns(int num_parts) const;
+  // mechanism mode: slot -> species split of the pre-processed field, and the
+  // matching record state (rho from p and T, thermally perfect rho*E)
+  void init_mechanism(std::vector<real>& rhoY) const;
+  void apply_mechanism_state(const std::vector<real>& rhoY);
+  void refresh_mechanism_primitives();
 
  private:
   void preprocess(InputDeck& d, const std::string& workdir, bool use_checkpoint);

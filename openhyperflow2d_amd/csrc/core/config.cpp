@@ -58,6 +58,10 @@ void Config::load_globals(InputDeck& d) {
   // new key (not in the reference, which always runs the Zeldovich model):
   // 0 frozen mixture, 1 Zeldovich (default), 2 finite-rate H2/air
   chem_model = d.get_int_or("ChemicalReactionsModel", CRM_ZELDOVICH);
+  mechanism = d.get_string_or("Mechanism", "");
+  chem_nsub = d.get_int_or("ChemSubsteps", 1);
+  if (chem_nsub < 1) chem_nsub = 1;
+  chem_tmin = d.get_float_or("ChemTmin", 300.0);
   species.arr_A = d.get_float_or("Arrhenius.A", species.arr_A);
   species.arr_Ta = d.get_float_or("Arrhenius.Ta", species.arr_Ta);
   species.arr_a = d.get_float_or("Arrhenius.FuelOrder", species.arr_a);

@@ -46,6 +46,10 @@ int sk_eligible(const Case& cs, std::string* why) {
     return (int)SK_GENERIC;
   };
   const Config& C = cs.cfg;
+  if (C.mech_mode()) {   // species block on SK_MECH for Euler and N-S decks
+    if (why) *why = "mechanism: SK_MECH";
+    return SK_MECH;
+  }
   if (C.ProblemType != SM_NS) return no("inviscid problem");
   if (!C.sources.empty()) return no("gas sources");
   if (C.chem_model == CRM_ARRENIUS) return no("finite-rate chemistry sources");
@@ -68,6 +72,15 @@ int sk_eligible(const Case& cs, std::string* why) {
   }
   if (why) *why = laminar ? "" : "turbulent: SK_SGT";
   return laminar ? SK_SGL : SK_SGT;
+}
+
+bool mech_species_cauchy(const Case& cs) {
+  for (const CellRecord& c : cs.J.c) {
+    if (!is_active(c.CT)) continue;
+    const EqFlags f = eq_flags(I_YFU, c.CT, c.TurbType, cs.cfg.ProblemType);
+    if (f.dx2 || f.dy2) return true;
+  }
+  return false;
 }
 
 bool lean_single_gas(const Case& cs) {
@@ -138,7 +151,8 @@ namespace hf2d {
 void compute_generic_flags(const Case& cs, HostArrays& h) {
   const long N = h.N;
   const std::vector<uint8_t> lb = lean_flags(h, cs.cfg.ProblemType);
-  const bool src_all = cs.cfg.chem_model == CRM_ARRENIUS || !cs.cfg.sources.empty();
+  // (mechanism mode: the kinetics are operator-split, no species Src)
+  const bool src_all = (cs.cfg.chem_model == CRM_ARRENIUS && !cs.cfg.mech_mode()) || !cs.cfg.sources.empty();
   static const real zero = 0.0;
   auto nonzero = [&](const std::vector<real>& a, long idx, int k0, int k1) {
     for (int k = k0; k < k1; k++)

@@ -133,6 +133,7 @@ HF_HD inline void lean_load_own(const LeanSoA& L, long idx, LeanOwn& o) {
 struct LeanIOCommon {
   static constexpr int NE = 4 + NCOMP;
   static constexpr bool skip(int) { return false; }
+  HF_HD static constexpr int eq(int k) { return k; }
   const LeanSoA& L;
   long N, idx, iL, iR, iU, iD;
   uint8_t lb = 0;

@@ -1,0 +1,425 @@
+// Mechanism files (*.mech, see openhyperflow2d_amd/ops/mechanism.py for the
+// format), the built-in H2/air mechanism and the conversion of a pre-processed
+// reference field to mechanism mode (Case::init_mechanism).
+#include "mechanism_io.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+
+#include "case.hpp"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+namespace hf2d {
+
+#include "mech_builtin.inc"
+
+namespace {
+
+std::vector<std::string> split_ws(const std::string& s) {
+  std::istringstream is(s);
+  std::vector<std::string> t;
+  std::string w;
+  while (is >> w) t.push_back(w);
+  return t;
+}
+
+double to_d(const std::string& s) {
+  size_t n = 0;
+  const double v = std::stod(s, &n);
+  if (n != s.size()) throw std::runtime_error("bad number '" + s + "'");
+  return v;
+}
+
+// "2 OH + H" (tokens between arrows) -> (species, coefficient) pairs
+void parse_side(const std::vector<std::string>& tok, size_t a, size_t b, const std::map<std::string, int>& idx,
+                int* sp, int* nu, int* n) {
+  *n = 0;
+  int coef = 1;
+  for (size_t i = a; i < b; i++) {
+    const std::string& t = tok[i];
+    if (t == "+" || t == "M" || t == "(+M)" || t == "(M)") continue;
+    bool digits = !t.empty();
+    for (char ch : t) digits = digits && ch >= '0' && ch <= '9';
+    if (digits) {
+      coef = std::stoi(t);
+      continue;
+    }
+    auto it = idx.find(t);
+    if (it == idx.end()) throw std::runtime_error("unknown species '" + t + "'");
+    int k = 0;
+    for (; k < *n; k++)
+      if (sp[k] == it->second) break;
+    if (k == *n) {
+      if (*n == 3) throw std::runtime_error("more than 3 distinct species on one side");
+      sp[k] = it->second;
+      nu[k] = 0;
+      (*n)++;
+    }
+    nu[k] += coef;
+    if (nu[k] > 3) throw std::runtime_error("stoichiometric coefficient > 3");
+    coef = 1;
+  }
+  if (*n == 0) throw std::runtime_error("empty reaction side");
+}
+
+// Neufeld et al. collision integral Omega(2,2)*
+double omega22(double Ts) {
+  return 1.16145 * std::pow(Ts, -0.14874) + 0.52487 * std::exp(-0.77320 * Ts) + 2.16178 * std::exp(-2.43787 * Ts);
+}
+
+}  // namespace
+
+std::shared_ptr<MechInfo> parse_mechanism(const std::string& text) {
+  auto info = std::make_shared<MechInfo>();
+  MechData& m = info->data;
+  std::map<std::string, int> idx;
+  std::map<std::string, std::vector<double>> thermo;
+  std::map<std::string, std::pair<double, double>> lj;
+  std::vector<std::vector<std::string>> rx_lines, slot_lines;
+  std::istringstream is(text);
+  std::string line;
+  int lineno = 0;
+  while (std::getline(is, line)) {
+    lineno++;
+    const size_t h = line.find('#');
+    if (h != std::string::npos) line = line.substr(0, h);
+    auto tok = split_ws(line);
+    if (tok.empty()) continue;
+    try {
+      if (tok[0] == "mechanism") {
+        info->name = tok.at(1);
+      } else if (tok[0] == "species") {
+        for (size_t i = 1; i < tok.size(); i++) {
+          if ((int)info->species.size() >= MECH_MAXSP) throw std::runtime_error("more than 16 species");
+          idx[tok[i]] = (int)info->species.size();
+          info->species.push_back(tok[i]);
+        }
+      } else if (tok[0] == "thermo") {
+        std::vector<double> v;
+        for (size_t i = 2; i < tok.size(); i++) v.push_back(to_d(tok[i]));
+        if (v.size() != 18) throw std::runtime_error("thermo needs W Tlo Tmid Thi and 14 coefficients");
+        thermo[tok.at(1)] = v;
+      } else if (tok[0] == "transport") {
+        lj[tok.at(1)] = {to_d(tok.at(2)), to_d(tok.at(3))};
+      } else if (tok[0] == "reaction") {
+        rx_lines.push_back(tok);
+      } else if (tok[0] == "slot") {
+        slot_lines.push_back(tok);
+      } else {
+        throw std::runtime_error("unknown record '" + tok[0] + "'");
+      }
+    } catch (const std::exception& e) {
+      throw std::runtime_error("mechanism line " + std::to_string(lineno) + ": " + e.what());
+    }
+  }
+  m.ns = (int)info->species.size();
+  if (m.ns < 1) throw std::runtime_error("mechanism: no species");
+  m.bath = m.ns - 1;
+  for (int s = 0; s < m.ns; s++) {
+    auto it = thermo.find(info->species[s]);
+    if (it == thermo.end()) throw std::runtime_error("mechanism: no thermo for " + info->species[s]);
+    const auto& v = it->second;
+    m.W[s] = v[0];
+    if (!(m.W[s] > 0)) throw std::runtime_error("mechanism: molar mass of " + info->species[s] + " must be > 0");
+    m.Rs[s] = MECH_RU / m.W[s];
+    m.Tmid[s] = v[2];
+    for (int k = 0; k < 7; k++) {
+      m.a[s][0][k] = v[4 + k];
+      m.a[s][1][k] = v[11 + k];
+    }
+    const auto l = lj.count(info->species[s]) ? lj[info->species[s]] : std::make_pair(3.5, 100.0);
+    for (int t = 0; t < MECH_NT; t++) {
+      const double T = MECH_TT0 + MECH_TDT * t;
+      const double mu = 2.6693e-6 * std::sqrt(m.W[s] * 1e3 * T) / (l.first * l.first * omega22(T / l.second));
+      const double cp = m.Rs[s] * nasa_cp(mech_coef(m, s, T), T);
+      m.mu_tab[s][t] = mu;
+      m.lam_tab[s][t] = mu * (cp + 1.25 * m.Rs[s]);   // Eucken
+    }
+  }
+  if ((int)rx_lines.size() > MECH_MAXR) throw std::runtime_error("mechanism: more than 64 reactions");
+  m.nr = (int)rx_lines.size();
+  for (int r = 0; r < m.nr; r++) {
+    const auto& tok = rx_lines[r];
+    MechReaction& R = m.rx[r];
+    try {
+      size_t arrow = 0;
+      for (size_t i = 1; i < tok.size(); i++)
+        if (tok[i] == "<=>" || tok[i] == "=>") arrow = i;
+      if (!arrow) throw std::runtime_error("no arrow");
+      R.rev = tok[arrow] == "<=>";
+      size_t kv = arrow + 1;
+      while (kv < tok.size() && tok[kv].find('=') == std::string::npos) kv++;
+      parse_side(tok, 1, arrow, idx, R.rs, R.rn, &R.nrs);
+      parse_side(tok, arrow + 1, kv, idx, R.ps, R.pn, &R.nps);
+      R.dnu = 0;
+      for (int t = 0; t < R.nps; t++) R.dnu += R.pn[t];
+      for (int t = 0; t < R.nrs; t++) R.dnu -= R.rn[t];
+      std::map<std::string, std::string> kvs;
+      for (size_t i = kv; i < tok.size(); i++) {
+        const size_t e = tok[i].find('=');
+        if (e == std::string::npos) {
+          if (tok[i] == "M") R.tb = 1;
+          else if (tok[i] == "falloff") R.fo = 1;
+          else throw std::runtime_error("unknown flag '" + tok[i] + "'");
+        } else {
+          kvs[tok[i].substr(0, e)] = tok[i].substr(e + 1);
+        }
+      }
+      R.A = to_d(kvs.at("A"));
+      if (!(R.A > 0)) throw std::runtime_error("A must be > 0");
+      R.b = kvs.count("b") ? to_d(kvs["b"]) : 0.0;
+      R.Ta = kvs.count("Ta") ? to_d(kvs["Ta"]) : 0.0;
+      if (R.fo) {
+        R.A0 = to_d(kvs.at("A0"));
+        R.b0 = kvs.count("b0") ? to_d(kvs["b0"]) : 0.0;
+        R.Ta0 = kvs.count("Ta0") ? to_d(kvs["Ta0"]) : 0.0;
+      }
+      if (kvs.count("troe")) {
+        std::string s = kvs["troe"];
+        std::replace(s.begin(), s.end(), ',', ' ');
+        auto v = split_ws(s);
+        if (v.size() < 3 || v.size() > 4) throw std::runtime_error("troe needs 3 or 4 values");
+        R.ntroe = (int)v.size();
+        for (int k = 0; k < R.ntroe; k++) R.troe[k] = to_d(v[k]);
+      }
+      if ((R.tb || R.fo) && kvs.count("eff")) {
+        if (m.ntb >= MECH_MAXTB) throw std::runtime_error("more than 16 reactions with efficiencies");
+        R.eff = m.ntb++;
+        for (int s = 0; s < m.ns; s++) m.eff[R.eff][s] = 1.0;
+        std::string s = kvs["eff"];
+        std::replace(s.begin(), s.end(), ',', ' ');
+        for (const auto& p : split_ws(s)) {
+          const size_t c = p.find(':');
+          if (c == std::string::npos) throw std::runtime_error("eff entries are species:value");
+          auto it = idx.find(p.substr(0, c));
+          if (it == idx.end()) throw std::runtime_error("eff: unknown species " + p.substr(0, c));
+          m.eff[R.eff][it->second] = to_d(p.substr(c + 1));
+        }
+      }
+    } catch (const std::exception& e) {
+      throw std::runtime_error("mechanism reaction " + std::to_string(r + 1) + ": " + e.what());
+    }
+  }
+  static const char* slots[4] = {"fuel", "ox", "cp", "air"};
+  for (const auto& tok : slot_lines) {
+    int k = -1;
+    for (int q = 0; q < 4; q++)
+      if (tok.at(1) == slots[q]) k = q;
+    if (k < 0) throw std::runtime_error("mechanism: unknown slot " + tok.at(1));
+    std::string s = tok.at(2);
+    std::replace(s.begin(), s.end(), ',', ' ');
+    double tot = 0, best = -1;
+    for (const auto& p : split_ws(s)) {
+      const size_t c = p.find(':');
+      auto it = idx.find(p.substr(0, c));
+      if (c == std::string::npos || it == idx.end()) throw std::runtime_error("mechanism: bad slot entry " + p);
+      const double v = to_d(p.substr(c + 1));
+      m.slot[k][it->second] += v;
+      tot += v;
+      if (v > best) {
+        best = v;
+        m.slot_sp[k] = it->second;
+      }
+    }
+    for (int q = 0; q < m.ns; q++) m.slot[k][q] /= tot;
+  }
+  return info;
+}
+
+std::shared_ptr<MechInfo> load_mechanism(const std::string& name, const std::string& workdir) {
+  if (name == "h2_air_li2004" || name == "H2Air-Li2004" || name == "h2air") {
+    auto m = parse_mechanism(MECH_H2_AIR_LI2004);
+    m->source = "builtin:h2_air_li2004";
+    return m;
+  }
+  std::vector<std::string> tries = {name};
+  if (!workdir.empty() && name.size() && name[0] != '/') tries.insert(tries.begin(), workdir + "/" + name);
+  for (const auto& p : tries) {
+    std::ifstream f(p);
+    if (!f) continue;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    auto m = parse_mechanism(ss.str());
+    m->source = p;
+    return m;
+  }
+  throw std::runtime_error("mechanism '" + name + "' not found (built-in: h2_air_li2004)");
+}
+
+// Reference record -> mechanism mode: species from the 4 slots, density from
+// (p, T) with the mechanism's mixture gas constant, rho*E from the thermally
+// perfect internal energy; the fuel/ox/cp slots of the record become 0.
+void Case::init_mechanism(std::vector<real>& rhoY) const {
+  const MechData& m = cfg.mech->data;
+  const int ns = m.ns;
+  rhoY.assign((size_t)ns * J.c.size(), 0.0);
+  const long N = (long)J.c.size();
+  for (long q = 0; q < N; q++) {
+    CellRecord c = J.c[(size_t)q];
+    if (!(c.S[I_RHO] > 0) || !(c.Tg > 0)) continue;
+    real Y[MECH_MAXSP] = {};
+    for (int k = 0; k < 4; k++)
+      for (int s = 0; s < ns; s++) Y[s] += m.slot[k][s] * c.Y[k];
+    real tot = 0;
+    for (int s = 0; s < ns; s++) tot += Y[s];
+    if (!(tot > 0)) continue;
+    for (int s = 0; s < ns; s++) Y[s] /= tot;
+    real e, cv, Rm, cp;
+    mech_mix_thermo<MECH_MAXSP>(m, Y, c.Tg, &e, &cv, &Rm, &cp);
+    const real rho = c.p / (Rm * c.Tg);
+    for (int s = 0; s < ns; s++) rhoY[(size_t)s * N + q] = rho * Y[s];
+  }
+}
+
+// Restart: the pre-processor's reference FillNode2D pass over a preloaded
+// image recomputes Tg with the reference closure; re-derive T (Newton on the
+// stored rho*E), R, Cp, k, p and transport from the species sidecar.
+void Case::refresh_mechanism_primitives() {
+  const MechData& m = cfg.mech->data;
+  const int ns = m.ns;
+  const long N = (long)J.c.size();
+  for (long q = 0; q < N; q++) {
+    CellRecord& c = J.c[(size_t)q];
+    const real rho = c.S[I_RHO];
+    if (!(rho > 0) || has_all(c.CT, CT_SOLID)) continue;
+    real Y[MECH_MAXSP] = {};
+    for (int s = 0; s < ns; s++) Y[s] = mech_rhoY[(size_t)s * N + q] / rho;
+    const real U = c.S[I_RHOU] / rho, V = c.S[I_RHOV] / rho;
+    const real e = (c.S[I_RHOE] - 0.5 * rho * (U * U + V * V)) / rho;
+    const real T = mech_T_from_e<MECH_MAXSP>(m, Y, e, c.Tg > 0 ? c.Tg : 1000.0);
+    real ee, cv, Rm, cp;
+    mech_mix_thermo<MECH_MAXSP>(m, Y, T, &ee, &cv, &Rm, &cp);
+    c.Tg = T;
+    c.R = Rm;
+    c.CP = cp;
+    c.k = cp / cv;
+    c.p = rho * Rm * T;
+    mech_transport<MECH_MAXSP>(m, Y, T, &c.mu, &c.lam);
+    mech_slot_fractions(m, Y, c.Y);
+  }
+}
+
+void Case::apply_mechanism_state(const std::vector<real>& rhoY) {
+  const MechData& m = cfg.mech->data;
+  const int ns = m.ns;
+  const long N = (long)J.c.size();
+  for (long q = 0; q < N; q++) {
+    CellRecord& c = J.c[(size_t)q];
+    if (!(c.S[I_RHO] > 0)) continue;
+    real Y[MECH_MAXSP] = {};
+    real rho = 0;
+    for (int s = 0; s < ns; s++) rho += rhoY[(size_t)s * N + q];
+    if (!(rho > 0)) continue;
+    for (int s = 0; s < ns; s++) Y[s] = rhoY[(size_t)s * N + q] / rho;
+    const real T = c.Tg;
+    real e, cv, Rm, cp;
+    mech_mix_thermo<MECH_MAXSP>(m, Y, T, &e, &cv, &Rm, &cp);
+    const real sc = rho / c.S[I_RHO];
+    c.S[I_RHO] = rho;
+    c.S[I_RHOU] *= sc;
+    c.S[I_RHOV] *= sc;
+    c.S[I_K] *= sc;
+    c.S[I_EPS] *= sc;
+    c.S[I_RHOE] = rho * e + 0.5 * rho * (c.U * c.U + c.V * c.V);
+    for (int k = 0; k < NCOMP; k++) c.S[4 + k] = 0.0;
+    c.R = Rm;
+    c.CP = cp;
+    c.k = cp / cv;
+    c.p = rho * Rm * T;
+    mech_transport<MECH_MAXSP>(m, Y, T, &c.mu, &c.lam);
+    mech_slot_fractions(m, Y, c.Y);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// species sidecar (layout version 2)
+// ---------------------------------------------------------------------------
+size_t species_sidecar_bytes(int ns, int nx, int ny) {
+  return SPECIES_HEADER + (size_t)16 * ns + (size_t)nx * ny * ns * sizeof(real);
+}
+
+namespace {
+std::string species_header(const MechInfo& m, int nx, int ny) {
+  std::string h(SPECIES_HEADER + 16 * m.species.size(), '\0');
+  std::memcpy(&h[0], "HF2DSPC2", 8);
+  const uint32_t v[4] = {2u, (uint32_t)m.species.size(), (uint32_t)nx, (uint32_t)ny};
+  std::memcpy(&h[8], v, sizeof v);
+  for (size_t s = 0; s < m.species.size(); s++)
+    std::strncpy(&h[SPECIES_HEADER + 16 * s], m.species[s].c_str(), 15);
+  return h;
+}
+void put_bytes(int fd, const void* p, size_t n, off_t off) {
+  const char* c = (const char*)p;
+  while (n) {
+    const ssize_t r = ::pwrite(fd, c, n, off);
+    if (r <= 0) throw std::runtime_error("short write to species checkpoint");
+    c += r;
+    n -= (size_t)r;
+    off += r;
+  }
+}
+}  // namespace
+
+void write_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, const std::vector<real>& rhoY) {
+  const int ns = (int)m.species.size();
+  const long N = (long)nx * ny;
+  if ((long)rhoY.size() != ns * N) throw std::runtime_error("write_species_sidecar: size mismatch");
+  write_species_slab(path, m, nx, ny, rhoY.data(), N, 0, 0, nx);
+  int fd = ::open(path.c_str(), O_WRONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + path);
+  const int rc = ::ftruncate(fd, (off_t)species_sidecar_bytes(ns, nx, ny));
+  ::close(fd);
+  if (rc != 0) throw std::runtime_error("cannot size " + path);
+}
+
+void write_species_slab(const std::string& path, const MechInfo& m, int nx, int ny, const real* rhoY_local,
+                        long local_n, int local_i0, int gi0, int ncols) {
+  const int ns = (int)m.species.size();
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT, 0644);
+  if (fd < 0) throw std::runtime_error("cannot open species checkpoint " + path);
+  try {
+    const std::string h = species_header(m, nx, ny);
+    put_bytes(fd, h.data(), h.size(), 0);
+    std::vector<real> buf((size_t)ncols * ny * ns);
+    for (int c = 0; c < ncols; c++)
+      for (int j = 0; j < ny; j++)
+        for (int s = 0; s < ns; s++)
+          buf[((size_t)c * ny + j) * ns + s] = rhoY_local[(long)s * local_n + (long)(local_i0 + c) * ny + j];
+    put_bytes(fd, buf.data(), buf.size() * sizeof(real), (off_t)(h.size() + (size_t)gi0 * ny * ns * sizeof(real)));
+  } catch (...) {
+    ::close(fd);
+    throw;
+  }
+  ::close(fd);
+}
+
+bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, std::vector<real>& rhoY) {
+  const int ns = (int)m.species.size();
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0 || (size_t)st.st_size != species_sidecar_bytes(ns, nx, ny)) return false;
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::string h(SPECIES_HEADER + 16 * ns, '\0');
+  f.read(&h[0], (std::streamsize)h.size());
+  if (h != species_header(m, nx, ny)) return false;
+  const long N = (long)nx * ny;
+  std::vector<real> buf((size_t)N * ns);
+  f.read((char*)buf.data(), (std::streamsize)(buf.size() * sizeof(real)));
+  if (!f) return false;
+  rhoY.assign((size_t)ns * N, 0.0);
+  for (long q = 0; q < N; q++)
+    for (int s = 0; s < ns; s++) rhoY[(size_t)s * N + q] = buf[(size_t)q * ns + s];
+  return true;
+}
+
+}  // namespace hf2d

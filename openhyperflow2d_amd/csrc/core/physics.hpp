@@ -333,13 +333,25 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
 // ---------------------------------------------------------------------------
 // FillNode2D equivalent.  Returns false when the node is skipped.
 // ---------------------------------------------------------------------------
-template <class N>
-HF_HD inline bool fill_node(N& n, const FillParams& P) {
+// Mixture closure of fill_node.  RefMix is the reference's: k = Cp/(Cp-R)
+// from the previous step's mixture Cp and R, formation enthalpy sum Hu_i rhoY_i
+// over the four species slots, p = (k-1)(rhoE - rho|V|^2/2 - H_f).  Mechanism
+// mode (stepkern.hpp MechMix) replaces the three marked places.
+struct RefMix {
+  static constexpr bool MECH = false;
+  template <class N>
+  HF_HD void state(N&) const {}
+  template <class N>
+  HF_HD void heat_flux(const N&, real&, real&) const {}
+};
+
+template <class N, class MX = RefMix>
+HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (has_all(n.CT, CT_SOLID)) return false;
   if (n.S[I_RHO] == 0) return false;
   if (n.k < 1) return false;
   real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
-  n.k = n.CP / (n.CP - n.R);
+  if (!MX::MECH) n.k = n.CP / (n.CP - n.R);
   if (has_all(n.CT, CT_U_CONST))
     n.S[I_RHOU] = n.U * n.S[I_RHO];
   else
@@ -358,12 +370,14 @@ HF_HD inline bool fill_node(N& n, const FillParams& P) {
     if (n.TurbType > 0) turb_model(n, P, P.is_mu_t, P.is_init);
   }
 
-  Tmp1 = n.S[I_RHO];
-  for (int i = 0; i < NCOMP; i++) {
-    Tmp3 += P.Hu[i] * n.S[i + 4];
-    Tmp1 -= n.S[i + 4];
+  if (!MX::MECH) {
+    Tmp1 = n.S[I_RHO];
+    for (int i = 0; i < NCOMP; i++) {
+      Tmp3 += P.Hu[i] * n.S[i + 4];
+      Tmp1 -= n.S[i + 4];
+    }
+    Tmp3 += P.Hu[NCOMP] * Tmp1;
   }
-  Tmp3 += P.Hu[NCOMP] * Tmp1;
 
   if (has_all(n.CT, CT_WALL_LAW)) {
     Tmp1 = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
@@ -391,8 +405,12 @@ HF_HD inline bool fill_node(N& n, const FillParams& P) {
     for (int i = 0; i < NEQ; i++) n.SrcAdd[i] = 0.;
   }
 
-  n.p = (n.k - 1.) * (n.S[I_RHOE] - n.S[I_RHO] * (n.U * n.U + n.V * n.V) * 0.5 - Tmp3);
-  n.Tg = n.p / n.R / n.S[I_RHO];
+  if (MX::MECH) {
+    mx.state(n);   // T by Newton on the thermally perfect e(T); R, Cp, k, p at T
+  } else {
+    n.p = (n.k - 1.) * (n.S[I_RHOE] - n.S[I_RHO] * (n.U * n.U + n.V * n.V) * 0.5 - Tmp3);
+    n.Tg = n.p / n.R / n.S[I_RHO];
+  }
 
   if (P.sm == SM_NS) {
     n.lam_t = n.mu_t * n.CP;
@@ -442,9 +460,13 @@ HF_HD inline bool fill_node(N& n, const FillParams& P) {
     const real txy = _mu * (n.dUdy + n.dVdx);
     real qx = _lam * n.dTdx;
     real qy = _lam * n.dTdy;
-    for (int i = 0; i < NSPEC; i++) {
-      qx += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdx[i];
-      qy += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdy[i];
+    if (MX::MECH) {
+      mx.heat_flux(n, qx, qy);   // sum_s Diff h_s(T) d(rho Y_s)
+    } else {
+      for (int i = 0; i < NSPEC; i++) {
+        qx += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdx[i];
+        qy += n.Diff * (n.CP * n.Tg + P.Hu[i]) * n.droYdy[i];
+      }
     }
     n.RX[I_RHO] = 0.;
     n.RX[I_RHOU] = sxx;

@@ -435,7 +435,27 @@ Case Case::from_deck(InputDeck deck, const std::string& workdir, bool use_checkp
   Case cs;
   cs.log = log;
   cs.cfg.load_globals(deck);
+  if (cs.cfg.chem_model == CRM_ARRENIUS && !cs.cfg.mechanism.empty()) {
+    cs.cfg.mech = load_mechanism(cs.cfg.mechanism, workdir);
+    cs.cfg.mech->data.nsub = cs.cfg.chem_nsub;
+    cs.cfg.mech->data.Tchem = cs.cfg.chem_tmin;
+    if (cs.cfg.mech->data.slot_sp[3] < 0 && cs.cfg.mech->data.slot_sp[0] < 0)
+      throw DeckError("mechanism " + cs.cfg.mech->name + " has no slot map (slot fuel|ox|cp|air records)");
+  }
   cs.preprocess(deck, workdir, use_checkpoint);
+  if (cs.cfg.mech_mode()) {
+    if (!cs.cfg.sources.empty())
+      throw DeckError("SourceList2D species sources are not supported in mechanism mode (NumSrc must be 0)");
+    if (!(cs.preloaded && read_species_sidecar(cs.species_path(), *cs.cfg.mech, cs.J.nx, cs.J.ny, cs.mech_rhoY))) {
+      if (cs.preloaded)
+        throw DeckError("checkpoint " + cs.swap_path + " has no matching species sidecar (" + cs.species_path() +
+                        ") for mechanism " + cs.cfg.mech->name);
+      cs.init_mechanism(cs.mech_rhoY);
+      cs.apply_mechanism_state(cs.mech_rhoY);
+    } else {
+      cs.refresh_mechanism_primitives();
+    }
+  }
   return cs;
 }
 

@@ -148,6 +148,71 @@ void HostArrays::to_field(Field& J, int gi0, int i_from, int i_to, int pb, int d
   }
 }
 
+void HostArrays::allocate_mech(const Case& cs) {
+  mech = cs.cfg.mech_mode() ? &cs.cfg.mech->data : nullptr;
+  nsp = mech ? mech->ns : 0;
+  if (!mech) return;
+  const size_t n = (size_t)nsp * N;
+  for (int b = 0; b < 2; b++) Ys[b].assign(n, 0.0);
+  As.assign(n, 0.0);
+  Bs.assign(n, 0.0);
+  Fs.assign(n, 0.0);
+  betas.assign(n, 0.0);
+  const bool cauchy = mech_species_cauchy(cs);
+  for (int b = 0; b < 2; b++) {
+    dSdxs[b].assign(cauchy ? n : 0, 0.0);
+    dSdys[b].assign(cauchy ? n : 0, 0.0);
+  }
+}
+
+void HostArrays::mech_from_case(const Case& cs, int gi0) {
+  if (!mech) return;
+  const long NG = (long)cs.J.nx * cs.J.ny;
+  const real FT = (real)cs.cfg.FT;
+  for (int li = 0; li < nx; li++) {
+    const int gi = gi0 + li;
+    for (int j = 0; j < ny; j++) {
+      const long idx = (long)li * ny + j;
+      const CellRecord& c = cs.J.at(gi, j);
+      for (int sp = 0; sp < nsp; sp++) {
+        const long o = (long)sp * N + idx;
+        const real r = cs.mech_rhoY[(size_t)sp * NG + (long)gi * ny + j];
+        Ys[0][o] = Ys[1][o] = r;
+        // inviscid start fluxes (the pre-processor's FillNode2D has no
+        // species gradients either); the first fill rewrites them
+        As[o] = r * c.U;
+        Bs[o] = r * c.V;
+        Fs[o] = FT * r * c.V;
+        betas[o] = c.beta[I_YFU];
+        if (!dSdxs[0].empty()) dSdxs[0][o] = dSdxs[1][o] = dSdys[0][o] = dSdys[1][o] = 0.0;
+      }
+    }
+  }
+}
+
+void HostArrays::mech_to_case(Case& cs, int gi0, int i_from, int i_to, int ybuf) const {
+  if (!mech) return;
+  const long NG = (long)cs.J.nx * cs.J.ny;
+  for (int li = i_from; li < i_to; li++)
+    for (int j = 0; j < ny; j++)
+      for (int sp = 0; sp < nsp; sp++)
+        cs.mech_rhoY[(size_t)sp * NG + (long)(gi0 + li) * ny + j] = Ys[ybuf][(long)sp * N + (long)li * ny + j];
+}
+
+void HostArrays::mech_view(SoA& s, int yb, int db) const {
+  s.mech = mech;
+  s.nsp = nsp;
+  if (!mech) return;
+  auto P = [](const std::vector<real>& v) { return v.empty() ? nullptr : const_cast<real*>(v.data()); };
+  s.Ys = P(Ys[yb]);
+  s.As = P(As);
+  s.Bs = P(Bs);
+  s.Fs = P(Fs);
+  s.betas = P(betas);
+  s.dSdxs = P(dSdxs[db]);
+  s.dSdys = P(dSdys[db]);
+}
+
 SoA HostArrays::view(int sb, int db, int pb) {
   SoA s;
   s.nx = nx;
@@ -189,6 +254,7 @@ SoA HostArrays::view(int sb, int db, int pb) {
   s.gf = gf.empty() ? nullptr : gf.data();
   s.iw = iw.data();
   s.jw = jw.data();
+  mech_view(s, sb, db);
   return s;
 }
 
@@ -584,6 +650,14 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
         write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
       }
     }
+    if (opt.write_checkpoint && C.mech_mode()) {
+      // versioned species sidecar (mechanism_io.hpp): each rank writes the
+      // byte range of its own columns
+      PhaseScope ph(*this, "outputs.checkpoint_species");
+      const auto own = owned_columns();
+      write_species_slab(dir + "/" + C.swap_file + ".species", *C.mech, J.nx, J.ny, cs.mech_rhoY.data(),
+                         (long)J.nx * J.ny, own.first, own.first, own.second - own.first);
+    }
     if (C.MonitorIndex < 5)
       monitor_cond = last_res.max_rms > C.ExitMonitorValue ? 1 : 0;
     else
@@ -601,6 +675,7 @@ CpuSolver::CpuSolver(Case& c, int g0, int g1) : SolverBase(c), gi0(g0), gi1(g1 <
   const int rh = gi1 < c.J.nx ? 1 : 0;
   l_off = lh;
   h.allocate((gi1 - gi0) + lh + rh, c.J.ny);
+  h.allocate_mech(c);
   upload();
 }
 
@@ -613,6 +688,7 @@ void RefSolver::poison_cell(int gi, int j) { cs.J.at(gi, j).S[I_RHOE] = -1.0e30;
 
 void CpuSolver::upload() {
   h.from_field(cs.J, gi0 - l_off);
+  h.mech_from_case(cs, gi0 - l_off);
   compute_generic_flags(cs, h);
   sbuf = 0;
   dsbuf = 0;
@@ -632,6 +708,7 @@ void CpuSolver::upload() {
 void CpuSolver::download(Field& J) {
   if (lean_state) lean_materialize();
   h.to_field(J, gi0 - l_off, l_off, l_off + (gi1 - gi0), pbuf, dsbuf);
+  h.mech_to_case(cs, gi0 - l_off, l_off, l_off + (gi1 - gi0), 0);
 }
 
 LeanSoA CpuSolver::lean_view(bool fromg) {
@@ -681,10 +758,11 @@ void CpuSolver::lean_materialize() {
 }
 
 int CpuSolver::halo_doubles(int g) const {
-  if (g == HALO_MID) return NEQ;
+  const int ns = h.nsp, sdx = h.dSdxs[0].empty() ? 0 : 1;
+  if (g == HALO_MID) return NEQ + ns;
   if (g == HALO_QDIR) return 4;
   if (g == HALO_LEAN) return 4 + 2 * NCOMP + 3 + NEQ;
-  return 4 * NEQ + 5;
+  return 4 * NEQ + 5 + ns * (3 + sdx);
 }
 
 void CpuSolver::pack_column(int g, int li, real* o) const {
@@ -694,6 +772,7 @@ void CpuSolver::pack_column(int g, int li, real* o) const {
     const long idx = (long)li * ny + j;
     if (g == HALO_MID) {
       for (int k = 0; k < NEQ; k++) *o++ = h.S[1][k * N + idx];
+      for (int sp = 0; sp < h.nsp; sp++) *o++ = h.Ys[1][sp * N + idx];
     } else if (g == HALO_QDIR) {
       for (int d = 0; d < 4; d++) *o++ = h.qdir[d * N + idx];
     } else if (g == HALO_LEAN) {
@@ -715,6 +794,12 @@ void CpuSolver::pack_column(int g, int li, real* o) const {
       *o++ = h.Tg[pbuf][idx];
       *o++ = h.lam[idx];
       *o++ = h.lam_t[idx];
+      for (int sp = 0; sp < h.nsp; sp++) {
+        *o++ = h.Ys[0][sp * N + idx];
+        *o++ = h.As[sp * N + idx];
+        *o++ = h.Bs[sp * N + idx];
+        if (!h.dSdxs[0].empty()) *o++ = h.dSdxs[dsbuf][sp * N + idx];
+      }
     }
   }
 }
@@ -726,6 +811,7 @@ void CpuSolver::unpack_column(int g, int li, const real* o) {
     const long idx = (long)li * ny + j;
     if (g == HALO_MID) {
       for (int k = 0; k < NEQ; k++) h.S[1][k * N + idx] = *o++;
+      for (int sp = 0; sp < h.nsp; sp++) h.Ys[1][sp * N + idx] = *o++;
     } else if (g == HALO_QDIR) {
       for (int d = 0; d < 4; d++) h.qdir[d * N + idx] = *o++;
     } else if (g == HALO_LEAN) {
@@ -747,6 +833,12 @@ void CpuSolver::unpack_column(int g, int li, const real* o) {
       h.Tg[pbuf][idx] = *o++;
       h.lam[idx] = *o++;
       h.lam_t[idx] = *o++;
+      for (int sp = 0; sp < h.nsp; sp++) {
+        h.Ys[0][sp * N + idx] = *o++;
+        h.As[sp * N + idx] = *o++;
+        h.Bs[sp * N + idx] = *o++;
+        if (!h.dSdxs[0].empty()) h.dSdxs[dsbuf][sp * N + idx] = *o++;
+      }
     }
   }
 }
@@ -829,22 +921,45 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
   }
   if (lean_state) lean_materialize();
   // predict: S[0] -> S[1], dS[dsbuf] -> dS[1-dsbuf]
+  const bool mech = h.mech != nullptr;
   SoA in = h.view(0, dsbuf, pbuf);
   SoA mid = h.view(1, 1 - dsbuf, pbuf);
   // halo columns keep their (exchanged) values in the mid buffer as well
   for (int i = P.i0; i < P.i1; i++)
-    for (int j = 0; j < P.ny; j++) predict_cell(P, in, mid, i, j, want_res ? &r.res : nullptr);
+    for (int j = 0; j < P.ny; j++) {
+      if (mech) {
+        if (want_res)
+          predict_cell_t<true, SK_MECH>(P, in, mid, i, j, r.res);
+        else {
+          ResidualPack d;
+          predict_cell_t<false, SK_MECH>(P, in, mid, i, j, d);
+        }
+      } else {
+        predict_cell(P, in, mid, i, j, want_res ? &r.res : nullptr);
+      }
+    }
   r.have_residual = want_res;
   if (halo_exchange && P.sm == SM_NS) halo_exchange(*this, HALO_MID);
+  if (mech) {
+    // operator-split kinetics: Ys[1] -> Ys[0] (N-S strips also react the
+    // exchanged ghost columns: same inputs, same result as their owner)
+    SoA co = h.view(0, 1 - dsbuf, pbuf);
+    const int ci0 = (halo_exchange && P.sm == SM_NS) ? 0 : P.i0;
+    const int ci1 = (halo_exchange && P.sm == SM_NS) ? P.nx : P.i1;
+    for (int i = ci0; i < ci1; i++)
+      for (int j = 0; j < P.ny; j++) mech_chem_soa_cell<MECH_MAXSP>(P, mid, co, h.Tg[pbuf].data(), i, j);
+  }
   // fill: S[1] (+nbrs) -> S[0]; prims pbuf -> 1-pbuf
   SoA sin = h.view(1, 1 - dsbuf, pbuf);
-  SoA pold = h.view(1, 1 - dsbuf, pbuf);
+  if (mech) h.mech_view(sin, 0, 1 - dsbuf);   // post-chemistry species
+  SoA pold = sin;
   SoA out = h.view(0, 1 - dsbuf, 1 - pbuf);
   int negT = 0;
   real dtmin = 1.0;
   for (int i = P.i0; i < P.i1; i++)
     for (int j = 0; j < P.ny; j++) {
-      const real d = fill_cell(P, sin, pold, out, i, j, &negT, true);
+      const real d = mech ? fill_cell<SK_MECH, MECH_MAXSP>(P, sin, pold, out, i, j, &negT, true)
+                          : fill_cell(P, sin, pold, out, i, j, &negT, true);
       dtmin = std::min(dtmin, d);
     }
   dsbuf = 1 - dsbuf;
@@ -876,7 +991,11 @@ void CpuSolver::cycle_update() {
 // ---------------------------------------------------------------------------
 // RefSolver: in-place reference-order sweep (deeps2d_core.cpp:853-1334)
 // ---------------------------------------------------------------------------
-RefSolver::RefSolver(Case& c) : SolverBase(c) { core.resize(c.J.c.size()); }
+RefSolver::RefSolver(Case& c) : SolverBase(c) {
+  if (c.cfg.mech_mode())
+    throw std::runtime_error("the reference-order backend has no mechanism mode (the reference has no detailed kinetics)");
+  core.resize(c.J.c.size());
+}
 
 StepResult RefSolver::do_step(const StepParams& P, bool /*want_res*/) {
   Field& J = cs.J;

@@ -44,12 +44,22 @@ struct HostArrays {
   std::vector<uint8_t> gf;  // GF_* traffic flags (compute_generic_flags)
   std::vector<int32_t> iw, jw;
   std::vector<real> time;   // per-cell record time (checkpoint only)
+  // mechanism mode (SK_MECH): species block, species-major [s * N + idx]
+  int nsp = 0;
+  const MechData* mech = nullptr;
+  std::vector<real> Ys[2], As, Bs, Fs, betas, dSdxs[2], dSdys[2];
+  void allocate_mech(const Case& cs);
+  // species of columns [gi0, gi0 + nx) from Case::mech_rhoY (fluxes: inviscid)
+  void mech_from_case(const Case& cs, int gi0);
+  void mech_to_case(Case& cs, int gi0, int i_from, int i_to, int ybuf) const;
 
   void allocate(int X, int Y);
   // columns [gi0, gi0 + X) of J
   void from_field(const Field& J, int gi0);
   void to_field(Field& J, int gi0, int i_from, int i_to, int prim_buf, int ds_buf) const;
   SoA view(int sbuf, int dsbuf, int pbuf);
+  // sets the species members of a view (ybuf: species state buffer)
+  void mech_view(SoA& s, int ybuf, int dsbuf) const;
 };
 
 // Communication hooks for multi-rank (strip) runs.  Single-rank: no-ops.
@@ -155,6 +165,7 @@ bool lean_eligible(const Case& cs, std::string* why);
 bool lean_single_gas(const Case& cs);
 int sk_eligible(const Case& cs, std::string* why);   // SK_* mode of the split kernels
 bool lean_any_cauchy_x(const Case& cs);
+bool mech_species_cauchy(const Case& cs);   // some node applies d2(rhoY)/dx2 or /dy2 = 0
 // per-cell GF_* flags of the generic stepper (from the uploaded host arrays)
 void compute_generic_flags(const Case& cs, HostArrays& h);
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);

@@ -16,6 +16,7 @@
 #pragma once
 
 #include "physics.hpp"
+#include "mechanism.hpp"
 #include "residual.hpp"
 
 namespace hf2d {
@@ -77,6 +78,17 @@ struct SoA {
   uint8_t* gf = nullptr;   // GF_* flags (nullptr: all set)
   int32_t* iw = nullptr;
   int32_t* jw = nullptr;
+  // mechanism mode (SK_MECH): species partial densities and their fluxes,
+  // blending factors and Cauchy dS, species-major [s * N + idx]
+  const MechData* mech = nullptr;
+  int nsp = 0;
+  real* Ys = nullptr;
+  real* As = nullptr;
+  real* Bs = nullptr;
+  real* Fs = nullptr;
+  real* betas = nullptr;
+  real* dSdxs = nullptr;   // nullptr unless some node applies d2(rhoY)/dx2 = 0
+  real* dSdys = nullptr;
 };
 
 enum { G_DUDX = 0, G_DUDY, G_DVDX, G_DVDY, G_DTDX, G_DTDY, G_DKDX, G_DKDY, G_DEDX, G_DEDY, NGRAD };
@@ -222,9 +234,12 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
   const int Num_Eq = PLAIN ? NEQ : num_eq_for(TT);
   const bool axi = P.fpa.FT != 0;
 #pragma unroll
-  for (int k = 0; k < IO::NE; k++) {
-    if (IO::skip(k)) continue;   // equation not stored by this accessor (single-gas species)
-    real s = io.S(k);
+  for (int kk = 0; kk < IO::NE; kk++) {
+    if (IO::skip(kk)) continue;   // equation not stored by this accessor (single-gas species)
+    // k: the reference equation whose BC masks / residual slot apply (the
+    // mechanism species accessor maps every species to the species group)
+    const int k = io.eq(kk);
+    real s = io.S(kk);
     const EqFlags f = PLAIN ? EqFlags{true, true, true, false, false} : eq_flags(k, CT, TT, P.sm);
     if (!PLAIN &&
         (k >= Num_Eq || !f.upd || (k >= 4 + NCOMP && !(P.sm == SM_NS && has_turb_eq(TT))))) {
@@ -233,10 +248,10 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
       // predictor scratch (0) in the reference: DD = 1, dS = -S.
       if (k < Num_Eq && !f.upd && k >= 4 + NCOMP && P.sm == SM_NS && has_turb_eq(TT) &&
           !pass2_frozen(k, CT, TT, P.sm) && s != 0.) {
-        const real beta = io.beta(k);
+        const real beta = io.beta(kk);
         const real DD = 1.0;
         const real bmin = has_all(CT, CT_NONREFLECTED) ? P.nrbc_beta0 : P.beta_min;
-        io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, 1.0));
+        io.put_beta(kk, blend_beta(P.bff, bmin, beta, DD, 1.0));
         if (RES) {
           EqResidual& e = rp.eq[k];
           if (DD >= e.dd_max) {
@@ -253,40 +268,40 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
           }
         }
       }
-      io.put_S(k, s);
-      io.keep_dS(k);
+      io.put_S(kk, s);
+      io.keep_dS(kk);
       continue;
     }
     real dXX, dYY, dsdx, dsdy;
     if (f.dx) {
-      dXX = dsdx = (io.AR(k) - io.AL(k)) * n_n_1;
+      dXX = dsdx = (io.AR(kk) - io.AL(kk)) * n_n_1;
     } else {
       // a missing neighbour resolves to the cell itself
-      const real sL = n1 ? io.SL(k) : s, sR = n2 ? io.SR(k) : s;
+      const real sL = n1 ? io.SL(kk) : s, sR = n2 ? io.SR(kk) : s;
       s = (sL * n2 + sR * n1) * n_n_1;
       dXX = dsdx = 0.;
     }
     if (f.dy) {
-      dYY = dsdy = (io.BU(k) - io.BD(k)) * m_m_1;
+      dYY = dsdy = (io.BU(kk) - io.BD(kk)) * m_m_1;
     } else {
-      const real sU = n3 ? io.SU(k) : s, sD = n4 ? io.SD(k) : s;
+      const real sU = n3 ? io.SU(kk) : s, sD = n4 ? io.SD(kk) : s;
       s = (sU * n3 + sD * n4) * m_m_1;
       dYY = dsdy = 0.;
     }
-    if (f.dx2) dXX = (io.dxL(k) + io.dxR(k)) * 0.5;
-    if (f.dy2) dYY = (io.dyU(k) + io.dyD(k)) * 0.5;
-    const real SL = n1 ? io.SL(k) : s, SR = n2 ? io.SR(k) : s;
-    const real SU = n3 ? io.SU(k) : s, SD = n4 ? io.SD(k) : s;
-    const real beta = io.beta(k);
+    if (f.dx2) dXX = (io.dxL(kk) + io.dxR(kk)) * 0.5;
+    if (f.dy2) dYY = (io.dyU(kk) + io.dyD(kk)) * 0.5;
+    const real SL = n1 ? io.SL(kk) : s, SR = n2 ? io.SR(kk) : s;
+    const real SU = n3 ? io.SU(kk) : s, SD = n4 ? io.SD(kk) : s;
+    const real beta = io.beta(kk);
     const real _beta = 1. - beta;
     real snew;
     if (axi)
       snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 -
-             (P.dtdx * dXX + P.dtdy * (dYY + io.F(k) / (j + 1))) + (io.Src(k)) * P.dt + io.SrcAdd(k);
+             (P.dtdx * dXX + P.dtdy * (dYY + io.F(kk) / (j + 1))) + (io.Src(kk)) * P.dt + io.SrcAdd(kk);
     else
       snew = s * beta + _beta * (P.dxx * (SL + SR) + P.dyy * (SU + SD)) * 0.5 - (P.dtdx * dXX + P.dtdy * dYY) +
-             (io.Src(k)) * P.dt + io.SrcAdd(k);
-    io.put_dS(k, dsdx, dsdy);
+             (io.Src(kk)) * P.dt + io.SrcAdd(kk);
+    io.put_dS(kk, dsdx, dsdy);
     // pass 2a: residual + blending factor
     if ((PLAIN || !pass2_frozen(k, CT, TT, P.sm)) && s != 0.) {
       const real absDD = snew - s;
@@ -299,7 +314,7 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
         DD = 1.0;
       }
       const real bmin = (!PLAIN && has_all(CT, CT_NONREFLECTED)) ? P.nrbc_beta0 : P.beta_min;
-      io.put_beta(k, blend_beta(P.bff, bmin, beta, DD, sqrt_res));
+      io.put_beta(kk, blend_beta(P.bff, bmin, beta, DD, sqrt_res));
       if (RES) {
         EqResidual& e = rp.eq[k];
         if (DD >= e.dd_max) {
@@ -316,7 +331,7 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
         }
       }
     }
-    io.put_S(k, snew);
+    io.put_S(kk, snew);
   }
 }
 
@@ -327,9 +342,11 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
 // Species partial densities are +0 and stay so in both specialisations (the
 // argument of the lean single-gas path), so their equations, fluxes, mixture
 // fractions and R need not move through memory (sk_eligible on the host).
-enum { SK_GENERIC = 0, SK_SGL = 1, SK_SGT = 2 };
+//   SK_MECH     mechanism mode: equations 0..3, 7, 8 of the record (its species
+//               slots are 0) + the mechanism species block (SoA::Ys)
+enum { SK_GENERIC = 0, SK_SGL = 1, SK_SGT = 2, SK_MECH = 3 };
 HF_HD constexpr bool sk_live(int mode, int k) {
-  return mode == SK_GENERIC || k < 4 || (mode == SK_SGT && k >= 4 + NCOMP);
+  return mode == SK_GENERIC || k < 4 || ((mode == SK_SGT || mode == SK_MECH) && k >= 4 + NCOMP);
 }
 
 // Accessor over the full SoA arrays (fluxes loaded).
@@ -337,6 +354,7 @@ template <int MODE = SK_GENERIC>
 struct SoAPredictIO {
   static constexpr int NE = MODE == SK_SGL ? 4 : NEQ;
   static constexpr bool skip(int k) { return !sk_live(MODE, k); }
+  HF_HD static constexpr int eq(int k) { return k; }
   const SoA& in;
   const SoA& out;
   long N, idx, iL, iR, iU, iD;
@@ -370,6 +388,51 @@ struct SoAPredictIO {
   uint8_t gf = 0xff;
 };
 
+// Accessor over one species s of the mechanism block (SK_MECH): the
+// reference's species-group BC masks and residual slot (I_YFU); no volume
+// source (the kinetics are operator-split), the no-slip wall source of the
+// species is SrcAdd_rho * Y_s like the reference's slots
+// (hyper_flow_node.hpp FillNode2D, SrcAdd[4+i] = SrcAdd[0] * Y[i]).
+struct SpeciesPredictIO {
+  static constexpr int NE = 1;
+  static constexpr bool skip(int) { return false; }
+  HF_HD static constexpr int eq(int) { return I_YFU; }
+  const SoA& in;
+  const SoA& out;
+  long N, idx, iL, iR, iU, iD;
+  uint8_t gf;
+  long o;   // s * N
+  HF_HD real S(int) const { return in.Ys[o + idx]; }
+  HF_HD real SL(int) const { return in.Ys[o + iL]; }
+  HF_HD real SR(int) const { return in.Ys[o + iR]; }
+  HF_HD real SU(int) const { return in.Ys[o + iU]; }
+  HF_HD real SD(int) const { return in.Ys[o + iD]; }
+  HF_HD real AL(int) const { return in.As[o + iL]; }
+  HF_HD real AR(int) const { return in.As[o + iR]; }
+  HF_HD real BU(int) const { return in.Bs[o + iU]; }
+  HF_HD real BD(int) const { return in.Bs[o + iD]; }
+  HF_HD real dxL(int) const { return in.dSdxs ? in.dSdxs[o + iL] : 0.0; }
+  HF_HD real dxR(int) const { return in.dSdxs ? in.dSdxs[o + iR] : 0.0; }
+  HF_HD real dyU(int) const { return in.dSdys ? in.dSdys[o + iU] : 0.0; }
+  HF_HD real dyD(int) const { return in.dSdys ? in.dSdys[o + iD] : 0.0; }
+  HF_HD real beta(int) const { return in.betas[o + idx]; }
+  HF_HD real F(int) const { return in.Fs[o + idx]; }
+  HF_HD real Src(int) const { return 0.0; }
+  HF_HD real SrcAdd(int) const {
+    return (gf & GF_SRCADD) ? in.SrcAdd[(long)I_RHO * N + idx] * (in.Ys[o + idx] / in.S[idx]) : 0.0;
+  }
+  HF_HD void put_S(int, real v) const { out.Ys[o + idx] = v; }
+  HF_HD void put_beta(int, real v) const { out.betas[o + idx] = v; }
+  HF_HD void put_dS(int, real a, real b) const {
+    if ((gf & GF_DX_OUT) && out.dSdxs) out.dSdxs[o + idx] = a;
+    if ((gf & GF_DY_OUT) && out.dSdys) out.dSdys[o + idx] = b;
+  }
+  HF_HD void keep_dS(int) const {
+    if ((gf & GF_DX_OUT) && out.dSdxs) out.dSdxs[o + idx] = in.dSdxs[o + idx];
+    if ((gf & GF_DY_OUT) && out.dSdys) out.dSdys[o + idx] = in.dSdys[o + idx];
+  }
+};
+
 template <bool RES, int MODE = SK_GENERIC>
 HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
                                  ResidualPack& res) {
@@ -384,14 +447,34 @@ HF_HD inline void predict_cell_t(const StepParams& P, const SoA& in, const SoA& 
       if (gf & GF_DX_OUT) out.dSdx[k * N + idx] = in.dSdx[k * N + idx];
       if (gf & GF_DY_OUT) out.dSdy[k * N + idx] = in.dSdy[k * N + idx];
     }
+    if (MODE == SK_MECH)
+      for (int s = 0; s < in.nsp; s++) {
+        const long o = (long)s * N + idx;
+        out.Ys[o] = in.Ys[o];
+        if ((gf & GF_DX_OUT) && out.dSdxs) out.dSdxs[o] = in.dSdxs[o];
+        if ((gf & GF_DY_OUT) && out.dSdys) out.dSdys[o] = in.dSdys[o];
+      }
     return;
   }
   const u64 TT = in.TT[idx];
   const uint8_t nbm = in.nb[idx];
   const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
   const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-  SoAPredictIO<MODE> io{in, out, N, idx, (long)(i - n1) * P.ny + j, (long)(i + n2) * P.ny + j, idx + n3, idx - n4, gf};
+  const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j;
+  SoAPredictIO<MODE> io{in, out, N, idx, iL, iR, idx + n3, idx - n4, gf};
   predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
+  if (MODE == SK_MECH) {
+    // transported species, then the bath gas as the remainder of the new rho
+    const int bath = in.mech->bath;
+    real sum = 0.0;
+    for (int s = 0; s < in.nsp; s++) {
+      if (s == bath) continue;
+      SpeciesPredictIO sio{in, out, N, idx, iL, iR, idx + n3, idx - n4, gf, (long)s * N};
+      predict_core<RES>(P, sio, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, res);
+      sum += out.Ys[(long)s * N + idx];
+    }
+    out.Ys[(long)bath * N + idx] = out.S[idx] - sum;
+  }
 }
 
 HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& out, int i, int j,
@@ -417,13 +500,50 @@ HF_HD inline void predict_cell(const StepParams& P, const SoA& in, const SoA& ou
 // fields); chemistry reduces to chemistry_single_gas_ns(); output-only fields
 // (SGL: Diff, grad) are written when store_grad (the host reads the record
 // after this step).  Every field equals the generic path (GPU tests).
-template <int MODE = SK_GENERIC>
+// Mechanism-mode mixture closure of fill_node (physics.hpp RefMix): T from
+// rho*E by Newton on the thermally perfect e(T) of the current composition,
+// then R, Cp, k = Cp/Cv and p = rho R T at that T; the species enthalpy
+// diffusion term uses the absolute species enthalpies h_s(T).
+template <int NSB>
+struct MechMix {
+  static constexpr bool MECH = true;
+  const MechData* m;
+  const real* Y;    // mass fractions
+  const real* gx;   // d(rho Y_s)/dx, d(rho Y_s)/dy
+  const real* gy;
+  template <class N>
+  HF_HD void state(N& n) const {
+    const real rho = n.S[I_RHO];
+    const real e = (n.S[I_RHOE] - rho * (n.U * n.U + n.V * n.V) * 0.5) / rho;
+    const real T = mech_T_from_e<NSB>(*m, Y, e, n.Tg);
+    real ee, cv, R, cp;
+    mech_mix_thermo<NSB>(*m, Y, T, &ee, &cv, &R, &cp);
+    n.Tg = T;
+    n.R = R;
+    n.CP = cp;
+    n.k = cp / cv;
+    n.p = rho * R * T;
+  }
+  template <class N>
+  HF_HD void heat_flux(const N& n, real& qx, real& qy) const {
+#pragma unroll
+    for (int s = 0; s < NSB; s++) {
+      if (s >= m->ns) break;
+      const real h = mech_h_species(*m, s, n.Tg);
+      qx += n.Diff * h * gx[s];
+      qy += n.Diff * h * gy[s];
+    }
+  }
+};
+
+template <int MODE = SK_GENERIC, int NSB = 1>
 HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
                             int* neg_T, bool store_grad) {
   const long N = sin.N;
   const long idx = (long)i * P.ny + j;
   const u64 CT = sin.CT[idx];
-  constexpr bool SGL = MODE == SK_SGL, SG = MODE != SK_GENERIC;
+  constexpr bool MECH = MODE == SK_MECH;
+  constexpr bool SGL = MODE == SK_SGL, SG = MODE == SK_SGL || MODE == SK_SGT;
   CellLocal c;
   for (int k = 0; k < NEQ; k++) c.S[k] = sk_live(MODE, k) ? sin.S[k * N + idx] : 0.0;
   if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
@@ -483,6 +603,16 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     c.Y[s] = SG ? (s == NCOMP ? 1.0 : 0.0) : sin.Y[s * N + idx];
     c.droYdx[s] = c.droYdy[s] = 0;
   }
+  // mechanism species: mass fractions and d(rho Y_s)/dx,y (active viscous nodes)
+  real mY[MECH ? NSB : 1], mgx[MECH ? NSB : 1], mgy[MECH ? NSB : 1];
+  if (MECH) {
+    const real rho = c.S[I_RHO];
+#pragma unroll
+    for (int s = 0; s < (MECH ? NSB : 1); s++) {
+      mY[s] = (s < sin.nsp && rho != 0) ? sin.Ys[(long)s * N + idx] / rho : 0.0;
+      mgx[s] = mgy[s] = 0.0;
+    }
+  }
   if (!(active && ns)) {   // velocity/temperature gradients are recomputed below for active viscous nodes
     c.dUdx = sin.grad[G_DUDX * N + idx];
     c.dUdy = sin.grad[G_DUDY * N + idx];
@@ -513,7 +643,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
     // SGL: species partial densities are +0, so aR - 0 - 0 - 0 == aR and the
     // species gradients are (0 - 0) * d == +0
-    for (int k = 4; k < (SG ? 4 : 4 + NCOMP); k++) {
+    for (int k = 4; k < ((SG || MECH) ? 4 : 4 + NCOMP); k++) {
       const long o = k * N;
       if (!nx0) {
         c.droYdx[k - 4] = (sin.S[o + iR] - sin.S[o + iL]) * dx_1_n;
@@ -528,6 +658,15 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     }
     if (!nx0) c.droYdx[NCOMP] = (aR - aL) * dx_1_n;
     if (!ny0) c.droYdy[NCOMP] = (aU - aD) * dy_1_m;
+    if (MECH) {
+#pragma unroll
+      for (int s = 0; s < (MECH ? NSB : 1); s++) {
+        if (s >= sin.nsp) break;
+        const long o = (long)s * N;
+        if (!nx0) mgx[s] = (sin.Ys[o + iR] - sin.Ys[o + iL]) * dx_1_n;
+        if (!ny0) mgy[s] = (sin.Ys[o + iU] - sin.Ys[o + iD]) * dy_1_m;
+      }
+    }
     const real* Uo = prim_old.U;
     const real* Vo = prim_old.V;
     const real rho = c.S[I_RHO];
@@ -574,11 +713,19 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     fp.is_mu_t = P.ffc.is_mu_t;
     fp.is_init = P.ffc.is_init;
   }
-  const bool filled = fill_node(c, fp);
+  bool filled;
+  if (MECH) {
+    MechMix<NSB> mx{sin.mech, mY, mgx, mgy};
+    filled = fill_node(c, fp, mx);
+  } else {
+    filled = fill_node(c, fp);
+  }
 
   real dt_local = 1.0;
   if (active) {
-    if (c.Tg < 0.) {
+    // mechanism mode: the Newton clamps T at MECH_TMIN; reaching it (or NaN)
+    // means the energy is unphysical
+    if (c.Tg < 0. || (MECH && !(c.Tg > MECH_TMIN))) {
       if (neg_T) *neg_T = 1;
     } else {
       const real AAA = std::sqrt(c.k * c.R * c.Tg);
@@ -587,7 +734,12 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
         const real nu_eff = (c.mu + c.mu_t) / c.S[I_RHO];
         if (nu_eff > 0) dt_local = hf_min(dt_local, P.visc_cfl / (nu_eff * (1.0 / (P.dx * P.dx) + 1.0 / (P.dy * P.dy))));
       }
-      if (SG) {
+      if (MECH) {
+        // mixture transport at the new T (the reference's lagged update) and
+        // the Tecplot slot fractions
+        mech_transport<NSB>(*sin.mech, mY, c.Tg, &c.mu, &c.lam);
+        mech_slot_fractions(*sin.mech, mY, c.Y);
+      } else if (SG) {
         if (P.chem_model != NO_REACTIONS) chemistry_single_gas_ns(c, *P.species);
       } else {
         if (P.chem_model != NO_REACTIONS) chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
@@ -606,6 +758,30 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     }
     if ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) out.Src[k * N + idx] = c.Src[k];
     if (gf & GF_SRCADD) out.SrcAdd[k * N + idx] = c.SrcAdd[k];
+  }
+  if (MECH && filled) {
+    // species fluxes: inviscid, Le = 1 diffusion with Diff (the reference's
+    // slot fluxes), axisymmetric F (N-S flat: F = 0)
+    const bool nsv = P.sm == SM_NS;
+    const int bath = sin.mech->bath;
+#pragma unroll
+    for (int s = 0; s < (MECH ? NSB : 1); s++) {
+      if (s >= sin.nsp) break;
+      if (s == bath) continue;
+      const long o = (long)s * N + idx;
+      const real rys = sin.Ys[o];
+      real a = rys * c.U, b = rys * c.V;
+      real f = axi ? (real)P.fpa.FT * b : 0.0;
+      if (nsv) {
+        const real rx = c.Diff * mgx[s], ry = c.Diff * mgy[s];
+        a -= rx;
+        b -= ry;
+        f = axi ? f - ry : 0.0;
+      }
+      out.As[o] = a;
+      out.Bs[o] = b;
+      if (axi) out.Fs[o] = f;
+    }
   }
   out.U[idx] = c.U;
   out.V[idx] = c.V;
@@ -639,6 +815,33 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     out.grad[G_DEDY * N + idx] = c.depsdy;
   }
   return dt_local;
+}
+
+// Operator-split kinetics of one cell (mechanism mode): the predicted species
+// mid.Ys -> out.Ys at constant rho and e over the step's dt.  Inactive
+// cells, cells colder than MechData::Tchem (by the previous step's T) and
+// dt = 0 copy through.  Runtime mechanism data: the host path of the device
+// kernels (chem_fast.hip / chem_mech.hip).
+template <int NSB>
+HF_HD inline void mech_chem_soa_cell(const StepParams& P, const SoA& mid, const SoA& out, const real* Tprev, int i,
+                                     int j) {
+  const long N = mid.N;
+  const long idx = (long)i * P.ny + j;
+  const MechData& m = *mid.mech;
+  const real rho = mid.S[idx];
+  const bool react = is_active(mid.CT[idx]) && rho > 0 && Tprev[idx] >= m.Tchem && P.dt > 0;
+  real rhoY[NSB];
+#pragma unroll
+  for (int s = 0; s < NSB; s++) rhoY[s] = s < m.ns ? mid.Ys[(long)s * N + idx] : 0.0;
+  if (react) {
+    const real ru = mid.S[(long)I_RHOU * N + idx], rv = mid.S[(long)I_RHOV * N + idx];
+    const real e = (mid.S[(long)I_RHOE * N + idx] - 0.5 * (ru * ru + rv * rv) / rho) / rho;
+    real T = Tprev[idx];
+    mech_chem_cell<NSB>(m, rho, e, rhoY, &T, P.dt, m.nsub);
+  }
+#pragma unroll
+  for (int s = 0; s < NSB; s++)
+    if (s < m.ns) out.Ys[(long)s * N + idx] = rhoY[s];
 }
 
 }  // namespace hf2d

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
   }
 }
 
-template <int MODE = SK_GENERIC>
+template <int MODE = SK_GENERIC, int NSB = 1>
 __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
                                                     DevScalars* sc, int slot, int slot_next, int serial,
                                                     int store_grad) {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA po
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    dtl = fill_cell<MODE>(P, sin, pold, out, i, j, &neg, store_grad != 0);
+    dtl = fill_cell<MODE, NSB>(P, sin, pold, out, i, j, &neg, store_grad != 0);
   }
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
   __shared__ double sdt[BLOCK / WAVE];
@@ -198,6 +198,20 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA po
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
+// Mechanism mode, operator-split kinetics (runtime mechanism data; the
+// per-cell point-implicit integrator of mechanism.hpp): predicted species
+// mid.Ys -> out.Ys over the step's dt at constant rho and e.
+template <int NSB>
+__global__ __launch_bounds__(BLOCK) void hf2d_chem_generic(StepParams P, SoA mid, SoA out, const real* Tprev, long c0,
+                                                            long c1, DevScalars* sc, int slot) {
+  apply_dt(P, sc, slot);
+  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  if (c < c1) {
+    const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
+    mech_chem_soa_cell<NSB>(P, mid, out, Tprev, i, j);
   }
 }
 
@@ -301,8 +315,9 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
 }
 
 // Halo pack: nf field columns (each ny contiguous doubles at src[f] + col*ny)
+constexpr int MAX_HALO_FIELDS = 128;   // 4*NEQ + 5 state fields + up to 16 species x 4
 struct ColList {
-  real* f[48];
+  real* f[MAX_HALO_FIELDS];
   int nf;
 };
 constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
@@ -1092,6 +1107,11 @@ struct DeviceSolver::Impl {
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   int32_t *iw, *jw;
+  // mechanism mode (SK_MECH): species block, Ys ping-pongs with S (sbuf)
+  MechData* mech = nullptr;
+  int nsp = 0;
+  real *Ys[2] = {nullptr, nullptr}, *As = nullptr, *Bs = nullptr, *Fs = nullptr, *betas = nullptr;
+  real *dSdxs[2] = {nullptr, nullptr}, *dSdys[2] = {nullptr, nullptr};
   SpeciesProps* species = nullptr;
   ScenarioTables* scen = nullptr;
   long* probe_idx = nullptr;   // K8 monitor probes (sample_monitors)
@@ -1198,7 +1218,20 @@ struct DeviceSolver::Impl {
     s.gf = gf;
     s.iw = iw;
     s.jw = jw;
+    mech_view(s, sb, db);
     return s;
+  }
+  void mech_view(SoA& s, int yb, int db) const {
+    s.mech = mech;
+    s.nsp = nsp;
+    if (!mech) return;
+    s.Ys = Ys[yb];
+    s.As = As;
+    s.Bs = Bs;
+    s.Fs = Fs;
+    s.betas = betas;
+    s.dSdxs = dSdxs[db];
+    s.dSdys = dSdys[db];
   }
 };
 
@@ -1272,6 +1305,22 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.nb = m.mem.alloc<uint8_t>(N);
   m.iw = m.mem.alloc<int32_t>(N);
   m.jw = m.mem.alloc<int32_t>(N);
+  h.allocate_mech(c);
+  if (h.mech) {
+    m.nsp = h.nsp;
+    const long n = (long)m.nsp * N;
+    m.mech = m.mem.alloc<MechData>(1);
+    for (int b = 0; b < 2; b++) m.Ys[b] = m.mem.alloc<real>(n);
+    m.As = m.mem.alloc<real>(n);
+    m.Bs = m.mem.alloc<real>(n);
+    m.Fs = m.mem.alloc<real>(n);
+    m.betas = m.mem.alloc<real>(n);
+    if (!h.dSdxs[0].empty())
+      for (int b = 0; b < 2; b++) {
+        m.dSdxs[b] = m.mem.alloc<real>(n);
+        m.dSdys[b] = m.mem.alloc<real>(n);
+      }
+  }
   m.species = m.mem.alloc<SpeciesProps>(1);
   m.scen = m.mem.alloc<ScenarioTables>(1);
   m.sc = m.mem.alloc<DevScalars>(1);
@@ -1286,7 +1335,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
   m.res_out = m.mem.alloc<ResidualPack>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.res_host, sizeof(ResidualPack), hipHostMallocDefault));
-  m.halo_cap = (long)48 * h.ny;
+  m.halo_cap = (long)MAX_HALO_FIELDS * h.ny;
   for (int d = 0; d < 2; d++) {
     m.halo_send[d] = m.mem.alloc<real>(m.halo_cap);
     m.halo_recv[d] = m.mem.alloc<real>(m.halo_cap);
@@ -1378,6 +1427,21 @@ void DeviceSolver::upload() {
   cp(m.iw, h.iw.data(), N * sizeof(int32_t));
   cp(m.jw, h.jw.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
+  if (h.mech) {
+    h.mech_from_case(cs, gi0 - l_off);
+    const size_t YB = (size_t)m.nsp * N * sizeof(real);
+    cp(m.mech, h.mech, sizeof(MechData));
+    for (int b = 0; b < 2; b++) cp(m.Ys[b], h.Ys[0].data(), YB);
+    cp(m.As, h.As.data(), YB);
+    cp(m.Bs, h.Bs.data(), YB);
+    cp(m.Fs, h.Fs.data(), YB);
+    cp(m.betas, h.betas.data(), YB);
+    if (m.dSdxs[0])
+      for (int b = 0; b < 2; b++) {
+        cp(m.dSdxs[b], h.dSdxs[0].data(), YB);
+        cp(m.dSdys[b], h.dSdys[0].data(), YB);
+      }
+  }
   scen_host.cfl = cs.cfg.CFL_Scenario.pack();
   scen_host.beta = cs.cfg.beta_Scenario.pack();
   scen_host.CFL = cs.cfg.CFL;
@@ -1472,8 +1536,10 @@ void DeviceSolver::download(Field& J) {
   cp(h.Q_conv.data(), m.Q_conv, SB);
   cp(h.grad.data(), m.grad, NGRAD * SB);
   cp(h.CT.data(), m.CT, N * sizeof(u64));
+  if (h.mech) cp(h.Ys[0].data(), m.Ys[sbuf], (size_t)m.nsp * N * sizeof(real));
   HIP_CHECK(hipStreamSynchronize(st));
   h.to_field(J, gi0 - l_off, l_off, l_off + (gi1 - gi0), 0, 0);
+  h.mech_to_case(cs, gi0 - l_off, l_off, l_off + (gi1 - gi0), 0);
 }
 
 void DeviceSolver::on_cycle_roll() { time_offset = last_dev_time; }
@@ -1802,6 +1868,7 @@ void DeviceSolver::exchange(int group, int dt_slot) {
     if (lean_has_cauchy_x) add_eq(m.dSdx[dsbuf]);
   } else if (group == CpuSolver::HALO_MID) {
     add_eq(m.S[1 - sbuf]);
+    for (int q = 0; q < m.nsp; q++) L.f[L.nf++] = m.Ys[1 - sbuf] + (long)q * N;
   } else if (group == CpuSolver::HALO_QDIR) {
     for (int d = 0; d < 4; d++) L.f[L.nf++] = m.qdir + (long)d * N;
   } else {
@@ -1814,7 +1881,14 @@ void DeviceSolver::exchange(int group, int dt_slot) {
     L.f[L.nf++] = m.Tg[pbuf];
     L.f[L.nf++] = m.lam;
     L.f[L.nf++] = m.lam_t;
+    for (int q = 0; q < m.nsp; q++) {
+      L.f[L.nf++] = m.Ys[sbuf] + (long)q * N;
+      L.f[L.nf++] = m.As + (long)q * N;
+      L.f[L.nf++] = m.Bs + (long)q * N;
+      if (m.dSdxs[0]) L.f[L.nf++] = m.dSdxs[dsbuf] + (long)q * N;
+    }
   }
+  if (L.nf > MAX_HALO_FIELDS) throw std::runtime_error("halo: too many exchanged fields");
   const int cnt = L.nf * ny;
   const unsigned nb2 = (unsigned)((2 * cnt + BLOCK - 1) / BLOCK);
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
@@ -2233,7 +2307,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
     lean_state = 1;
-  } else if (euler && fused) {
+  } else if (euler && fused && !m.mech) {
     if (lean_state) lean_materialize();
     // Predictor and fill of a cell run back to back in one thread, so the
     // new state goes to the other S buffer (neighbours still read the old
@@ -2255,28 +2329,48 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (lean_state) lean_materialize();
     SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
     SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
-    // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT)
-    const int mode = (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+    // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
+    // mechanism mode: SK_MECH (Euler and N-S)
+    const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
 #define HF2D_PRED(R, M)                                                                                     \
   hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
                      serial, m.partials)
     if (want_res) {
       if (mode == SK_SGL) HF2D_PRED(true, SK_SGL);
       else if (mode == SK_SGT) HF2D_PRED(true, SK_SGT);
+      else if (mode == SK_MECH) HF2D_PRED(true, SK_MECH);
       else HF2D_PRED(true, SK_GENERIC);
     } else {
       if (mode == SK_SGL) HF2D_PRED(false, SK_SGL);
       else if (mode == SK_SGT) HF2D_PRED(false, SK_SGT);
+      else if (mode == SK_MECH) HF2D_PRED(false, SK_MECH);
       else HF2D_PRED(false, SK_GENERIC);
     }
 #undef HF2D_PRED
     HIP_CHECK(hipGetLastError());
+    const bool multi = (m.comm || m.local || m.p2p.on) && m.nranks > 1;
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
     SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
+    if (mode == SK_MECH) {
+      // operator-split kinetics: Ys[1-sbuf] -> Ys[sbuf]; N-S strips also react
+      // their ghost columns (exchanged above; same inputs as on the owner)
+      const bool ghosts = multi && P.sm == SM_NS;
+      const long k0 = ghosts ? 0 : c0, k1 = ghosts ? h.N : c1;
+      const unsigned nbk = (unsigned)((k1 - k0 + BLOCK - 1) / BLOCK);
+      launch_chem(P, sin, out, k0, k1, nbk, slot);
+      m.mech_view(sin, sbuf, 1 - dsbuf);   // the fill reads the post-chemistry species
+    }
     // SGL: gradients / Diff only when the host reads the record (or y+ follows)
     const int sg_out = (step_outputs || want_res) ? 1 : 0;
-    if (mode == SK_SGL)
+    if (mode == SK_MECH) {
+      if (m.nsp <= 9)
+        hipLaunchKernelGGL((hf2d_fill<SK_MECH, 9>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,
+                           slot, slot_next, serial, 1);
+      else
+        hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
+                           m.sc, slot, slot_next, serial, 1);
+    } else if (mode == SK_SGL)
       hipLaunchKernelGGL(hf2d_fill<SK_SGL>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
                          slot_next, serial, sg_out);
     else if (mode == SK_SGT)
@@ -2315,6 +2409,19 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     r.have_residual = true;
   }
   return r;
+}
+
+void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb,
+                               int slot) {
+  Impl& m = *impl;
+  const real* Tprev = m.Tg[pbuf];
+  if (m.nsp <= 9)
+    hipLaunchKernelGGL(hf2d_chem_generic<9>, dim3(nb), dim3(BLOCK), 0, m.stream, P, mid, out, Tprev, k0, k1, m.sc,
+                       slot);
+  else
+    hipLaunchKernelGGL(hf2d_chem_generic<MECH_MAXSP>, dim3(nb), dim3(BLOCK), 0, m.stream, P, mid, out, Tprev, k0, k1,
+                       m.sc, slot);
+  HIP_CHECK(hipGetLastError());
 }
 
 void DeviceSolver::synchronize() {

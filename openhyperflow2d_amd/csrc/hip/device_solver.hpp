@@ -148,6 +148,8 @@ class DeviceSolver : public SolverBase {
   std::unique_ptr<GraphCache> graph;
   std::vector<StepParams> pending;
   void run_graph();
+  // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
+  void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device);

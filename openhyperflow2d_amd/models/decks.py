@@ -507,5 +507,15 @@ def reactor0d(nx: int = 8, ny: int = 8, *, T: float = 1500.0, p: float = 1.0e5, 
     return t
 
 
+def with_mechanism(text: str, mechanism: str = "h2_air_li2004", substeps: int = 1, tmin: float = 300.0) -> str:
+    """Switch a deck to mechanism mode: detailed finite-rate kinetics
+    (ChemicalReactionsModel = 2 + Mechanism, new keys; the reference's
+    four species slots map to the mechanism species through its slot table)."""
+    t = set_key(text, "ChemicalReactionsModel", 2)
+    t = set_key(t, "Mechanism", mechanism)
+    t = set_key(t, "ChemSubsteps", substeps)
+    return set_key(t, "ChemTmin", tmin)
+
+
 GENERATORS = {"wedge15": wedge15, "step": step, "triple_point": triple_point, "resonator": resonator,
               "scramjet": scramjet, "reactor0d": reactor0d}

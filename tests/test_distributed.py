@@ -22,6 +22,10 @@ def _free_port():
     return p
 
 
+def _fields(text):
+    return FIELDS + (["Y:H2", "Y:O2", "Y:H2O", "Y:OH", "Y:N2"] if "<data/Mechanism=" in text else [])
+
+
 def _worker(rank, world, port, text, steps, lean, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -34,7 +38,7 @@ def _worker(rank, world, port, text, steps, lean, outdir):
         sim = DistributedSimulation(text, "cpu", rank=rank, world=world, lean=lean)
         for s in range(3):
             sim.step(steps, residual=(s != 1))
-        out = {f: sim.gather_field(f) for f in FIELDS}
+        out = {f.replace(":", "_"): sim.gather_field(f) for f in _fields(text)}
         summ = sim.summary()
         if rank == 0:
             np.savez(os.path.join(outdir, "res.npz"), dt=summ["dt"], time=summ["time"],
@@ -48,6 +52,9 @@ CASES = {
     "wedge15_euler": (lambda: decks.wedge15(90, 30, nmax=10 ** 6, nout=10 ** 5), 5),
     "wedge15_ns_keps": (lambda: decks.wedge15(90, 30, navier_stokes=True, turbulence=4, nmax=10 ** 6,
                                               nout=10 ** 5), 4),
+    # mechanism mode (species block + operator-split kinetics + SST)
+    "scramjet_mech": (lambda: decks.with_mechanism(decks.scramjet(120, 40, nmax=10 ** 6, nout=10 ** 5), substeps=2,
+                                                   tmin=250.0), 4),
 }
 
 
@@ -65,8 +72,8 @@ def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
     summ = ref.summary()
     assert float(got["dt"]) == summ["dt"]
     np.testing.assert_allclose(got["rms"], summ["rms"], rtol=1e-12, atol=0)
-    for f in FIELDS:
-        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+    for f in _fields(text):
+        np.testing.assert_array_equal(got[f.replace(":", "_")], ref.field(f), err_msg=f)
 
 
 def _run_worker(rank, world, port, text, outdir):
