@@ -24,7 +24,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("HF2D_OFFLOAD_ARCH", "gfx950")
 
 CORE_SRCS = ["deck.cpp", "gasdyn.cpp", "config.cpp", "preprocess.cpp", "checkpoint.cpp", "postproc.cpp", "solver.cpp", "lean.cpp", "mechanism.cpp"]
-HIP_SRCS = ["device_solver.hip", "chem_mech.hip"]
+HIP_SRCS = ["device_solver.hip", "chem_mech.hip", "chem_fast.hip"]
 
 
 def ext_path() -> str:

@@ -13,6 +13,7 @@
 #include "../core/postproc.hpp"
 #include "../core/solver.hpp"
 #include "../hip/chem_mech.hpp"
+#include "../hip/chem_fast.hpp"
 #include "../hip/device_solver.hpp"
 
 namespace py = pybind11;
@@ -471,6 +472,26 @@ PYBIND11_MODULE(_hf2d, m) {
     }
     return py::make_tuple(out, Tout);
   });
+  m.def("chem_fast_run", [](const std::string& name, py::array_t<double, py::array::c_style | py::array::forcecast> rhoY,
+                            py::array_t<double, py::array::c_style | py::array::forcecast> rho,
+                            py::array_t<double, py::array::c_style | py::array::forcecast> e,
+                            py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub,
+                            int repeats) {
+    // compiled-mechanism kinetics kernel on the GPU: returns (rhoY, T, mean ms)
+    const long n = (long)rho.size();
+    if (rhoY.ndim() != 2 || rhoY.shape(1) != n || e.size() != n || T.size() != n)
+      throw std::runtime_error("chem_fast_run: shapes [ns, n], [n], [n], [n]");
+    py::array_t<double> y({(long)rhoY.shape(0), n});
+    std::memcpy(y.mutable_data(), rhoY.data(), sizeof(double) * rhoY.size());
+    py::array_t<double> Tout(n);
+    std::memcpy(Tout.mutable_data(), T.data(), sizeof(double) * n);
+    double ms;
+    {
+      py::gil_scoped_release nogil;
+      ms = chem_fast_run_host(name, y.mutable_data(), rho.data(), e.data(), Tout.mutable_data(), n, dt, nsub, repeats);
+    }
+    return py::make_tuple(y, Tout, ms);
+  });
   m.def("mech_thermo_host", [](const std::string& name, std::vector<double> Y, double T) {
     auto mi = load_mechanism(name);
     double e, cv, R, cp, mu, lam;
@@ -523,6 +544,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_occ", &DeviceSolver::lean_occ)
       .def_readwrite("lean_wgcu", &DeviceSolver::lean_wgcu)
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
+      .def_readwrite("chem_fast", &DeviceSolver::chem_fast)
+      .def_readonly("chem_fast_ok", &DeviceSolver::chem_fast_ok)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
       .def_readwrite("lean_march", &DeviceSolver::lean_march)

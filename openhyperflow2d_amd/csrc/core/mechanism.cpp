@@ -235,6 +235,20 @@ std::shared_ptr<MechInfo> parse_mechanism(const std::string& text) {
   return info;
 }
 
+bool mech_same_kinetics(const MechData& a, const MechData& b) {
+  if (a.ns != b.ns || a.nr != b.nr || a.ntb != b.ntb) return false;
+  if (std::memcmp(a.W, b.W, sizeof a.W) || std::memcmp(a.a, b.a, sizeof a.a) || std::memcmp(a.Tmid, b.Tmid, sizeof a.Tmid) ||
+      std::memcmp(a.eff, b.eff, sizeof a.eff))
+    return false;
+  for (int r = 0; r < a.nr; r++)
+    if (std::memcmp(&a.rx[r], &b.rx[r], sizeof(MechReaction))) return false;
+  return true;
+}
+
+bool mech_is_builtin(const MechInfo& m, const std::string& builtin) {
+  return m.name == builtin && mech_same_kinetics(m.data, load_mechanism(builtin)->data);
+}
+
 std::shared_ptr<MechInfo> load_mechanism(const std::string& name, const std::string& workdir) {
   if (name == "h2_air_li2004" || name == "H2Air-Li2004" || name == "h2air") {
     auto m = parse_mechanism(MECH_H2_AIR_LI2004);

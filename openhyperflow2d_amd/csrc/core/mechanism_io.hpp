@@ -22,11 +22,15 @@ struct MechInfo {
   std::string name, source;
   std::vector<std::string> species;
   MechData data;
+  const MechData* data_ptr() const { return &data; }
 };
 
 std::shared_ptr<MechInfo> parse_mechanism(const std::string& text);
 // built-in name ("h2_air_li2004") or a *.mech path (relative to workdir first)
 std::shared_ptr<MechInfo> load_mechanism(const std::string& name, const std::string& workdir = "");
+// kinetics/thermo data identical (a file copy of a built-in mechanism may use its compiled kernel)
+bool mech_same_kinetics(const MechData& a, const MechData& b);
+bool mech_is_builtin(const MechInfo& m, const std::string& builtin);
 
 constexpr size_t SPECIES_HEADER = 8 + 16;
 size_t species_sidecar_bytes(int ns, int nx, int ny);

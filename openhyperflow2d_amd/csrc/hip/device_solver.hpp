@@ -127,6 +127,8 @@ class DeviceSolver : public SolverBase {
   void set_lean_plain(bool on);
   bool lean_ok = false;
   std::string lean_why;
+  bool chem_fast = true;  // mechanism mode: compiled-mechanism kinetics kernel when one exists
+  bool chem_fast_ok = false;   // the loaded mechanism equals a compiled one
   bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
   bool sgl_ok = false;
   int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)

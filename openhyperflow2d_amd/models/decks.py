@@ -334,10 +334,12 @@ def resonator(nx: int = 2000, ny: int = 200, *, nmax: int = 200, nout: int = 100
 
 
 def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100, project: Optional[str] = None,
-             exit_time: float = 1.0e-30, chemistry: int = 2, turbulence: int = 6) -> str:
+             exit_time: float = 1.0e-30, chemistry: int = 2, turbulence: int = 6,
+             mechanism: Optional[str] = "h2_air_li2004", substeps: int = 1) -> str:
     """Axisymmetric Mach-8 H2/air scramjet channel: converging inlet, constant
     area combustor with a wall H2 injection slot, straight to the outlet.
-    Finite-rate chemistry (ChemicalReactionsModel=2) and k-omega SST
+    Finite-rate chemistry (ChemicalReactionsModel=2 with the built-in
+    9-species / 21-step Li et al. H2/air mechanism, mechanism mode) and k-omega SST
     (TurbulenceModel=6, the default here) are new physics keys (not in the
     reference).  SST runs with point-implicit k/omega destruction and a
     free-stream eddy-viscosity ratio <= 10; tools/stability_probe.py shows the
@@ -424,6 +426,10 @@ def scramjet(nx: int = 6000, ny: int = 400, *, nmax: int = 200, nout: int = 100,
     t = set_key(t, "Area2.Flow2D", 3)
     t = set_key(t, "Area2.TurbulenceModel", 0)
     t = set_key(t, "Area2.MaterialID", 0)
+    if chemistry == 2 and mechanism:
+        # detailed kinetics (9 species / 21 reversible steps by default); the
+        # free stream (226 K) and the cold fuel jet do not react
+        t = with_mechanism(t, mechanism, substeps=substeps, tmin=600.0)
     return t
 
 
