@@ -125,30 +125,32 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
-  // K12 MFMA mechanism chemistry (csrc/hip/chem_mech.hip); rhoY is [ns][ncell], updated in place.
+  // K12 kinetics for runtime mechanisms on the MFMA cores (csrc/hip/chem_mech.hip): mechanism
+  // given as a built-in name or the text of a .mech file; returns (rhoY, T, mean ms)
   m.def(
       "chem_mech_run",
-      [](py::array_t<double, py::array::c_style | py::array::forcecast> nmat,
-         py::array_t<double, py::array::c_style | py::array::forcecast> arr,
-         py::array_t<int, py::array::c_style | py::array::forcecast> rsp,
-         py::array_t<int, py::array::c_style | py::array::forcecast> rord,
-         py::array_t<double, py::array::c_style | py::array::forcecast> W, py::array_t<double, py::array::c_style> rhoY,
+      [](const std::string& mech, py::array_t<double, py::array::c_style | py::array::forcecast> rhoY,
+         py::array_t<double, py::array::c_style | py::array::forcecast> rho,
+         py::array_t<double, py::array::c_style | py::array::forcecast> e,
          py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub, int repeats) {
-        const int ns = (int)W.size(), R = (int)(arr.size() / 3);
-        const int ncell = (int)T.size();
-        if (nmat.size() != (py::ssize_t)16 * R || rsp.size() != (py::ssize_t)3 * R || rord.size() != (py::ssize_t)3 * R ||
-            rhoY.size() != (py::ssize_t)ns * ncell)
-          throw std::runtime_error("chem_mech_run: inconsistent array sizes");
+        auto mi = mech.find('\n') == std::string::npos ? load_mechanism(mech) : parse_mechanism(mech);
+        const long n = (long)rho.size();
+        if (rhoY.ndim() != 2 || rhoY.shape(0) != mi->data.ns || rhoY.shape(1) != n || e.size() != n || T.size() != n)
+          throw std::runtime_error("chem_mech_run: shapes [ns, n], [n], [n], [n]");
+        py::array_t<double> y({(long)mi->data.ns, n});
+        std::memcpy(y.mutable_data(), rhoY.data(), sizeof(double) * rhoY.size());
+        py::array_t<double> Tout(n);
+        std::memcpy(Tout.mutable_data(), T.data(), sizeof(double) * n);
         double ms;
         {
           py::gil_scoped_release nogil;
-          ms = chem_mech_run_host(nmat.data(), arr.data(), rsp.data(), rord.data(), W.data(), ns, R,
-                                  rhoY.mutable_data(), T.data(), ncell, dt, nsub, repeats);
+          ms = chem_mech_run_host(mi->data, y.mutable_data(), rho.data(), e.data(), Tout.mutable_data(), n, dt, nsub,
+                                  repeats);
         }
-        return ms;
+        return py::make_tuple(y, Tout, ms);
       },
-      py::arg("nmat"), py::arg("arr"), py::arg("rsp"), py::arg("rord"), py::arg("W"), py::arg("rhoY"), py::arg("T"),
-      py::arg("dt"), py::arg("nsub") = 1, py::arg("repeats") = 1);
+      py::arg("mech"), py::arg("rhoY"), py::arg("rho"), py::arg("e"), py::arg("T"), py::arg("dt"), py::arg("nsub") = 1,
+      py::arg("repeats") = 1);
   m.attr("CHEM_MECH_MAX_REACTIONS") = chem_mech_max_reactions();
   m.def("request_stop", &request_stop, "ask a running driver to finish the cycle, write outputs and return");
   m.def("stop_requested", &stop_requested);
@@ -452,7 +454,7 @@ PYBIND11_MODULE(_hf2d, m) {
                              py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub) {
     // [ns, ncell] partial densities at constant (rho, e): the scalar point-implicit
     // integrator the device kernels are checked against; returns (rhoY, T)
-    auto mi = load_mechanism(name);
+    auto mi = name.find('\n') == std::string::npos ? load_mechanism(name) : parse_mechanism(name);
     const MechData& md = mi->data;
     const long n = (long)rho.size();
     if (rhoY.ndim() != 2 || rhoY.shape(0) != md.ns || rhoY.shape(1) != n || e.size() != n || T.size() != n)
@@ -545,6 +547,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_wgcu", &DeviceSolver::lean_wgcu)
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
       .def_readwrite("chem_fast", &DeviceSolver::chem_fast)
+      .def_readwrite("chem_kernel", &DeviceSolver::chem_kernel)
+      .def_readonly("chem_kernel_used", &DeviceSolver::chem_kernel_used)
       .def_readonly("chem_fast_ok", &DeviceSolver::chem_fast_ok)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)

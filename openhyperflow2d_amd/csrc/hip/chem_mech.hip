@@ -1,22 +1,21 @@
-// K12: finite-rate multi-reaction chemistry on the MFMA matrix cores (gfx950, FP64).
+// K12 for runtime (file) mechanisms on the MFMA matrix cores (gfx950, FP64).
 //
-// The reference has only the "infinite speed" Zeldovich global reaction
-// (deeps2d_core.cpp:4697-4780) and an empty CRM_ARRENIUS slot
-// (hyper_flow_bound.hpp:37-42); SURVEY.md 2.4 K12 asks for a finite-rate kinetics
-// kernel with per-cell Jacobians on MFMA.  This kernel advances a mass-action
-// mechanism (ns <= 16 species, R reactions, R % 4 == 0, irreversible Arrhenius
-// steps with integer reactant orders; a reversible step is two entries) by
-// nsub linearised backward-Euler (point-implicit) substeps at frozen T:
-//
-//     (I - h J) dc = h N q(c),   J = N D,   D[r][j] = dq_r / dc_j,   c <- max(c + dc, 0)
-//
-// with c = rhoY / W [mol/m^3] and N = nu'' - nu' (ns x R).  Both matrix products
-// are MFMA work (v_mfma_f64_16x16x4_f64, one wavefront = one 16-cell tile):
-//   * rates   Omega(16 species x 16 cells) = N(16 x R) . Q(R x 16 cells)   R/4 MFMAs
-//   * Jacobian J_c(16 x 16)                = N(16 x R) . D_c(R x 16)       R/4 MFMAs per cell
-// and the 16x16 systems are solved by Gauss-Jordan with partial pivoting, 16 lanes
-// per cell (lane = row, held in registers), 4 cells at a time, staged through LDS.
-// The 4 Jacobians of a round are independent MFMA chains (latency hiding).
+// Mechanism mode's kinetics operator (core/mechanism.hpp mech_chem_cell is the
+// host oracle; chem_fast.hip the register-resident kernel for compiled
+// mechanisms): nsub linearised backward-Euler substeps (I - h J) dc = h w at
+// constant rho and e with reversible rates, third-body efficiencies, Troe
+// fall-off and T re-solved from e after every substep.  A mechanism loaded at
+// run time has no compile-time structure, so the reaction-space algebra is
+// done as dense 16x16 tiles on the matrix cores, one wavefront = 16 cells
+// (the MFMA N dimension), v_mfma_f64_16x16x4_f64 throughout:
+//   ln Kc (R x cells) = -N^T (R x 16 sp) . G (16 sp x cells)      Gibbs energies
+//   [M]   (R x cells) =  E   (R x 16 sp) . C (16 sp x cells)      collider conc.
+//   w     (16 sp x cells) = N (16 x R) . Q (R x cells)            net rates
+//   J_c   (16 x 16) = N (16 x R) . D_c (R x 16)  per cell          Jacobian
+// Per-(cell, reaction) scalars (k_f, fall-off, k_r = k_f / Kc, q, dq/dc) run
+// in the MFMA output layout; the 16x16 systems are solved by Gauss-Jordan
+// with partial pivoting, 16 lanes per cell, 4 cells at a time, staged
+// through LDS.
 //
 // f64 MFMA operand maps (cdna_hip_programming.md): A[row=l&15][k=l>>4],
 // B[k=l>>4][col=l&15], C/D col=l&15, row=(l>>4)+4*i.
@@ -25,71 +24,192 @@
 #include <algorithm>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
+#include "../core/mechanism.hpp"
 #include "chem_mech.hpp"
 
+namespace hf2d {
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int TILE = 16;     // cells per wavefront (MFMA N dimension)
-constexpr int MAXR = 64;     // reactions per mechanism
+constexpr int MAXR = 64;     // reactions per mechanism (multiple of 16 after padding)
 constexpr int LD = 18;       // row stride of the staged systems (16 cols + rhs + pad)
 
-// x^o for o in 0..3 without branches
 __device__ __forceinline__ double pw3(double x, int o) {
   const double x2 = x * x;
   return o == 0 ? 1.0 : (o == 1 ? x : (o == 2 ? x2 : x2 * x));
 }
 
-// NSP: system size (ns rounded up to a multiple of 4).  Rows/columns >= ns carry an
-// identity block (no reaction touches them), so only the NSP x NSP block and the rhs
-// are eliminated.
+__device__ __forceinline__ const double* nasa(const ChemMechDev& m, int s, double T) {
+  return m.thermo + (s * 2 + (T < m.thermo[16 * 14 + s] ? 0 : 1)) * 7;
+}
+
+// specific internal energy and cv of the concentrations of one cell at T
+__device__ void cell_e_cv(const ChemMechDev& m, const double* c, double rho, double T, double* e, double* cv) {
+  double se = 0.0, scv = 0.0;
+  for (int s = 0; s < m.ns; s++) {
+    const double* a = nasa(m, s, T);
+    const double cpR = a[0] + T * (a[1] + T * (a[2] + T * (a[3] + T * a[4])));
+    const double hRT = a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) + a[5] / T;
+    se += c[s] * (T * (hRT - 1.0));
+    scv += c[s] * (cpR - 1.0);
+  }
+  *e = se * MECH_RU / rho;
+  *cv = scv * MECH_RU / rho;
+}
+
+__device__ double cell_T(const ChemMechDev& m, const double* c, double rho, double e, double T0) {
+  double T = T0 > MECH_TMIN ? (T0 < MECH_TMAX ? T0 : MECH_TMAX) : MECH_TMIN;
+  for (int it = 0; it < 30; it++) {
+    double ee, cv;
+    cell_e_cv(m, c, rho, T, &ee, &cv);
+    double dT = (e - ee) / cv;
+    dT = dT > 500.0 ? 500.0 : (dT < -500.0 ? -500.0 : dT);
+    double Tn = T + dT;
+    Tn = Tn > MECH_TMIN ? (Tn < MECH_TMAX ? Tn : MECH_TMAX) : MECH_TMIN;
+    const double d = Tn - T;
+    T = Tn;
+    if (fabs(d) <= 1e-10 * T) break;
+  }
+  return T;
+}
+
+// NSP: system size (ns rounded up to 4); rows/columns >= ns are identity.
 template <int NSP>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf2d_chem_mech(const double* __restrict__ nmat,   // [16][R]
-                                                     const double* __restrict__ arr,    // A[R], b[R], Ta[R]
-                                                     const int* __restrict__ rsp,       // [R][3]
-                                                     const int* __restrict__ rord,      // [R][3]
-                                                     const double* __restrict__ W,      // [ns]
-                                                     int ns, int R, int ncell, double* __restrict__ rhoY,
-                                                     const double* __restrict__ T, double dt, int nsub) {
-  __shared__ double c_s[TILE][TILE + 1];        // [cell][species]
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf2d_chem_mech(
+    ChemMechDev m, MechCells q, double dt, int nsub) {
+  __shared__ double c_s[TILE][TILE + 1];        // [cell][species] concentrations
+  __shared__ double g_s[TILE][TILE + 1];        // [cell][species] Gibbs h/RT - s/R
   __shared__ double m_s[4][TILE][LD];           // 4 systems in flight: [cell][row][col | rhs]
   __shared__ double x_s[4][TILE];
-  __shared__ int rx_s[MAXR];                    // packed reactants: 3 x (species 4 bits, order 2 bits)
-  extern __shared__ double kf_dyn[];            // [cell][R + 1] rate constants (sized per mechanism)
+  __shared__ double cellv[4][TILE];             // rho, e, T, lnP0RT per cell
+  __shared__ int rx_s[MAXR], px_s[MAXR], fl_s[MAXR];
+  extern __shared__ double dyn[];               // kf | kr | mult: [3][cell][R + 1]
 
   const int l = threadIdx.x, col = l & 15, quad = l >> 4;
-  const int cell0 = blockIdx.x * TILE;
-  const int mycell = cell0 + col;
-  const bool live = mycell < ncell;
-
+  const int R = m.R;
+  if (q.dt_bits) dt = __longlong_as_double((long long)*q.dt_bits);
+  double* kf_d = dyn;
+  double* kr_d = dyn + TILE * (R + 1);
+  double* mu_d = dyn + 2 * TILE * (R + 1);
+  const long cell = q.c0 + (long)blockIdx.x * TILE + col;
+  bool live = cell < q.c1;
+  // only active, warm cells react; the rest of the tile computes on a dummy
+  // state (T = 1000 K, c = 1) and does not store
+  bool react = false;
+  if (live) {
+    const double rho = q.S[cell];
+    react = q.active(cell) && rho > 0 && q.Tprev[cell] >= q.Tchem && dt > 0;
+  }
   for (int r = l; r < R; r += 64) {
-    int pk = 0;
-    for (int t = 0; t < 3; t++) pk |= (rsp[r * 3 + t] | (rord[r * 3 + t] << 4)) << (6 * t);
-    rx_s[r] = pk;
+    rx_s[r] = m.rx[r * 4 + 0];
+    px_s[r] = m.rx[r * 4 + 1];
+    fl_s[r] = m.rx[r * 4 + 2];
   }
   for (int i = 0; i < 4; i++) {
     const int s = quad + 4 * i;
-    c_s[col][s] = (live && s < ns) ? rhoY[(size_t)s * ncell + mycell] / W[s] : 0.0;
+    double v = 0.0;
+    if (s < m.ns) v = react ? fmax(q.Yin[(long)s * q.N + cell], 0.0) / m.W[s] : 1.0;
+    c_s[col][s] = v;
   }
-  {
-    const double Tc = live ? T[mycell] : 300.0;
-    const double lnT = log(Tc), rT = 1.0 / Tc;
-    for (int r = quad; r < R; r += 4) kf_dyn[col * (R + 1) + r] = arr[r] * exp(arr[R + r] * lnT - arr[2 * R + r] * rT);
+  if (quad == 0) {
+    double rho = 1.0, e = 0.0, T = 1000.0;
+    if (react) {
+      rho = q.S[cell];
+      const double ru = q.S[(long)I_RHOU * q.N + cell], rv = q.S[(long)I_RHOV * q.N + cell];
+      e = (q.S[(long)I_RHOE * q.N + cell] - 0.5 * (ru * ru + rv * rv) / rho) / rho;
+      T = q.Tprev[cell];
+    }
+    cellv[0][col] = rho;
+    cellv[1][col] = e;
+    cellv[2][col] = T;
+  }
+  __syncthreads();
+  if (quad == 0) {
+    double c[TILE];
+    for (int s = 0; s < TILE; s++) c[s] = c_s[col][s];
+    if (react) cellv[2][col] = cell_T(m, c, cellv[0][col], cellv[1][col], cellv[2][col]);
   }
   const double h = dt / nsub;
 
   for (int sub = 0; sub < nsub; sub++) {
     __syncthreads();
-    // Omega[s][cell] = sum_r N[s][r] q[r][cell]; lane (quad, col): Omega[quad + 4 i][col]
+    // --- per-cell thermodynamics: Gibbs energies of every species ---------
+    {
+      const double T = cellv[2][col], lnT = log(T);
+      for (int i = 0; i < 4; i++) {
+        const int s = quad + 4 * i;
+        double gv = 0.0;
+        if (s < m.ns) {
+          const double* a = nasa(m, s, T);
+          const double hRT =
+              a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) + a[5] / T;
+          const double sR = a[0] * lnT + T * (a[1] + T * (a[2] * 0.5 + T * (a[3] * (1.0 / 3.0) + T * a[4] * 0.25))) + a[6];
+          gv = hRT - sR;
+        }
+        g_s[col][s] = gv;
+      }
+      if (quad == 0) cellv[3][col] = log(MECH_PATM / (MECH_RU * T));
+    }
+    __syncthreads();
+    // --- rate constants: ln Kc and [M] as MFMA tiles, scalars in the D layout --
+    for (int rt = 0; rt < R; rt += 16) {
+      d4 lk = {0.0, 0.0, 0.0, 0.0}, mm = {0.0, 0.0, 0.0, 0.0};
+      for (int ks = 0; ks < NSP; ks += 4) {
+        const int s = ks + quad, r = rt + col;
+        const double an = -m.nmat[s * R + r];            // A[row r][k s]
+        const double ae = m.eff[r * 16 + s];
+        lk = __builtin_amdgcn_mfma_f64_16x16x4f64(an, g_s[col][s], lk, 0, 0, 0);   // B[k s][col cell]
+        mm = __builtin_amdgcn_mfma_f64_16x16x4f64(ae, c_s[col][s], mm, 0, 0, 0);
+      }
+      const double T = cellv[2][col], lnT = log(T), invT = 1.0 / T, lp = cellv[3][col];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int r = rt + quad + 4 * i;   // D row; column = cell `col`
+        const int fl = fl_s[r];
+        double kf = m.arr[r] * exp(m.arr[R + r] * lnT - m.arr[2 * R + r] * invT);
+        double mult = 1.0;
+        if (fl & 4) {   // fall-off
+          const double k0 = m.fall[r] * exp(m.fall[R + r] * lnT - m.fall[2 * R + r] * invT);
+          const double Pr = k0 * mm[i] / kf;
+          double F = 1.0;
+          const int nt = (fl >> 3) & 7;
+          if (nt >= 3) {
+            const double a = m.fall[3 * R + r];
+            double Fc = (1.0 - a) * exp(-T / m.fall[4 * R + r]) + a * exp(-T / m.fall[5 * R + r]);
+            if (nt > 3) Fc += exp(-m.fall[6 * R + r] * invT);
+            const double lFc = log10(Fc > 1e-300 ? Fc : 1e-300);
+            const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+            const double cc = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;
+            const double f1 = (lPr + cc) / (nn - 0.14 * (lPr + cc));
+            F = pow(10.0, lFc / (1.0 + f1 * f1));
+          }
+          kf = kf * (Pr / (1.0 + Pr)) * F;
+        } else if (fl & 2) {   // "+ M"
+          mult = mm[i];
+        }
+        const int dnu = (fl >> 8) - 16;
+        const double kr = (fl & 1) ? kf * exp(-(lk[i] + dnu * lp)) : 0.0;
+        kf_d[col * (R + 1) + r] = kf;
+        kr_d[col * (R + 1) + r] = kr;
+        mu_d[col * (R + 1) + r] = mult;
+      }
+    }
+    __syncthreads();
+    // --- net rates w = N . Q ------------------------------------------------
     d4 om = {0.0, 0.0, 0.0, 0.0};
     for (int r0 = 0; r0 < R; r0 += 4) {
-      const int r = r0 + quad, pk = rx_s[r];
-      double q = kf_dyn[col * (R + 1) + r];
+      const int r = r0 + quad, pk = rx_s[r], pp = px_s[r];
+      double pf = kf_d[col * (R + 1) + r], pr = kr_d[col * (R + 1) + r];
 #pragma unroll
-      for (int t = 0; t < 3; t++) q *= pw3(c_s[col][(pk >> (6 * t)) & 15], (pk >> (6 * t + 4)) & 3);
-      om = __builtin_amdgcn_mfma_f64_16x16x4f64(nmat[col * R + r], q, om, 0, 0, 0);
+      for (int t = 0; t < 3; t++) {
+        pf *= pw3(c_s[col][(pk >> (6 * t)) & 15], (pk >> (6 * t + 4)) & 3);
+        pr *= pw3(c_s[col][(pp >> (6 * t)) & 15], (pp >> (6 * t + 4)) & 3);
+      }
+      om = __builtin_amdgcn_mfma_f64_16x16x4f64(m.nmat[col * R + r], mu_d[col * (R + 1) + r] * (pf - pr), om, 0, 0, 0);
     }
 #pragma unroll
     for (int g = 0; g < 4; g++) {
@@ -99,21 +219,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
 #pragma unroll
       for (int qq = 0; qq < 4; qq++) jac[qq] = d4{0.0, 0.0, 0.0, 0.0};
       for (int r0 = 0; r0 < R; r0 += 4) {
-        const int r = r0 + quad, pk = rx_s[r];
-        const double nv = nmat[col * R + r];
-        const int s0 = pk & 15, o0 = (pk >> 4) & 3, s1 = (pk >> 6) & 15, o1 = (pk >> 10) & 3, s2 = (pk >> 12) & 15,
-                  o2 = (pk >> 16) & 3;
-        const bool h0 = s0 == col && o0 > 0, h1 = s1 == col && o1 > 0, h2 = s2 == col && o2 > 0;
+        const int r = r0 + quad, pk = rx_s[r], pp = px_s[r], fl = fl_s[r];
+        const double nv = m.nmat[col * R + r];
+        const double ev = ((fl & 6) == 2) ? m.eff[r * 16 + col] : 0.0;   // pure third body
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {
           const int cc = 4 * g + qq;
-          const double c0 = c_s[cc][s0], c1 = c_s[cc][s1], c2 = c_s[cc][s2];
-          const double p0 = pw3(c0, o0), p1 = pw3(c1, o1), p2 = pw3(c2, o2);
-          const double kf = kf_dyn[cc * (R + 1) + r];
-          double d = 0.0;
-          if (h0) d = kf * (o0 * pw3(c0, o0 - 1)) * p1 * p2;
-          if (h1) d = kf * p0 * (o1 * pw3(c1, o1 - 1)) * p2;
-          if (h2) d = kf * p0 * p1 * (o2 * pw3(c2, o2 - 1));
+          const double kf = kf_d[cc * (R + 1) + r], kr = kr_d[cc * (R + 1) + r], mu = mu_d[cc * (R + 1) + r];
+          double pf = kf, pr = kr, df = 0.0, dr = 0.0;
+#pragma unroll
+          for (int t = 0; t < 3; t++) {
+            const int sf = (pk >> (6 * t)) & 15, of = (pk >> (6 * t + 4)) & 3;
+            const int sr = (pp >> (6 * t)) & 15, orr = (pp >> (6 * t + 4)) & 3;
+            const double cf = c_s[cc][sf], cr = c_s[cc][sr];
+            // d(prod)/dc_col by the product rule over the (distinct) species
+            df = df * pw3(cf, of) + ((sf == col && of > 0) ? pf * (of * pw3(cf, of - 1)) : 0.0);
+            dr = dr * pw3(cr, orr) + ((sr == col && orr > 0) ? pr * (orr * pw3(cr, orr - 1)) : 0.0);
+            pf *= pw3(cf, of);
+            pr *= pw3(cr, orr);
+          }
+          const double d = mu * (df - dr) + ev * (pf - pr);
           jac[qq] = __builtin_amdgcn_mfma_f64_16x16x4f64(nv, d, jac[qq], 0, 0, 0);
         }
       }
@@ -126,20 +251,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
         }
       if ((col >> 2) == g)
         for (int i = 0; i < 4; i++) m_s[col & 3][quad + 4 * i][TILE] = h * om[i];
+      x_s[quad][col] = 0.0;
       __syncthreads();
       double row[TILE + 1];
 #pragma unroll
       for (int j = 0; j <= TILE; j++) row[j] = m_s[quad][col][j];
 
-      // Gauss-Jordan, group `quad` solves cell 4g+quad; lane `col` holds row col in
-      // registers (k, j unrolled), the pivot row is read with in-group shuffles.
+      // Gauss-Jordan, group `quad` solves cell 4g+quad; lane `col` holds row col
       bool used = false;
       int kk = 0;
       double diag = 1.0;
 #pragma unroll
       for (int k = 0; k < NSP; k++) {
-        // Pivot = max |M[i][k]| over unused rows, ties to the lower row: one 64-bit key per
-        // lane (|v|'s bits, monotone for v >= 0, low 4 mantissa bits replaced by 15 - row).
+        // pivot = max |M[i][k]| over unused rows (ties to the lower row): one
+        // 64-bit key per lane, |v|'s bits with the low 4 replaced by 15 - row
         unsigned long long key =
             used ? 0ull : ((unsigned long long)__double_as_longlong(fabs(row[k])) & ~15ull) | (unsigned)(15 - col);
 #pragma unroll
@@ -150,7 +275,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
         const int p = 15 - (int)(key & 15ull);
         const double pk = __shfl(row[k], p, 16);
         const bool me = col == p;
-        const double f = me ? 0.0 : row[k] / pk;
+        const double f = (me || pk == 0.0) ? 0.0 : row[k] / pk;
         if (me) {
           used = true;
           kk = k;
@@ -162,39 +287,52 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
         for (int j = k + 1; j <= TILE; j++)
           if (j < NSP || j == TILE) row[j] -= f * __shfl(row[j], p, 16);
       }
-      if (used) x_s[quad][kk] = row[TILE] / diag;
+      // a singular system (zero pivot) leaves that cell's species unchanged
+      if (used && kk < m.ns) x_s[quad][kk] = fabs(diag) > 0.0 ? row[TILE] / diag : 0.0;
       __syncthreads();
       {
         const int cc = 4 * g + quad;
-        if (col < ns) c_s[cc][col] = fmax(c_s[cc][col] + x_s[quad][col], 0.0);
+        if (col < m.ns) c_s[cc][col] = fmax(c_s[cc][col] + x_s[quad][col], 0.0);
       }
       __syncthreads();
     }
+    // mass re-normalisation and T from e, one lane per cell
+    if (quad == 0) {
+      double c[TILE], tot = 0.0;
+      for (int s = 0; s < TILE; s++) {
+        c[s] = c_s[col][s];
+        if (s < m.ns) tot += c[s] * m.W[s];
+      }
+      const double rho = cellv[0][col];
+      const double sc = tot > 0.0 ? rho / tot : 1.0;
+      for (int s = 0; s < m.ns; s++) {
+        c[s] *= sc;
+        c_s[col][s] = c[s];
+      }
+      if (react) cellv[2][col] = cell_T(m, c, rho, cellv[1][col], cellv[2][col]);
+    }
   }
   __syncthreads();
-  if (live)
+  if (live) {
     for (int i = 0; i < 4; i++) {
       const int s = quad + 4 * i;
-      if (s < ns) rhoY[(size_t)s * ncell + mycell] = c_s[col][s] * W[s];
+      if (s < m.ns) q.Yout[(long)s * q.N + cell] = react ? c_s[col][s] * m.W[s] : q.Yin[(long)s * q.N + cell];
     }
+    if (quad == 0 && q.Tout) q.Tout[cell] = react ? cellv[2][col] : q.Tprev[cell];
+  }
 }
 
 }  // namespace
 
-namespace hf2d {
-
 int chem_mech_max_reactions() { return MAXR; }
 
-// Device pointers; returns a hipError_t code (0 = ok).
-int chem_mech_launch(const ChemMechDev& m, double* rhoY, const double* T, int ncell, double dt, int nsub,
-                     hipStream_t stream) {
-  if (m.ns < 1 || m.ns > TILE || m.R < 4 || m.R % 4 != 0 || m.R > MAXR || ncell < 1 || nsub < 1)
-    return (int)hipErrorInvalidValue;
-  const int blocks = (ncell + TILE - 1) / TILE;
-  const size_t lds = sizeof(double) * TILE * (m.R + 1);
-#define HF2D_CHEM_LAUNCH(N)                                                                                  \
-  hipLaunchKernelGGL(hf2d_chem_mech<N>, dim3(blocks), dim3(64), lds, stream, m.nmat, m.arr, m.rsp, m.rord, m.W, \
-                     m.ns, m.R, ncell, rhoY, T, dt, nsub)
+int chem_mech_launch(const ChemMechDev& m, const MechCells& q, double dt, int nsub, hipStream_t stream) {
+  if (m.ns < 1 || m.ns > TILE || m.R < 16 || m.R % 16 != 0 || m.R > MAXR || nsub < 1) return (int)hipErrorInvalidValue;
+  if (q.c1 <= q.c0) return 0;
+  const unsigned blocks = (unsigned)((q.c1 - q.c0 + TILE - 1) / TILE);
+  const size_t lds = sizeof(double) * 3 * TILE * (m.R + 1);
+#define HF2D_CHEM_LAUNCH(N) \
+  hipLaunchKernelGGL(hf2d_chem_mech<N>, dim3(blocks), dim3(64), lds, stream, m, q, dt, nsub)
   switch ((m.ns + 3) / 4) {
     case 1: HF2D_CHEM_LAUNCH(4); break;
     case 2: HF2D_CHEM_LAUNCH(8); break;
@@ -205,64 +343,141 @@ int chem_mech_launch(const ChemMechDev& m, double* rhoY, const double* T, int nc
   return (int)hipGetLastError();
 }
 
-}  // namespace hf2d
-
-namespace hf2d {
-
+// ---------------------------------------------------------------------------
+// Device pack of a MechData (owned device buffers)
+// ---------------------------------------------------------------------------
 namespace {
 void ck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("chem_mech: ") + what + ": " + hipGetErrorString(e));
 }
 }  // namespace
 
-double chem_mech_run_host(const double* nmat, const double* arr, const int* rsp, const int* rord, const double* W,
-                          int ns, int R, double* rhoY, const double* T, int ncell, double dt, int nsub,
-                          int repeats) {
-  if (ns < 1 || ns > 16 || R < 4 || R % 4 != 0 || R > MAXR || ncell < 1 || nsub < 1)
-    throw std::runtime_error("chem_mech: need 1 <= ns <= 16, 4 <= R <= 64 with R % 4 == 0, ncell >= 1, nsub >= 1");
-  for (int i = 0; i < 3 * R; i++)
-    if (rsp[i] < 0 || rsp[i] >= ns || rord[i] < 0 || rord[i] > 3)
-      throw std::runtime_error("chem_mech: reactant species out of range or order not in 0..3");
-  const size_t nY = (size_t)ns * ncell;
-  double *d_nmat, *d_arr, *d_W, *d_Y, *d_Y0, *d_T;
-  int *d_rsp, *d_rord;
-  ck(hipMalloc(&d_nmat, sizeof(double) * 16 * R), "malloc");
-  ck(hipMalloc(&d_arr, sizeof(double) * 3 * R), "malloc");
-  ck(hipMalloc(&d_W, sizeof(double) * ns), "malloc");
-  ck(hipMalloc(&d_rsp, sizeof(int) * 3 * R), "malloc");
-  ck(hipMalloc(&d_rord, sizeof(int) * 3 * R), "malloc");
-  ck(hipMalloc(&d_Y, sizeof(double) * nY), "malloc");
-  ck(hipMalloc(&d_Y0, sizeof(double) * nY), "malloc");
-  ck(hipMalloc(&d_T, sizeof(double) * ncell), "malloc");
-  ck(hipMemcpy(d_nmat, nmat, sizeof(double) * 16 * R, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_arr, arr, sizeof(double) * 3 * R, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_W, W, sizeof(double) * ns, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_rsp, rsp, sizeof(int) * 3 * R, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_rord, rord, sizeof(int) * 3 * R, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_Y0, rhoY, sizeof(double) * nY, hipMemcpyHostToDevice), "h2d");
-  ck(hipMemcpy(d_T, T, sizeof(double) * ncell, hipMemcpyHostToDevice), "h2d");
-  ChemMechDev m;
-  m.nmat = d_nmat; m.arr = d_arr; m.rsp = d_rsp; m.rord = d_rord; m.W = d_W; m.ns = ns; m.R = R;
-  hipEvent_t e0, e1;
+ChemMechPack::~ChemMechPack() {
+  for (void* p : bufs) (void)hipFree(p);
+}
+
+std::unique_ptr<ChemMechPack> chem_mech_pack(const MechData& md) {
+  std::unique_ptr<ChemMechPack> pk(new ChemMechPack);
+  const int R = std::max(16, (md.nr + 15) / 16 * 16);
+  if (md.ns > 16 || R > MAXR) throw std::runtime_error("chem_mech: at most 16 species and 64 reactions");
+  std::vector<double> nmat(16 * R, 0.0), arr(3 * R, 0.0), fall(7 * R, 0.0), eff(R * 16, 0.0);
+  std::vector<double> thermo(16 * 14 + 16 + 16, 0.0);
+  std::vector<int> rx(R * 4, 0);
+  for (int s = 0; s < md.ns; s++) {
+    for (int b = 0; b < 2; b++)
+      for (int k = 0; k < 7; k++) thermo[(s * 2 + b) * 7 + k] = md.a[s][b][k];
+    thermo[16 * 14 + s] = md.Tmid[s];
+  }
+  for (int s = md.ns; s < 16; s++) thermo[16 * 14 + s] = 1000.0;
+  for (int r = 0; r < R; r++) {
+    int fl = 16 << 8;   // dnu = 0
+    if (r < md.nr) {
+      const MechReaction& x = md.rx[r];
+      int pr = 0, pp = 0;
+      for (int t = 0; t < x.nrs; t++) {
+        nmat[x.rs[t] * R + r] -= x.rn[t];
+        pr |= (x.rs[t] | (x.rn[t] << 4)) << (6 * t);
+      }
+      for (int t = 0; t < x.nps; t++) {
+        nmat[x.ps[t] * R + r] += x.pn[t];
+        pp |= (x.ps[t] | (x.pn[t] << 4)) << (6 * t);
+      }
+      arr[r] = x.A;
+      arr[R + r] = x.b;
+      arr[2 * R + r] = x.Ta;
+      fall[r] = x.A0;
+      fall[R + r] = x.b0;
+      fall[2 * R + r] = x.Ta0;
+      for (int k = 0; k < 4; k++) fall[(3 + k) * R + r] = x.troe[k];
+      if (x.tb || x.fo)
+        for (int s = 0; s < md.ns; s++) eff[r * 16 + s] = x.eff >= 0 ? md.eff[x.eff][s] : 1.0;
+      fl = (x.rev ? 1 : 0) | ((x.tb && !x.fo) ? 2 : 0) | (x.fo ? 4 : 0) | ((x.ntroe & 7) << 3) | ((x.dnu + 16) << 8);
+      rx[r * 4 + 0] = pr;
+      rx[r * 4 + 1] = pp;
+    } else {
+      arr[r] = 0.0;   // padding reaction: k = 0
+    }
+    rx[r * 4 + 2] = fl;
+  }
+  auto up = [&](const void* h, size_t bytes) {
+    void* d = nullptr;
+    ck(hipMalloc(&d, std::max<size_t>(bytes, 8)), "malloc");
+    pk->bufs.push_back(d);
+    ck(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), "h2d");
+    return d;
+  };
+  std::vector<double> W(16, 1.0);
+  for (int s = 0; s < md.ns; s++) W[s] = md.W[s];
+  ChemMechDev& m = pk->dev;
+  m.nmat = (const double*)up(nmat.data(), nmat.size() * 8);
+  m.arr = (const double*)up(arr.data(), arr.size() * 8);
+  m.fall = (const double*)up(fall.data(), fall.size() * 8);
+  m.eff = (const double*)up(eff.data(), eff.size() * 8);
+  m.thermo = (const double*)up(thermo.data(), thermo.size() * 8);
+  m.W = (const double*)up(W.data(), W.size() * 8);
+  m.rx = (const int*)up(rx.data(), rx.size() * 4);
+  m.ns = md.ns;
+  m.R = R;
+  return pk;
+}
+
+double chem_mech_run_host(const MechData& md, double* rhoY, const double* rho, const double* e, double* T, long n,
+                          double dt, int nsub, int repeats) {
+  if (n < 1 || nsub < 1) throw std::runtime_error("chem_mech: need n >= 1 and nsub >= 1");
+  for (long i = 0; i < n; i++)
+    if (!(T[i] > 0.0) || !(rho[i] > 0.0)) throw std::runtime_error("chem_mech: T and rho must be > 0 and finite");
+  auto pk = chem_mech_pack(md);
+  const int ns = md.ns;
+  // the solver's SoA form: S = [rho, rhoU = 0, rhoV = 0, rho*e], every cell active
+  std::vector<double> S(4 * n), Y((size_t)ns * n);
+  for (long i = 0; i < n; i++) {
+    S[i] = rho[i];
+    S[n + i] = S[2 * n + i] = 0.0;
+    S[3 * n + i] = rho[i] * e[i];
+  }
+  struct Buf {
+    void* p = nullptr;
+    ~Buf() {
+      if (p) (void)hipFree(p);
+    }
+  } dS, dY0, dY, dT0, dT;
+  const size_t nb = sizeof(double) * n;
+  ck(hipMalloc(&dS.p, 4 * nb), "malloc");
+  ck(hipMalloc(&dY0.p, ns * nb), "malloc");
+  ck(hipMalloc(&dY.p, ns * nb), "malloc");
+  ck(hipMalloc(&dT0.p, nb), "malloc");
+  ck(hipMalloc(&dT.p, nb), "malloc");
+  ck(hipMemcpy(dS.p, S.data(), 4 * nb, hipMemcpyHostToDevice), "h2d");
+  ck(hipMemcpy(dY0.p, rhoY, ns * nb, hipMemcpyHostToDevice), "h2d");
+  ck(hipMemcpy(dT0.p, T, nb, hipMemcpyHostToDevice), "h2d");
+  MechCells q;
+  q.S = (const double*)dS.p;
+  q.Yin = (const double*)dY0.p;
+  q.Yout = (double*)dY.p;
+  q.Tprev = (const double*)dT0.p;
+  q.Tout = (double*)dT.p;
+  q.CT = nullptr;
+  q.N = n;
+  q.c0 = 0;
+  q.c1 = n;
+  q.Tchem = 0.0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
   ck(hipEventCreate(&e0), "event");
   ck(hipEventCreate(&e1), "event");
   float total = 0.f;
   for (int it = 0; it < std::max(repeats, 1); it++) {
-    ck(hipMemcpyAsync(d_Y, d_Y0, sizeof(double) * nY, hipMemcpyDeviceToDevice, 0), "d2d");
     ck(hipEventRecord(e0, 0), "record");
-    ck((hipError_t)chem_mech_launch(m, d_Y, d_T, ncell, dt, nsub, 0), "launch");
+    ck((hipError_t)chem_mech_launch(pk->dev, q, dt, nsub, 0), "launch");
     ck(hipEventRecord(e1, 0), "record");
     ck(hipEventSynchronize(e1), "sync");
     float ms = 0.f;
     ck(hipEventElapsedTime(&ms, e0, e1), "elapsed");
     total += ms;
   }
-  ck(hipMemcpy(rhoY, d_Y, sizeof(double) * nY, hipMemcpyDeviceToHost), "d2h");
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  for (void* p : {(void*)d_nmat, (void*)d_arr, (void*)d_W, (void*)d_rsp, (void*)d_rord, (void*)d_Y, (void*)d_Y0,
-                  (void*)d_T})
-    (void)hipFree(p);
+  ck(hipMemcpy(rhoY, dY.p, ns * nb, hipMemcpyDeviceToHost), "d2h");
+  ck(hipMemcpy(T, dT.p, nb, hipMemcpyDeviceToHost), "d2h");
   return total / std::max(repeats, 1);
 }
 

@@ -38,6 +38,7 @@
 #include "device_solver.hpp"
 #include "dev_common.hpp"
 #include "chem_fast.hpp"
+#include "chem_mech.hpp"
 
 #define HIP_CHECK(x)                                                                             \
   do {                                                                                           \
@@ -1072,6 +1073,7 @@ struct DeviceSolver::Impl {
   // mechanism mode (SK_MECH): species block, Ys ping-pongs with S (sbuf)
   MechData* mech = nullptr;
   int nsp = 0;
+  std::unique_ptr<ChemMechPack> chem_pack;   // MFMA kinetics kernel's mechanism image
   real *Ys[2] = {nullptr, nullptr}, *As = nullptr, *Bs = nullptr, *Fs = nullptr, *betas = nullptr;
   real *dSdxs[2] = {nullptr, nullptr}, *dSdys[2] = {nullptr, nullptr};
   SpeciesProps* species = nullptr;
@@ -2380,10 +2382,36 @@ void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& o
   Impl& m = *impl;
   const real* Tprev = m.Tg[pbuf];
   const MechData& md = *cs.cfg.mech->data_ptr();
+  const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : 2);
   // compiled mechanism: register-resident VALU kernel (chem_fast.hip)
-  if (chem_fast && chem_fast_ok &&
-      chem_fast_launch(cs.cfg.mech->name, P, mid, out, Tprev, k0, k1, m.sc, slot, md.Tchem, md.nsub, m.stream))
+  if (kind == 1) {
+    if (!chem_fast_ok) throw std::runtime_error("chem_kernel=1: no compiled kernel for mechanism " + cs.cfg.mech->name);
+    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, out, Tprev, k0, k1, m.sc, slot, md.Tchem, md.nsub, m.stream))
+      throw std::runtime_error("hf2d_chem_fast launch failed");
+    chem_kernel_used = "hf2d_chem_fast";
     return;
+  }
+  // runtime mechanism: reaction-space algebra on the matrix cores (chem_mech.hip).
+  // The dt of the step lives on the device: the kernel takes it from the slot.
+  if (kind == 2) {
+    if (!m.chem_pack) m.chem_pack = chem_mech_pack(md);
+    MechCells q;
+    q.S = mid.S;
+    q.Yin = mid.Ys;
+    q.Yout = out.Ys;
+    q.Tprev = Tprev;
+    q.Tout = nullptr;
+    q.CT = mid.CT;
+    q.N = h.N;
+    q.c0 = k0;
+    q.c1 = k1;
+    q.Tchem = md.Tchem;
+    q.dt_bits = &m.sc->dt_bits[slot];
+    HIP_CHECK((hipError_t)chem_mech_launch(m.chem_pack->dev, q, 0.0, md.nsub, m.stream));
+    chem_kernel_used = "hf2d_chem_mech";
+    return;
+  }
+  chem_kernel_used = "hf2d_chem_generic";
   if (m.nsp <= 9)
     hipLaunchKernelGGL(hf2d_chem_generic<9>, dim3(nb), dim3(BLOCK), 0, m.stream, P, mid, out, Tprev, k0, k1, m.sc,
                        slot);

@@ -129,6 +129,10 @@ class DeviceSolver : public SolverBase {
   std::string lean_why;
   bool chem_fast = true;  // mechanism mode: compiled-mechanism kinetics kernel when one exists
   bool chem_fast_ok = false;   // the loaded mechanism equals a compiled one
+  // kinetics kernel: 0 auto (compiled VALU kernel if the mechanism has one, else
+  // the MFMA kernel), 1 compiled, 2 MFMA, 3 generic runtime-data VALU
+  int chem_kernel = 0;
+  std::string chem_kernel_used;
   bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
   bool sgl_ok = false;
   int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)

@@ -20,7 +20,8 @@ CASES = {
     "wedge15_ns_keps": (lambda: decks.wedge15(120, 50, navier_stokes=True, turbulence=4, nmax=10 ** 6, nout=10 ** 5), 12),
     "wedge15_ns_lam": (lambda: decks.wedge15(120, 50, navier_stokes=True, turbulence=0, nmax=10 ** 6, nout=10 ** 5), 12),
     "resonator": (lambda: decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5), 12),
-    "scramjet_sst": (lambda: decks.scramjet(450, 40, nmax=10 ** 6, nout=10 ** 5, turbulence=6), 12),
+    "scramjet_sst": (lambda: decks.scramjet(450, 40, nmax=10 ** 6, nout=10 ** 5, turbulence=6, mechanism=None), 12),
+    "scramjet_mech": (lambda: decks.scramjet(450, 40, nmax=10 ** 6, nout=10 ** 5, turbulence=6), 12),
     "step_ns": (lambda: decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5), 12),
     "triple_point": (lambda: decks.triple_point(210, 90, nmax=10 ** 6, nout=10 ** 5), 12),
     "reactor0d": (lambda: decks.reactor0d(T=1200.0), 12),
