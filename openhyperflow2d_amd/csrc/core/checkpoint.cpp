@@ -62,6 +62,15 @@ void write_hf2d(const std::string& path, const Field& J) {
   if (!ok) throw std::runtime_error("short write to checkpoint " + path);
 }
 
+void create_zero_hf2d(const std::string& path, int nx, int ny) {
+  const off_t len = (off_t)nx * ny * (off_t)sizeof(CellRecord);
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+  if (fd < 0) throw std::runtime_error("cannot create checkpoint " + path);
+  const int rc = ::ftruncate(fd, len);
+  ::close(fd);
+  if (rc != 0) throw std::runtime_error("cannot size checkpoint " + path);
+}
+
 void write_hf2d_slab(const std::string& path, const Field& local, int local_i0, int global_i0, int ncols,
                      int global_nx) {
   int fd = ::open(path.c_str(), O_WRONLY | O_CREAT, 0644);

@@ -13,6 +13,8 @@ namespace hf2d {
 
 // Returns true and fills J when `path` exists with exactly nx*ny*1248 bytes.
 bool read_hf2d(const std::string& path, Field& J);
+// zero-filled image of the full size (the reference's swap file of a cold start)
+void create_zero_hf2d(const std::string& path, int nx, int ny);
 // Writes the whole field (pwrite in <=1 GiB chunks).
 void write_hf2d(const std::string& path, const Field& J);
 // Writes a column slab [i0, i1) of a global-size file at its file offset

@@ -37,6 +37,19 @@ struct FillParams {
 };
 
 HF_HD inline real hf_max(real a, real b) { return a > b ? a : b; }
+
+// x^n for an integer exponent the way the reference's C++98 build evaluates
+// pow(double, int) (libgcc __powidf2: binary powering, e.g. x^6 = x^2 * x^4),
+// which differs from libm pow in the last bits.
+HF_HD inline real powi_ref(real x, int m) {
+  unsigned n = m < 0 ? 0u - (unsigned)m : (unsigned)m;
+  real y = (n % 2) ? x : 1.0;
+  while (n >>= 1) {
+    x = x * x;
+    if (n % 2) y = y * x;
+  }
+  return m < 0 ? 1.0 / y : y;
+}
 HF_HD inline real hf_min(real a, real b) { return a < b ? a : b; }
 
 // ---------------------------------------------------------------------------
@@ -187,7 +200,7 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
     } else if (P.tem == TEM_Escudier) {
       l = (P.delta > 0.) ? hf_min(n_0, 0.09 * P.delta) : n_0;
     } else if (P.tem == TEM_Klebanoff) {
-      l = (P.delta > 0.) ? n_0 / std::sqrt(1 + 5.5 * std::pow(n.l_min / P.delta, 6)) : n_0;
+      l = (P.delta > 0.) ? n_0 / std::sqrt(1 + 5.5 * powi_ref(n.l_min / P.delta, 6)) : n_0;
     }
     n.mu_t = n.S[I_RHO] * l * l * hf_max(std::fabs(n.dUdy), std::fabs(n.dVdx));
     n.lam_t = n.mu_t * n.CP;

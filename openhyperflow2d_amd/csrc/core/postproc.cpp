@@ -395,9 +395,9 @@ void save_x_heat_flux(const std::string& path, const Case& cs, const Field& J) {
       Cp[i] = cp;
       St[i] = st;
     }
-  for (int i = 0; i < NX; i++)
-    o << i * C.dx << " " << Q[i] << " " << Al[i] << " " << Cp[i] << " " << St[i] << " " << QR[i] << " " << AR[i]
-      << " " << Re[i] << " " << Pr[i] << "\n";
+  // the reference's default build (no _REF_TEST_) writes X, Q, alpha, Cp, St;
+  // the laminar-correlation columns QR, AR, Re, Pr are kept for tests only
+  for (int i = 0; i < NX; i++) o << i * C.dx << " " << Q[i] << " " << Al[i] << " " << Cp[i] << " " << St[i] << "\n";
 }
 
 void save_y_heat_flux(const std::string& path, const Case& cs, const Field& J) {

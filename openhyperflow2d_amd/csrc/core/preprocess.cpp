@@ -583,7 +583,17 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
   preloaded = false;
   swap_path = workdir.empty() ? C.swap_file : (workdir + "/" + C.swap_file);
   if (use_checkpoint) {
-    if (read_hf2d(swap_path, J)) {
+    // an all-zero image is the placeholder a failed first cycle leaves behind
+    // (create_zero_hf2d): not a checkpoint
+    bool any_set = false;
+    if (read_hf2d(swap_path, J))
+      for (const CellRecord& c : J.c)
+        if (c.CT != 0) {
+          any_set = true;
+          break;
+        }
+    if (!any_set) std::fill(J.c.begin(), J.c.end(), CellRecord{});
+    if (any_set) {
       preloaded = true;
       say("Mapping computation area...OK (preloaded " + swap_path + ")\n");
       // the reference restarts its iteration counter at 0 (it is not in the

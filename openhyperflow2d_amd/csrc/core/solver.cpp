@@ -466,7 +466,9 @@ void SolverBase::failure_snapshot(const RunOptions& opt, const std::string& dir,
   }
   const std::string name = (nr > 1 ? "rank-" + std::to_string(r) + "-" : std::string()) + plt_stem(C.out_file) +
                            "-err.plt";
-  if (opt.write_outputs) save_field_plt(dir + "/" + name, cs, cs.J, cs.global_time + cur_time_part, true);
+  // the reference stamps the snapshot with GlobalTime, which advances only at
+  // cycle ends (deeps2d_core.cpp:1264-1279, 1785-1788)
+  if (opt.write_outputs) save_field_plt(dir + "/" + name, cs, cs.J, cs.global_time, true);
   if (log && (r == 0 || nr > 1)) {
     *log << "\n" << why;
     // the first owned active cell with Tg < 0 (deeps2d_core.cpp:1246-1316 report + PrintCond)
@@ -531,6 +533,21 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
   const std::string dir = opt.outdir.empty() ? "." : opt.outdir;
   const std::string rms_path = dir + "/RMS-" + C.out_file;
   const std::string mon_path = dir + "/Monitors-" + C.out_file;
+  if (root && opt.write_outputs) {
+    // the pre-processor truncates the field file of a cold start
+    // (deeps2d_core.cpp:3858-3860): a run that fails in its first cycle
+    // leaves it empty
+    if (!cs.preloaded) {
+      std::FILE* t = std::fopen((dir + "/" + C.out_file).c_str(), "w");
+      if (t) std::fclose(t);
+    }
+  }
+  if (root && opt.write_checkpoint && !cs.preloaded) {
+    // LoadSwapFile2D creates the swap file zero-filled at its full size on a
+    // cold start (obj_data.cpp:173-219): a run that fails before its first
+    // cycle end leaves that image
+    create_zero_hf2d(dir + "/" + C.swap_file, C.MaxX, C.MaxY);
+  }
   if (root && opt.write_outputs) {
     save_rms_header(rms_path, C);
     if (!C.monitors.empty()) save_monitors_header(mon_path, C);
@@ -994,6 +1011,9 @@ void CpuSolver::cycle_update() {
 RefSolver::RefSolver(Case& c) : SolverBase(c) {
   if (c.cfg.mech_mode())
     throw std::runtime_error("the reference-order backend has no mechanism mode (the reference has no detailed kinetics)");
+  // the reference does not persist the iteration counter: a resumed run
+  // restarts its scenarios and TurbStartIter at 0
+  last_iter = 0;
   core.resize(c.J.c.size());
 }
 
@@ -1133,7 +1153,11 @@ StepResult RefSolver::do_step(const StepParams& P, bool /*want_res*/) {
         }
         fill_node(c, P.fpa);
         if (c.Tg < 0.) {
+          // the reference aborts inside the sweep (deeps2d_core.cpp:1246-1316):
+          // cells after this one keep their pass-1 state in its error snapshot
           r.neg_T = 1;
+          r.dt_min = dtmin;
+          return r;
         } else {
           const real AAA = std::sqrt(c.k * c.R * c.Tg);
           dtmin = std::min(dtmin, P.CFL_min * std::min(C.dx / (AAA + std::fabs(c.U)), C.dy / (AAA + std::fabs(c.V))));

@@ -40,12 +40,33 @@ def test_reference_outputs_bitwise(case, cli, tmp_path):
     d = os.path.join(FIXTURES, "ref", case)
     want = json.load(open(os.path.join(d, "sha256.json")))
     shutil.copy(os.path.join(d, "deck.dat"), tmp_path / "deck.dat")
-    r = subprocess.run([cli, "--backend", "ref", "--semantics", "serial", "deck.dat"], cwd=tmp_path,
-                       capture_output=True, text=True, timeout=900)
-    assert r.returncode == want["_returncode"], r.stdout[-2000:] + r.stderr[-2000:]
+    # _runs > 1: later runs resume from the .hf2d the previous run wrote
+    for _ in range(want.get("_runs", 1)):
+        r = subprocess.run([cli, "--backend", "ref", "--semantics", "serial", "deck.dat"], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=900)
+    # the reference exits 0 even after its Tg < 0 abort (exit(0) in
+    # Abort_OpenHyperFLOW2D); ours reports the failure with a non-zero status
+    failed = any(k.endswith("-err.plt") for k in want)
+    if failed:
+        assert r.returncode != 0, r.stdout[-2000:]
+    else:
+        assert r.returncode == want["_returncode"], r.stdout[-2000:] + r.stderr[-2000:]
+    if "_log_lines" in want:   # integral quantities printed per cycle (Cx/Cy/Fx/Fy, XCut mass flow)
+        got = [ln.strip() for ln in r.stdout.splitlines() if ln.strip().startswith(("Cx", "Cut("))]
+        assert got == want["_log_lines"]
     for name, h in want.items():
         if name.startswith("_"):
             continue
         p = tmp_path / name
         assert p.exists(), name
+        if name.endswith(".hf2d") and "_hf2d_nan_canonical" in want:
+            # the reference's record holds NaN in fields of a diverging model path;
+            # x87/SSE operand order decides the NaN sign bit there: compare with
+            # every NaN canonicalised (every other bit must match)
+            import numpy as np
+
+            a = np.fromfile(p, dtype=np.float64).copy()
+            a[np.isnan(a)] = np.nan
+            assert hashlib.sha256(a.tobytes()).hexdigest() == want["_hf2d_nan_canonical"], name
+            continue
         assert _sha(p) == h, "%s differs from the reference" % name

@@ -41,6 +41,24 @@ def _finite(text, nmax, nout=None):
     return t
 
 
+def _wedge(turb=0, tem=None, ns=None, ft=0, nx=120, ny=40, steps=30, **kw):
+    """Small Wedge15 variant: turbulence model / extension, flow type, extra keys."""
+    ns = bool(turb) if ns is None else ns
+    t = decks.wedge15(nx, ny, navier_stokes=ns, turbulence=turb, nmax=steps, nout=10)
+    t = decks.set_key(t, "FlowType", ft)
+    if tem is not None:
+        t = decks.set_key(t, "TurbExtModel", tem)
+    for k, v in kw.items():
+        t = decks.set_key(t, k.replace("__", ".").replace("Point_", "Point-"), v)
+    return _finite(t, steps, 10)
+
+
+def _with_objects(text, **kw):
+    for k, v in kw.items():
+        text = decks.set_key(text, k.replace("__", "."), v)
+    return text
+
+
 def cases():
     return {
         "wedge15_200x40_euler": _finite(decks.wedge15(200, 40, nmax=101, nout=25), 101, 25),
@@ -49,6 +67,44 @@ def cases():
         "wedge_keps_wallheat": _finite(_fixture_deck("Wedge.dat"), 30),
         "wedge15_200x60_ns_keps": _finite(decks.wedge15(200, 60, navier_stokes=True, turbulence=4,
                                                         nmax=30, nout=10), 30, 10),
+        # round 2: the rest of the reference's feature surface
+        "axisym_euler": _wedge(ft=1),
+        "axisym_keps": _wedge(turb=4, ft=1),
+        # the reference's SA diverges on this deck at iteration 3: the full SA path
+        # runs until then and the error snapshot must match as well
+        "spalart_allmaras_blowup": _wedge(turb=3, tem=10),
+        "spalart_allmaras_start": _wedge(turb=3, tem=10, TurbStartIter=100),
+        "prandtl": _wedge(turb=2, tem=0),
+        "van_driest": _wedge(turb=2, tem=1),
+        "escudier": _wedge(turb=2, tem=2, delta_bl=0.004),
+        "klebanoff": _wedge(turb=2, tem=3, delta_bl=0.004),
+        "smagorinsky": _wedge(turb=5),
+        "keps_chien": _wedge(turb=4, tem=5),
+        "keps_jones_launder": _wedge(turb=4, tem=6),
+        "keps_launder_sharma": _wedge(turb=4, tem=7),
+        "keps_rng": _wedge(turb=4, tem=8),
+        "bff_linear": _wedge(BFF=0),
+        "bff_square_relax": _wedge(BFF=3),
+        "bff_sqrt_relax": _wedge(BFF=5),
+        "zeldovich_reacting": _finite(decks.set_key(decks.reactor0d(12, 12, T=1500.0, nmax=20, nout=5),
+                                                    "ChemicalReactionsModel", 1), 20, 5),
+        "gas_source": _wedge(NumSrc=1, Src1__GasSrcSX=20, Src1__GasSrcSY=10, Src1__GasSrcEX=20,
+                             Src1__GasSrcEY=20, Src1__GasSrcIndex=3, Src1__Msrc=0.5, Src1__Tsrc=600.0,
+                             Src1__Tf_src=1000.0, Src1__StartIter=0),
+        "solid_rect": _wedge(NumRects=1, Rect1__Xstart=0.03, Rect1__Ystart=0.015, Rect1__DX=0.012, Rect1__DY=0.008,
+                             Rect1__Flow2D=1, Rect1__TurbulenceModel=0),
+        "circle": _wedge(NumCircles=1, Circle1__Xstart=0.04, Circle1__Ystart=0.02, Circle1__X0=0.047,
+                         Circle1__Y0=0.02, Circle1__MaterialID=1, Circle1__TurbulenceModel=0, Circle1__Flow2D=1),
+        "naca_airfoil": _wedge(NumAirfoils=1, Airfoil1__Xstart=0.025, Airfoil1__Ystart=0.022, Airfoil1__Type=0,
+                               Airfoil1__pp=0.4, Airfoil1__mm=0.02, Airfoil1__thick=0.12, Airfoil1__scale=0.04,
+                               Airfoil1__attack_angle=5.0, Airfoil1__Flow2D=1, Airfoil1__TurbulenceModel=0,
+                               # the reference reads Cx_Flow_Index for the airfoil Re only when is_Cx_calc = 1
+                               is_Cx_calc=1, x_body=0.02, y_body=0.01, dx_body=0.05, dy_body=0.025, Cx_Flow_Index=1),
+        "monitors_heatflux_cx": _wedge(turb=4, NumMonitorPoints=2, Point_1__X=0.05, Point_1__Y=0.02,
+                                       Point_2__X=0.1, Point_2__Y=0.01, isOutHeatFluxX=1, Cp_Flow_Index=1,
+                                       y_max=20, y_min=0, isOutHeatFluxY=1, is_Cx_calc=1, x_body=0.07,
+                                       y_body=0.0, dx_body=0.05, dy_body=0.012, Cx_Flow_Index=1),
+        "restart_from_hf2d": (_wedge(steps=20), 2),
     }
 
 
@@ -65,20 +121,34 @@ def main():
     ap.add_argument("--ref", default="/tmp/refexact/bin/OpenHyperFLOW2D-1.03")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    for name, text in cases().items():
+    for name, spec in cases().items():
         if a.only and name not in a.only:
             continue
+        text, runs = spec if isinstance(spec, tuple) else (spec, 1)
         d = os.path.join(FIX, "ref", name)
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "deck.dat"), "w") as f:
             f.write(text)
         with tempfile.TemporaryDirectory() as tmp:
             shutil.copy(os.path.join(d, "deck.dat"), tmp)
-            r = subprocess.run([a.ref, "deck.dat"], cwd=tmp, capture_output=True, text=True, errors="replace",
-                               timeout=1800)
+            # runs > 1: the later runs resume from the .hf2d the previous one wrote
+            for _ in range(runs):
+                r = subprocess.run([a.ref, "deck.dat"], cwd=tmp, capture_output=True, text=True, errors="replace",
+                                   timeout=1800)
             outs = sorted(f for f in os.listdir(tmp) if f.endswith((".plt", ".hf2d")))
             rec = {f: sha256(os.path.join(tmp, f)) for f in outs}
             rec["_returncode"] = r.returncode
+            rec["_runs"] = runs
+            # integral-quantity lines of the log (XCut mass flow, Cx/Cy/Fx/Fy)
+            rec["_log_lines"] = [ln.strip() for ln in r.stdout.splitlines() if ln.strip().startswith(("Cx", "Cut("))]
+            for f in outs:
+                if f.endswith(".hf2d"):
+                    import numpy as np
+
+                    arr = np.fromfile(os.path.join(tmp, f), dtype=np.float64).copy()
+                    if np.isnan(arr).any():   # NaN-sign-insensitive hash (see test_reference_golden.py)
+                        arr[np.isnan(arr)] = np.nan
+                        rec["_hf2d_nan_canonical"] = hashlib.sha256(arr.tobytes()).hexdigest()
         with open(os.path.join(d, "sha256.json"), "w") as f:
             json.dump(rec, f, indent=1, sort_keys=True)
         print(name, r.returncode, outs)
