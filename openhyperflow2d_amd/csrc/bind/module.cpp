@@ -27,21 +27,16 @@ struct PyComm : Comm {
   std::function<double(double)> f_min, f_sum;
   std::function<int(int)> f_maxi;
   std::function<py::bytes(py::bytes)> f_res;   // allgather-of-packs, returns concatenated bytes
-  // gather(gi0, gi1, strip bytes) -> list of (gi0, gi1, bytes) on rank 0
-  std::function<py::object(int, int, py::bytes)> f_gather;
-  void gather_columns(Field& J, int gi0, int gi1) override {
-    if (!f_gather) return;
+  // allgather(bytes) -> list of every rank's bytes, in rank order
+  std::function<py::object(py::bytes)> f_allgather;
+  std::vector<std::string> allgather_bytes(const std::string& mine) override {
+    if (!f_allgather || n == 1) return {mine};
     py::gil_scoped_acquire g;
-    const size_t col = (size_t)J.ny * sizeof(CellRecord);
-    py::object res = f_gather(gi0, gi1, py::bytes((const char*)&J.at(gi0, 0), (size_t)(gi1 - gi0) * col));
-    if (r != 0 || res.is_none()) return;
-    for (auto item : res) {
-      auto t = item.cast<py::tuple>();
-      const int a = t[0].cast<int>(), b = t[1].cast<int>();
-      std::string bytes = t[2].cast<py::bytes>();
-      if (bytes.size() != (size_t)(b - a) * col) throw std::runtime_error("gather_columns: bad strip size");
-      std::memcpy((void*)&J.at(a, 0), bytes.data(), bytes.size());
-    }
+    py::object res = f_allgather(py::bytes(mine));
+    std::vector<std::string> out;
+    for (auto item : res) out.push_back(item.cast<std::string>());
+    if ((int)out.size() != n) throw std::runtime_error("allgather_bytes: wrong rank count");
+    return out;
   }
   int rank() const override { return r; }
   int size() const override { return n; }
@@ -65,11 +60,22 @@ struct PyComm : Comm {
   }
 };
 
+// whole-grid host entry points refuse a trimmed strip rank's Case
+void need_whole(const Case& c) {
+  if (!c.J.whole())
+    throw std::runtime_error("this Case keeps only columns [" + std::to_string(c.J.i0) + ", " +
+                             std::to_string(c.J.i0 + c.J.nxl) + ") resident (strip rank)");
+}
+
 py::array_t<double> field_scalar(const Field& J, const std::string& name) {
   py::array_t<double> a({J.nx, J.ny});
   auto m = a.mutable_unchecked<2>();
   for (int i = 0; i < J.nx; i++)
     for (int j = 0; j < J.ny; j++) {
+      if (!J.resident(i)) {   // trimmed strip rank: other ranks' columns read 0
+        m(i, j) = 0.0;
+        continue;
+      }
       const CellRecord& c = J.at(i, j);
       double v = 0;
       if (name.size() == 2 && name[0] == 'S') v = c.S[name[1] - '0'];
@@ -246,12 +252,16 @@ PYBIND11_MODULE(_hf2d, m) {
           const auto& names = c.cfg.mech->species;
           const auto it = std::find(names.begin(), names.end(), sp);
           if (it == names.end()) throw std::runtime_error("unknown species " + sp);
-          const long q = it - names.begin(), NG = (long)c.J.nx * c.J.ny;
+          const int q = (int)(it - names.begin());
           py::array_t<double> a({c.J.nx, c.J.ny});
           auto m = a.mutable_unchecked<2>();
           for (int i = 0; i < c.J.nx; i++)
             for (int j = 0; j < c.J.ny; j++) {
-              const double r = c.mech_rhoY[(size_t)q * NG + (long)i * c.J.ny + j];
+              if (!c.J.resident(i)) {
+                m(i, j) = 0.0;
+                continue;
+              }
+              const double r = c.mech_rhoY[c.mech_idx(q, i, j)];
               const double rho = c.J.at(i, j).S[I_RHO];
               m(i, j) = frac ? (rho != 0 ? r / rho : 0.0) : r;
             }
@@ -264,59 +274,81 @@ PYBIND11_MODULE(_hf2d, m) {
         return c.cfg.mech ? c.cfg.mech->species : std::vector<std::string>{};
       })
       .def_property_readonly("mech_name", [](const Case& c) { return c.cfg.mech ? c.cfg.mech->name : std::string(); })
+      .def("trim_to_columns", &Case::trim_to_columns, py::arg("a"), py::arg("b"),
+           "strip rank: keep only columns [a, b) of the host field resident (after the solver uploaded its strip)")
+      .def_property_readonly("resident_columns", [](const Case& c) { return py::make_tuple(c.J.i0, c.J.i0 + c.J.nxl); })
       .def("records", [](const Case& c) {
+        need_whole(c);
         return py::bytes((const char*)c.J.c.data(), c.J.c.size() * sizeof(CellRecord));
       })
       .def("set_records", [](Case& c, py::bytes b) {
+        need_whole(c);
         std::string s = b;
         if (s.size() != c.J.c.size() * sizeof(CellRecord)) throw std::runtime_error("record size mismatch");
         std::memcpy((void*)c.J.c.data(), s.data(), s.size());
       })
-      .def("write_checkpoint", [](const Case& c, const std::string& p) { write_hf2d(p, c.J); })
+      .def("write_checkpoint", [](const Case& c, const std::string& p) {
+        need_whole(c);
+        write_hf2d(p, c.J);
+      })
       .def("read_checkpoint", [](Case& c, const std::string& p) { return read_hf2d(p, c.J); })
       .def("save_plt", [](const Case& c, const std::string& p, bool rewrite) {
+        need_whole(c);
         save_field_plt(p, c, c.J, c.global_time, rewrite);
       })
       .def("mass_flow_x", [](const Case& c, double x0, double y0, double dy) {
+        need_whole(c);
         return mass_flow_rate_x(c, c.J, x0, y0, dy);
       })
       // libOutCFD integrals on the host records (out_cfd_param.cpp)
       .def("flow2d_count", [](const Case& c) { return (int)c.flows2d.size(); })
       .def("area_x", [](const Case& c, double x0, double y0, double dy) { return calc_area(c, c.J, x0, y0, dy); })
       .def("x_force", [](const Case& c, double x0, double y0, double dx, double dy) {
+        need_whole(c);
+        need_whole(c);
         return x_force(c, c.J, x0, y0, dx, dy);
       })
       .def("y_force", [](const Case& c, double x0, double y0, double dx, double dy) {
+        need_whole(c);
         return y_force(c, c.J, x0, y0, dx, dy);
       })
       .def("x_force_ysym", [](const Case& c, double x0, double l, double d) {
+        need_whole(c);
         return x_force_ysym(c, c.J, x0, l, d);
       })
       .def("mid_section_area", [](const Case& c, double x0, double y0, double dx, double dy) {
+        need_whole(c);
         return mid_section_area(c, c.J, x0, y0, dx, dy);
       })
       .def("cx", [](const Case& c, double x0, double y0, double dx, double dy, int flow) {
+        need_whole(c);
         return calc_cx(c, c.J, x0, y0, dx, dy, c.flows2d.at(flow - 1));
       })
       .def("cy", [](const Case& c, double x0, double y0, double dx, double dy, int flow) {
+        need_whole(c);
         return calc_cy(c, c.J, x0, y0, dx, dy, c.flows2d.at(flow - 1));
       })
       .def("cd", [](const Case& c, double x0, double y0, double dy, int flow) {
+        need_whole(c);
         return calc_cd(c, c.J, x0, y0, dy, c.flows2d.at(flow - 1));
       })
       .def("cv", [](const Case& c, double x0, double y0, double dy, double p_amb, int flow) {
+        need_whole(c);
         return calc_cv(c, c.J, x0, y0, dy, p_amb, c.flows2d.at(flow - 1));
       })
       .def("average_pressure", [](const Case& c, double x0, double l, double d) {
+        need_whole(c);
         return average_pressure(c, c.J, x0, l, d);
       })
       .def("average_temperature", [](const Case& c, double x0, double l, double d, int mid_enthalpy) {
+        need_whole(c);
         return average_temperature(c, c.J, x0, l, d, mid_enthalpy);
       })
       .def("derived_field", [](const Case& c, const std::string& name) {
         // p* (total pressure), T* (total temperature), schlieren |grad rho| (libOutCFD)
         py::array_t<double> a({c.J.nx, c.J.ny});
         auto m = a.mutable_unchecked<2>();
+        need_whole(c);
         for (int i = 0; i < c.J.nx; i++)
           for (int j = 0; j < c.J.ny; j++) {
             const CellRecord& n = c.J.at(i, j);
@@ -330,6 +362,7 @@ PYBIND11_MODULE(_hf2d, m) {
         return a;
       })
       .def("save_heat_flux", [](const Case& c, const std::string& px, const std::string& py_) {
+        need_whole(c);
         if (!px.empty()) save_x_heat_flux(px, c, c.J);
         if (!py_.empty()) save_y_heat_flux(py_, c, c.J);
       });
@@ -359,7 +392,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("set_comm",
            [](SolverBase& s, int rank, int size, std::function<double(double)> fmin, std::function<double(double)> fsum,
               std::function<int(int)> fmaxi, std::function<py::bytes(py::bytes)> fres,
-              std::function<py::object(int, int, py::bytes)> fgather) {
+              std::function<py::object(py::bytes)> fallgather) {
              auto* c = new PyComm();
              c->r = rank;
              c->n = size;
@@ -367,11 +400,11 @@ PYBIND11_MODULE(_hf2d, m) {
              c->f_sum = fsum;
              c->f_maxi = fmaxi;
              c->f_res = fres;
-             c->f_gather = fgather;
+             c->f_allgather = fallgather;
              s.comm = c;   // leaked intentionally: lives as long as the solver
            },
            py::arg("rank"), py::arg("size"), py::arg("fmin"), py::arg("fsum"), py::arg("fmaxi"), py::arg("fres"),
-           py::arg("fgather") = nullptr)
+           py::arg("fallgather") = nullptr)
       .def("run",
            [](SolverBase& s, int max_cycles, const std::string& outdir, bool outputs, bool checkpoint, bool verbose,
               const std::string& metrics, const std::string& profile, long fault_step, int fault_rank,

@@ -96,13 +96,21 @@ struct Config {
 };
 
 // Cell field on the host: x-major (idx = i*MaxY + j) like the .hf2d file.
+// A strip rank keeps only the columns [i0, i0 + nxl) resident (its strip plus
+// one ghost column each side, Field::trim); nx stays the global width and
+// at() takes global column indices.
 struct Field {
   int nx = 0, ny = 0;
+  int i0 = 0, nxl = 0;   // resident columns
   std::vector<CellRecord> c;
   void resize(int X, int Y);
-  CellRecord& at(int i, int j) { return c[(size_t)i * ny + j]; }
-  const CellRecord& at(int i, int j) const { return c[(size_t)i * ny + j]; }
+  CellRecord& at(int i, int j) { return c[(size_t)(i - i0) * ny + j]; }
+  const CellRecord& at(int i, int j) const { return c[(size_t)(i - i0) * ny + j]; }
   bool in(long i, long j) const { return i >= 0 && j >= 0 && i < nx && j < ny; }
+  bool resident(long i) const { return i >= i0 && i < i0 + nxl; }
+  bool whole() const { return i0 == 0 && nxl == nx; }
+  // drop every column outside [a, b) (global indices, clipped to the grid)
+  void trim(int a, int b);
 };
 
 class Case {
@@ -118,9 +126,15 @@ class Case {
   long restart_iter = 0;     // iteration count from the .hf2d.meta sidecar of a preloaded checkpoint
   std::string swap_path;     // resolved checkpoint path ("" = none)
   std::ostream* log = nullptr;
-  // mechanism mode: species partial densities, species-major [ns][MaxX*MaxY]
+  // mechanism mode: species partial densities, species-major
+  // [ns][resident columns * MaxY] (the same columns as J)
   std::vector<real> mech_rhoY;
   std::string species_path() const { return swap_path + ".species"; }
+  long mech_n() const { return (long)J.nxl * J.ny; }
+  size_t mech_idx(int sp, int gi, int j) const { return (size_t)sp * mech_n() + (size_t)(gi - J.i0) * J.ny + j; }
+  // Strip ranks: keep only the columns [a, b) of J and mech_rhoY resident
+  // (after the backend uploaded its strip; host RSS then scales with the strip)
+  void trim_to_columns(int a, int b);
 
   // Build the whole problem from a deck.  workdir is where <Project>.hf2d is
   // looked up; checkpoint=false ignores any existing swap file.

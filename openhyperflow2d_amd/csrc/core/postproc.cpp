@@ -4,61 +4,82 @@
 #include <cmath>
 #include <cstdio>
 #include <fstream>
+#include <stdexcept>
 #include <vector>
 
 namespace hf2d {
 
-void save_field_plt(const std::string& path, const Case& cs, const Field& J, real global_time, bool rewrite) {
+std::string plt_header(const Case& cs, real global_time, int ncols) {
   const Config& C = cs.cfg;
-  std::ofstream o(path, rewrite ? std::ios::trunc : std::ios::app);
   char h1[1024], h2[256];
   std::snprintf(h1, sizeof h1,
                 "VARIABLES = X, %s, U, V, T, p, Rho, Y_fuel, Y_ox, Y_cp, Y_i, %s, Mach, l_min, y+, Cp\n",
                 C.FT == 1 ? "R" : "Y", C.is_p_asterisk_out ? "p*" : "mu_t/mu");
-  std::snprintf(h2, sizeof h2, "ZONE T=\"Time: %g sec.\" I= %i J= %i F=POINT\n", global_time, C.MaxX, C.MaxY);
-  o << h1 << h2;
+  std::snprintf(h2, sizeof h2, "ZONE T=\"Time: %g sec.\" I= %i J= %i F=POINT\n", global_time, ncols, C.MaxY);
+  return std::string(h1) + h2;
+}
+
+const GasFlow* plt_cx_flow(const Case& cs) {
+  const Config& C = cs.cfg;
+  return (C.is_Cx_calc && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size())
+             ? &cs.flows2d[C.Cx_Flow_index - 1]
+             : nullptr;
+}
+
+void plt_row(std::ostream& o, const Case& cs, const Field& J, int j, int ib, int ie, const GasFlow* cxf) {
+  const Config& C = cs.cfg;
   const real dx_out = (C.dx * C.MaxX) / (C.MaxX - 1);
   const real dy_out = (C.dy * C.MaxY) / (C.MaxY - 1);
-  const GasFlow* cxf = (C.is_Cx_calc && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size())
-                           ? &cs.flows2d[C.Cx_Flow_index - 1]
-                           : nullptr;
-  for (int j = 0; j < C.MaxY; j++) {
-    for (int i = 0; i < C.MaxX; i++) {
-      const CellRecord& n = J.at(i, j);
-      o << i * dx_out * 1.e3 << "  ";
-      o << dy_out * j * 1.e3 << "  ";
-      real Mach = 0;
-      if (!n.is(CT_SOLID)) {
-        o << n.U << "  " << n.V << "  " << n.Tg << "  " << n.p << "  " << n.S[0] << "  ";
-        const real A = std::sqrt(n.k * n.R * n.Tg + 1.e-30);
-        const real W = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
-        Mach = W / A;
-        if (n.S[0] != 0.) {
-          o << n.S[4] / n.S[0] << "  " << n.S[5] / n.S[0] << "  " << n.S[6] / n.S[0] << "  ";
-          o << std::fabs(1 - n.S[4] / n.S[0] - n.S[5] / n.S[0] - n.S[6] / n.S[0]) << "  ";
-          if (C.is_p_asterisk_out)
-            o << p_asterisk(n) << "  ";
-          else
-            o << n.mu_t / n.mu << "  ";
-        } else {
-          o << " +0. +0  +0  +0  +0  ";
-        }
-      } else {
-        o << "  0  0  " << n.Tg << "  0  0  0  0  0  0  0";
-      }
-      if (!n.is(CT_SOLID)) {
-        if (Mach > 1.e-30)
-          o << Mach << "  " << n.l_min << " " << n.y_plus;
+  for (int i = ib; i < ie; i++) {
+    const CellRecord& n = J.at(i, j);
+    o << i * dx_out * 1.e3 << "  ";
+    o << dy_out * j * 1.e3 << "  ";
+    real Mach = 0;
+    if (!n.is(CT_SOLID)) {
+      o << n.U << "  " << n.V << "  " << n.Tg << "  " << n.p << "  " << n.S[0] << "  ";
+      const real A = std::sqrt(n.k * n.R * n.Tg + 1.e-30);
+      const real W = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+      Mach = W / A;
+      if (n.S[0] != 0.) {
+        o << n.S[4] / n.S[0] << "  " << n.S[5] / n.S[0] << "  " << n.S[6] / n.S[0] << "  ";
+        o << std::fabs(1 - n.S[4] / n.S[0] - n.S[5] / n.S[0] - n.S[6] / n.S[0]) << "  ";
+        if (C.is_p_asterisk_out)
+          o << p_asterisk(n) << "  ";
         else
-          o << "  0  0  0  ";
+          o << n.mu_t / n.mu << "  ";
       } else {
-        o << "  0  0  0  ";
+        o << " +0. +0  +0  +0  +0  ";
       }
-      if (C.is_Cx_calc && cxf)
-        o << " " << calc_cp(n, *cxf) << "\n";
-      else
-        o << " 0\n";
+    } else {
+      o << "  0  0  " << n.Tg << "  0  0  0  0  0  0  0";
     }
+    if (!n.is(CT_SOLID)) {
+      if (Mach > 1.e-30)
+        o << Mach << "  " << n.l_min << " " << n.y_plus;
+      else
+        o << "  0  0  0  ";
+    } else {
+      o << "  0  0  0  ";
+    }
+    if (C.is_Cx_calc && cxf)
+      o << " " << calc_cp(n, *cxf) << "\n";
+    else
+      o << " 0\n";
+  }
+}
+
+void save_field_plt(const std::string& path, const Case& cs, const Field& J, real global_time, bool rewrite) {
+  save_field_plt_cols(path, cs, J, global_time, rewrite, 0, cs.cfg.MaxX);
+}
+
+void save_field_plt_cols(const std::string& path, const Case& cs, const Field& J, real global_time, bool rewrite,
+                         int ib, int ie) {
+  if (!J.resident(ib) || !J.resident(ie - 1)) throw std::runtime_error("save_field_plt: columns not resident");
+  std::ofstream o(path, rewrite ? std::ios::trunc : std::ios::app);
+  o << plt_header(cs, global_time, ie - ib);
+  const GasFlow* cxf = plt_cx_flow(cs);
+  for (int j = 0; j < cs.cfg.MaxY; j++) {
+    plt_row(o, cs, J, j, ib, ie, cxf);
     if (rewrite) o << "\n";
   }
 }
@@ -70,16 +91,11 @@ void save_rms_header(const std::string& path, const Config& C) {
     << (C.is_Cd_calc ? ", Cd(N), Cv(N)" : "") << "\n";
 }
 
-void append_rms(const std::string& path, long n, const real* rms, const Case& cs, const Field& J) {
+void append_rms(const std::string& path, long n, const real* rms, const Config& C, const real* cd_cv) {
   std::ofstream o(path, std::ios::app);
   o << n << " ";
   for (int i = 0; i < NEQ; i++) o << rms[i] << " ";
-  const Config& C = cs.cfg;
-  if (C.is_Cd_calc && C.Cd_Flow_index >= 1 && C.Cd_Flow_index <= (int)cs.flows2d.size()) {
-    const GasFlow& f = cs.flows2d[C.Cd_Flow_index - 1];
-    o << " " << calc_cd(cs, J, C.x0_nozzle, C.y0_nozzle, C.dy_nozzle, f) << " "
-      << calc_cv(cs, J, C.x0_nozzle, C.y0_nozzle, C.dy_nozzle, C.p_ambient, f) << " ";
-  }
+  if (cd_cv) o << " " << cd_cv[0] << " " << cd_cv[1] << " ";
   o << "\n";
 }
 
@@ -137,10 +153,10 @@ static bool in_box(const Config& C, int i, int j, real x0, real y0, real dx, rea
   return i >= (int)(x0 / C.dx) && i <= (int)((x0 + dx) / C.dx) && j >= (int)(y0 / C.dy) && j <= (int)((y0 + dy) / C.dy);
 }
 
-real x_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+void x_force_terms(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, int ib, int ie,
+                   std::vector<real>& fp, std::vector<real>& fd) {
   const Config& C = cs.cfg;
-  real Fp = 0, Fd = 0;
-  for (int i = 0; i < J.nx; i++)
+  for (int i = ib; i < ie; i++)
     for (int j = 0; j < J.ny; j++) {
       const CellRecord& n = J.at(i, j);
       if (!((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy))) continue;
@@ -152,24 +168,24 @@ real x_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy)
         Sp = 2 * M_PI * (j + 0.5) * C.dy * C.dy;
         Sd = 2 * M_PI * (j + 0.5) * C.dy * C.dx;
       }
+      // Fp -= x is Fp += -x exactly: the terms are folded in this order
       if (i > 0 && J.at(i - 1, j).is(CT_SOLID))
-        Fp -= Sp * n.p;
+        fp.push_back(-(Sp * n.p));
       else if (i < J.nx - 1 && J.at(i + 1, j).is(CT_SOLID))
-        Fp += Sp * n.p;
+        fp.push_back(Sp * n.p);
       const real tau = Sd * (n.mu + n.mu_t) * std::fabs(n.dUdy);
       if (j < J.ny - 1 && !J.at(i, j + 1).is(CT_SOLID)) {
-        Fd += J.at(i, j + 1).U > 0 ? tau : -tau;
+        fd.push_back(J.at(i, j + 1).U > 0 ? tau : -tau);
       } else if (j > 0 && !J.at(i, j - 1).is(CT_SOLID)) {
-        Fd += J.at(i, j - 1).U > 0 ? tau : -tau;
+        fd.push_back(J.at(i, j - 1).U > 0 ? tau : -tau);
       }
     }
-  return Fp + Fd;
 }
 
-real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+void y_force_terms(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, int ib, int ie,
+                   std::vector<real>& fp, std::vector<real>& fd) {
   const Config& C = cs.cfg;
-  real Fp = 0, Fd = 0;
-  for (int i = 0; i < J.nx; i++)
+  for (int i = ib; i < ie; i++)
     for (int j = 0; j < J.ny; j++) {
       const CellRecord& n = J.at(i, j);
       if (!((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy))) continue;
@@ -182,17 +198,34 @@ real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy)
         Sd = 2 * M_PI * n.y * C.dy;
       }
       if (j > 0 && J.at(i, j - 1).is(CT_SOLID))
-        Fp -= Sp * n.p;
+        fp.push_back(-(Sp * n.p));
       else if (j < J.ny - 1 && J.at(i, j + 1).is(CT_SOLID))
-        Fp += Sp * n.p;
+        fp.push_back(Sp * n.p);
       const real tau = -Sd * (n.mu + n.mu_t) * std::fabs(n.dVdx);
       if (i < J.nx - 1 && !J.at(i + 1, j).is(CT_SOLID)) {
-        Fd += J.at(i + 1, j).V > 0 ? tau : -tau;
+        fd.push_back(J.at(i + 1, j).V > 0 ? tau : -tau);
       } else if (i > 0 && !J.at(i - 1, j).is(CT_SOLID)) {
-        Fd += J.at(i - 1, j).V > 0 ? tau : -tau;
+        fd.push_back(J.at(i - 1, j).V > 0 ? tau : -tau);
       }
     }
-  return Fp + Fd;
+}
+
+real fold_terms(const std::vector<real>& t) {
+  real s = 0;
+  for (real v : t) s += v;
+  return s;
+}
+
+real x_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  std::vector<real> fp, fd;
+  x_force_terms(cs, J, x0, y0, dx, dy, 0, J.nx, fp, fd);
+  return fold_terms(fp) + fold_terms(fd);
+}
+
+real y_force(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+  std::vector<real> fp, fd;
+  y_force_terms(cs, J, x0, y0, dx, dy, 0, J.nx, fp, fd);
+  return fold_terms(fp) + fold_terms(fd);
 }
 
 // CalcXForceYSym2D (out_cfd_param.cpp:199-254): x force on the wall cells of
@@ -254,26 +287,31 @@ void smooth_x(real* A, int nx, int ny) {
     }
 }
 
-static real wall_span_x(const Case& cs, const Field& J, real x0, real y0, real dx, real dy) {
+void wall_span_terms(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, int ib, int ie,
+                     std::vector<real>& t) {
   const Config& C = cs.cfg;
-  real S = 0;
-  for (int i = 0; i < J.nx; i++) {
+  for (int i = ib; i < ie; i++) {
     bool hit = false;
     for (int j = 0; j < J.ny; j++) {
       const CellRecord& n = J.at(i, j);
       if ((n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP)) && in_box(C, i, j, x0, y0, dx, dy)) hit = true;
     }
-    if (hit) S += C.dx;
+    if (hit) t.push_back(C.dx);
   }
-  return S;
 }
 
+real body_pmax(real span, const GasFlow& f) { return f.ROG() * f.Wg2d() * f.Wg2d() * 0.5 * span; }
+
 real calc_cx(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f) {
-  const real Pmax = f.ROG() * f.Wg2d() * f.Wg2d() * 0.5 * wall_span_x(cs, J, x0, y0, dx, dy);
+  std::vector<real> t;
+  wall_span_terms(cs, J, x0, y0, dx, dy, 0, J.nx, t);
+  const real Pmax = body_pmax(fold_terms(t), f);
   return Pmax == 0. ? 0 : x_force(cs, J, x0, y0, dx, dy) / Pmax;
 }
 real calc_cy(const Case& cs, const Field& J, real x0, real y0, real dx, real dy, const GasFlow& f) {
-  const real Pmax = f.ROG() * f.Wg2d() * f.Wg2d() * 0.5 * wall_span_x(cs, J, x0, y0, dx, dy);
+  std::vector<real> t;
+  wall_span_terms(cs, J, x0, y0, dx, dy, 0, J.nx, t);
+  const real Pmax = body_pmax(fold_terms(t), f);
   return Pmax == 0. ? 0 : y_force(cs, J, x0, y0, dx, dy) / Pmax;
 }
 real calc_cp(const CellRecord& n, const GasFlow& f) {
@@ -353,16 +391,15 @@ static real near_lam(const Field& J, int i, int j, const CellRecord& n, int& cnt
   return s;
 }
 
-void save_x_heat_flux(const std::string& path, const Case& cs, const Field& J) {
+bool heat_flux_x_cols(const Case& cs, const Field& J, int ib, int ie, real* Q, real* Al, real* Cp, real* St) {
   const Config& C = cs.cfg;
-  std::ofstream o(path, std::ios::trunc);
-  o << "#VARIABLES = X, HeatFlux(X),  Alpha(X), Cp(X), St(X)\n";
-  const int NX = J.nx;
-  std::vector<real> Q(NX, 0.), Al(NX, 0.), Cp(NX, 0.), St(NX, 0.), QR(NX, 0.), AR(NX, 0.), Re(NX, 0.), Pr(NX, 0.);
-  if (C.Cp_Flow_index < 1 || C.Cp_Flow_index > (int)cs.flows2d.size()) return;
+  if (C.Cp_Flow_index < 1 || C.Cp_Flow_index > (int)cs.flows2d.size()) return false;
   const GasFlow& F = cs.flows2d[C.Cp_Flow_index - 1];
   const real Trec = (1 + 0.45 * (F.kg() - 1.0) * F.flow_MACH() * F.flow_MACH()) * F.Tg();
-  for (int i = 0; i < NX; i++)
+  for (int i = ib; i < ie; i++) {
+    // the reference also keeps laminar-correlation maxima (QR, AR) and Re, Pr
+    // for its _REF_TEST_ build; only the written columns are formed here
+    Q[i] = Al[i] = Cp[i] = St[i] = 0.;
     for (int j = std::max(0, C.y_min); j < std::min(C.y_max, J.ny - 1); j++) {
       const CellRecord& n = J.at(i, j);
       if (!n.is(CT_WALL_NO_SLIP)) continue;
@@ -370,51 +407,70 @@ void save_x_heat_flux(const std::string& path, const Case& cs, const Field& J) {
       const real lam_eff = near_lam(J, i, j, n, cnt) / cnt;
       real q = lam_eff * (n.Tg - C.Ts0) / C.dy;
       real alpha = lam_eff / C.dy;
-      const real re = (J.at(i, J.ny - 1).U * (i + 0.5) * C.dx * n.S[0]) / n.mu;
-      const real pr = n.mu * n.CP / n.lam;
-      const real Nu = re < 5.0e5 ? 0.332 * std::sqrt(re) * std::pow(pr, 1.0 / 3.0)
-                                 : 0.0296 * std::pow(re, 0.8) * std::pow(pr, 1.0 / 3.0);
-      real aref = Nu * n.lam / ((i + 0.5) * C.dx);
-      real qref = aref * (n.Tg - C.Ts0);
       const real st = q / (F.ROG() * F.Wg2d() * F.C * (Trec - C.Ts0));
       const real cp = calc_cp(n, F);
-      Re[i] = re;
-      Pr[i] = pr;
       if (Q[i] != 0.) {
-        q = std::max(Q[i], q);
-        QR[i] = std::max(QR[i], qref);
-        AR[i] = std::max(AR[i], aref);
-        Q[i] = q;
+        Q[i] = std::max(Q[i], q);
         Al[i] = std::max(Al[i], alpha);
       } else {
         Q[i] = q;
         Al[i] = alpha;
-        AR[i] = aref;
-        QR[i] = qref;
       }
       Cp[i] = cp;
       St[i] = st;
     }
-  // the reference's default build (no _REF_TEST_) writes X, Q, alpha, Cp, St;
-  // the laminar-correlation columns QR, AR, Re, Pr are kept for tests only
-  for (int i = 0; i < NX; i++) o << i * C.dx << " " << Q[i] << " " << Al[i] << " " << Cp[i] << " " << St[i] << "\n";
+  }
+  return true;
 }
 
-void save_y_heat_flux(const std::string& path, const Case& cs, const Field& J) {
-  const Config& C = cs.cfg;
+void write_x_heat_flux(const std::string& path, const Config& C, bool valid, const real* Q, const real* Al,
+                       const real* Cp, const real* St) {
   std::ofstream o(path, std::ios::trunc);
-  o << "#VARIABLES = Y, HeatFlux(Y)\n";
-  std::vector<real> Q(J.ny, 0.);
+  o << "#VARIABLES = X, HeatFlux(X),  Alpha(X), Cp(X), St(X)\n";
+  if (!valid) return;
+  // the reference's default build (no _REF_TEST_) writes X, Q, alpha, Cp, St
+  for (int i = 0; i < C.MaxX; i++) o << i * C.dx << " " << Q[i] << " " << Al[i] << " " << Cp[i] << " " << St[i] << "\n";
+}
+
+void save_x_heat_flux(const std::string& path, const Case& cs, const Field& J) {
+  const int NX = J.nx;
+  std::vector<real> Q(NX, 0.), Al(NX, 0.), Cp(NX, 0.), St(NX, 0.);
+  const bool ok = heat_flux_x_cols(cs, J, 0, NX, Q.data(), Al.data(), Cp.data(), St.data());
+  write_x_heat_flux(path, cs.cfg, ok, Q.data(), Al.data(), Cp.data(), St.data());
+}
+
+void heat_flux_y_terms(const Case& cs, const Field& J, int ib, int ie, std::vector<real>& jq) {
+  const Config& C = cs.cfg;
   for (int j = 0; j < J.ny; j++)
-    for (int i = 0; i < J.nx - 1; i++) {
+    for (int i = ib; i < std::min(ie, J.nx - 1); i++) {
       const CellRecord& n = J.at(i, j);
       if (!n.is(CT_WALL_NO_SLIP)) continue;
       int cnt;
       const real lam_eff = near_lam(J, i, j, n, cnt) / cnt;
-      real q = lam_eff * (n.Tg - C.Ts0) / C.dx;
-      Q[j] = (Q[j] != 0.) ? std::max(Q[j], q) : q;
+      jq.push_back((real)j);
+      jq.push_back(lam_eff * (n.Tg - C.Ts0) / C.dx);
     }
-  for (int j = 0; j < J.ny; j++) o << j * C.dy << " " << Q[j] << "\n";
+}
+
+void fold_heat_flux_y(std::vector<real>& Q, const std::vector<real>& jq) {
+  for (size_t k = 0; k + 1 < jq.size(); k += 2) {
+    real& Qj = Q[(size_t)jq[k]];
+    const real q = jq[k + 1];
+    Qj = (Qj != 0.) ? std::max(Qj, q) : q;
+  }
+}
+
+void write_y_heat_flux(const std::string& path, const Config& C, const std::vector<real>& Q) {
+  std::ofstream o(path, std::ios::trunc);
+  o << "#VARIABLES = Y, HeatFlux(Y)\n";
+  for (int j = 0; j < C.MaxY; j++) o << j * C.dy << " " << Q[j] << "\n";
+}
+
+void save_y_heat_flux(const std::string& path, const Case& cs, const Field& J) {
+  std::vector<real> jq, Q(J.ny, 0.);
+  heat_flux_y_terms(cs, J, 0, J.nx, jq);
+  fold_heat_flux_y(Q, jq);
+  write_y_heat_flux(path, cs.cfg, Q);
 }
 
 namespace {

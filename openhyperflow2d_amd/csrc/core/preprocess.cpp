@@ -419,8 +419,35 @@ struct PreCtx {
 void Field::resize(int X, int Y) {
   nx = X;
   ny = Y;
+  i0 = 0;
+  nxl = X;
   c.assign((size_t)X * Y, CellRecord{});
   std::memset((void*)c.data(), 0, c.size() * sizeof(CellRecord));
+}
+
+void Field::trim(int a, int b) {
+  a = std::max(a, i0);
+  b = std::min(b, i0 + nxl);
+  if (a >= b) throw std::runtime_error("Field::trim: empty column range");
+  std::vector<CellRecord> k((size_t)(b - a) * ny);
+  std::memcpy((void*)k.data(), (const void*)&at(a, 0), k.size() * sizeof(CellRecord));
+  c.swap(k);
+  i0 = a;
+  nxl = b - a;
+}
+
+void Case::trim_to_columns(int a, int b) {
+  a = std::max(a, J.i0);
+  b = std::min(b, J.i0 + J.nxl);
+  if (!mech_rhoY.empty()) {
+    const int ns = (int)(mech_rhoY.size() / (size_t)mech_n());
+    std::vector<real> k((size_t)ns * (b - a) * J.ny);
+    const size_t per = (size_t)(b - a) * J.ny;
+    for (int s = 0; s < ns; s++)
+      std::memcpy(&k[(size_t)s * per], &mech_rhoY[mech_idx(s, a, 0)], per * sizeof(real));
+    mech_rhoY.swap(k);
+  }
+  J.trim(a, b);
 }
 
 void Case::fill_node(CellRecord& n, int is_mu_t, int is_init) const {

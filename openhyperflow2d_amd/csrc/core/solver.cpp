@@ -9,9 +9,11 @@
 #include <cstring>
 #include <ostream>
 #include <stdexcept>
+#include <unordered_map>
 
 #include "checkpoint.hpp"
 #include "postproc.hpp"
+#include "stripio.hpp"
 
 namespace hf2d {
 
@@ -42,8 +44,7 @@ void HostArrays::allocate(int X, int Yn) {
   CT.assign(N, 0);
   TT.assign(N, 0);
   nb.assign(N, 0);
-  iw.assign(N, 0);
-  jw.assign(N, 0);
+  wslot.assign(N, -1);
 }
 
 void HostArrays::from_field(const Field& J, int gi0) {
@@ -90,9 +91,33 @@ void HostArrays::from_field(const Field& J, int gi0) {
       CT[idx] = c.CT;
       TT[idx] = c.TurbType;
       nb[idx] = (c.idXl ? NB_XL : 0) | (c.idXr ? NB_XR : 0) | (c.idYu ? NB_YU : 0) | (c.idYd ? NB_YD : 0);
-      iw[idx] = c.i_wall;
-      jw[idx] = c.j_wall;
     }
+  }
+}
+
+void HostArrays::wall_slots(const Case& cs, int gx0, int gi0, int gi1) {
+  std::unordered_map<long, int32_t> slot;
+  slot.reserve(cs.wall_nodes.size() * 2 + 1);
+  const long NY = cs.J.ny;
+  for (size_t k = 0; k < cs.wall_nodes.size(); k++)
+    slot[(long)cs.wall_nodes[k].first * NY + cs.wall_nodes[k].second] = (int32_t)k;
+  wslot.assign(N, -1);
+  for (int li = 0; li < nx; li++) {
+    const int gi = gx0 + li;
+    if (!cs.J.resident(gi)) continue;
+    for (int j = 0; j < ny; j++) {
+      const CellRecord& c = cs.J.at(gi, j);
+      const auto it = slot.find((long)c.i_wall * NY + c.j_wall);
+      if (it != slot.end()) wslot[(long)li * ny + j] = it->second;
+    }
+  }
+  wall_own.clear();
+  wall_own_slot.clear();
+  for (size_t k = 0; k < cs.wall_nodes.size(); k++) {
+    const int gi = cs.wall_nodes[k].first;
+    if (gi < gi0 || gi >= gi1) continue;
+    wall_own.push_back((long)(gi - gx0) * ny + cs.wall_nodes[k].second);
+    wall_own_slot.push_back((int32_t)k);
   }
 }
 
@@ -167,7 +192,6 @@ void HostArrays::allocate_mech(const Case& cs) {
 
 void HostArrays::mech_from_case(const Case& cs, int gi0) {
   if (!mech) return;
-  const long NG = (long)cs.J.nx * cs.J.ny;
   const real FT = (real)cs.cfg.FT;
   for (int li = 0; li < nx; li++) {
     const int gi = gi0 + li;
@@ -176,7 +200,7 @@ void HostArrays::mech_from_case(const Case& cs, int gi0) {
       const CellRecord& c = cs.J.at(gi, j);
       for (int sp = 0; sp < nsp; sp++) {
         const long o = (long)sp * N + idx;
-        const real r = cs.mech_rhoY[(size_t)sp * NG + (long)gi * ny + j];
+        const real r = cs.mech_rhoY[cs.mech_idx(sp, gi, j)];
         Ys[0][o] = Ys[1][o] = r;
         // inviscid start fluxes (the pre-processor's FillNode2D has no
         // species gradients either); the first fill rewrites them
@@ -192,11 +216,10 @@ void HostArrays::mech_from_case(const Case& cs, int gi0) {
 
 void HostArrays::mech_to_case(Case& cs, int gi0, int i_from, int i_to, int ybuf) const {
   if (!mech) return;
-  const long NG = (long)cs.J.nx * cs.J.ny;
   for (int li = i_from; li < i_to; li++)
     for (int j = 0; j < ny; j++)
       for (int sp = 0; sp < nsp; sp++)
-        cs.mech_rhoY[(size_t)sp * NG + (long)(gi0 + li) * ny + j] = Ys[ybuf][(long)sp * N + (long)li * ny + j];
+        cs.mech_rhoY[cs.mech_idx(sp, gi0 + li, j)] = Ys[ybuf][(long)sp * N + (long)li * ny + j];
 }
 
 void HostArrays::mech_view(SoA& s, int yb, int db) const {
@@ -252,8 +275,7 @@ SoA HostArrays::view(int sb, int db, int pb) {
   s.TT = TT.data();
   s.nb = nb.data();
   s.gf = gf.empty() ? nullptr : gf.data();
-  s.iw = iw.data();
-  s.jw = jw.data();
+  s.wslot = const_cast<int32_t*>(wslot.data());
   mech_view(s, sb, db);
   return s;
 }
@@ -367,6 +389,32 @@ void SolverBase::run_steps(long n, bool want_res_last) {
   sync_scalars();
 }
 
+void SolverBase::merge_wall_uw(const std::vector<int32_t>& slots, const std::vector<real>& vals,
+                               std::vector<real>& uw, std::vector<uint8_t>& ok) {
+  uw.assign(cs.wall_nodes.size(), 0.);
+  ok.assign(cs.wall_nodes.size(), 0);
+  auto take = [&](const int32_t* sl, const real* v, size_t n) {
+    for (size_t k = 0; k < n; k++) {
+      uw[(size_t)sl[k]] = v[k];
+      ok[(size_t)sl[k]] = 1;
+    }
+  };
+  if (comm->size() == 1) {
+    take(slots.data(), vals.data(), slots.size());
+    return;
+  }
+  std::string m((const char*)slots.data(), slots.size() * sizeof(int32_t));
+  m.append((const char*)vals.data(), vals.size() * sizeof(real));
+  for (const std::string& b : comm->allgather_bytes(m)) {
+    const size_t n = b.size() / (sizeof(int32_t) + sizeof(real));
+    std::vector<int32_t> sl(n);
+    std::vector<real> v(n);
+    std::memcpy(sl.data(), b.data(), n * sizeof(int32_t));
+    std::memcpy(v.data(), b.data() + n * sizeof(int32_t), n * sizeof(real));
+    take(sl.data(), v.data(), n);
+  }
+}
+
 void SolverBase::sample_monitors(std::vector<MonitorPoint>& mp) {
   if (mp.empty()) return;
   Field& J = cs.J;
@@ -468,7 +516,12 @@ void SolverBase::failure_snapshot(const RunOptions& opt, const std::string& dir,
                            "-err.plt";
   // the reference stamps the snapshot with GlobalTime, which advances only at
   // cycle ends (deeps2d_core.cpp:1264-1279, 1785-1788)
-  if (opt.write_outputs) save_field_plt(dir + "/" + name, cs, cs.J, cs.global_time, true);
+  // (a strip rank writes its own columns: the failure need not be collective)
+  if (opt.write_outputs) {
+    const auto own = owned_columns();
+    save_field_plt_cols(dir + "/" + name, cs, cs.J, cs.global_time, true, nr > 1 ? own.first : 0,
+                        nr > 1 ? own.second : cs.J.nx);
+  }
   if (log && (r == 0 || nr > 1)) {
     *log << "\n" << why;
     // the first owned active cell with Tg < 0 (deeps2d_core.cpp:1246-1316 report + PrintCond)
@@ -552,6 +605,8 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
     save_rms_header(rms_path, C);
     if (!C.monitors.empty()) save_monitors_header(mon_path, C);
   }
+  // collective output decisions must agree on every rank
+  const bool log_any = comm->allreduce_max_int(log ? 1 : 0) != 0;
   int I = 0;
   int monitor_cond = 1;
   bool interrupted = false;
@@ -580,6 +635,15 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
       }
       if (out_step) {
         if (!C.monitors.empty()) sample_monitors(C.monitors);
+        // nozzle Cd / Cv of the RMS file: evaluated by the owner of the cut
+        // column (collective, so every rank takes part)
+        real cd_cv[2];
+        const bool want_cd = C.isVerboseOutput && opt.write_outputs && C.is_Cd_calc && C.Cd_Flow_index >= 1 &&
+                             C.Cd_Flow_index <= (int)cs.flows2d.size();
+        if (want_cd) {
+          const auto own = owned_columns();
+          strip_cd_cv(*comm, cs, cs.J, own.first, own.second, cs.flows2d[C.Cd_Flow_index - 1], cd_cv);
+        }
         if (C.isVerboseOutput && root) {
           auto now = clk::now();
           const double d_time = std::chrono::duration<double>(now - mark).count();
@@ -597,7 +661,7 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
             }
           }
           if (opt.write_outputs) {
-            append_rms(rms_path, last_iter + this_iter, last_res.rms, cs, cs.J);
+            append_rms(rms_path, last_iter + this_iter, last_res.rms, C, want_cd ? cd_cv : nullptr);
             if (!C.monitors.empty()) append_monitors(mon_path, cs.global_time + cur_time_part, C.monitors);
           }
           if (log) {
@@ -618,30 +682,35 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
       cycle_update();
     }
     Field& J = cs.J;
+    const auto own = owned_columns();
     {
-      PhaseScope ph(*this, "gather");
+      // each rank refreshes only its strip (+ the neighbours' edge columns
+      // that the wall integrals read); nothing is gathered
+      PhaseScope ph(*this, "download");
       download(J);
-      if (comm->size() > 1) comm->gather_columns(J, owned_columns().first, owned_columns().second);
+      strip_exchange_ghosts(*comm, J, own.first, own.second);
     }
     PhaseScope ph_out(*this, "outputs");
     step_seconds = std::chrono::duration<double>(clk::now() - t_cycle).count();
-    if (root) {
-      for (size_t x = 0; x < C.xcuts.size() && log; x++) {
+    for (size_t x = 0; x < C.xcuts.size() && log_any; x++) {
+      const real mf = strip_mass_flow(*comm, cs, J, own.first, own.second, C.xcuts[x].x0, C.xcuts[x].y0, C.xcuts[x].dy);
+      if (root && log) {
         char b[256];
         std::snprintf(b, sizeof b, "Cut(%zu) X=%g Y=%g dY=%g MassFlow=%g  (kg/sec*m)\n", x + 1, C.xcuts[x].x0,
-                      C.xcuts[x].y0, C.xcuts[x].dy, mass_flow_rate_x(cs, J, C.xcuts[x].x0, C.xcuts[x].y0, C.xcuts[x].dy));
+                      C.xcuts[x].y0, C.xcuts[x].dy, mf);
         *log << b;
       }
-      if (opt.write_outputs) {
-        save_field_plt(dir + "/" + C.out_file, cs, J, cs.global_time, true);
-        if ((I / C.NSaveStep) * C.NSaveStep == I) save_field_plt(dir + "/" + C.tecplot_file, cs, J, cs.global_time, false);
-      }
-      if (log) {
-        char b[256];
-        std::snprintf(b, sizeof b, "HyperFLOW/DEEPS computation cycle time=%g sec ( average  speed %g step/sec).       \n",
-                      step_seconds, C.Nmax / step_seconds);
-        *log << b << std::flush;
-      }
+    }
+    if (opt.write_outputs) {
+      strip_write_plt(*comm, dir + "/" + C.out_file, cs, J, own.first, own.second, cs.global_time, true);
+      if ((I / C.NSaveStep) * C.NSaveStep == I)
+        strip_write_plt(*comm, dir + "/" + C.tecplot_file, cs, J, own.first, own.second, cs.global_time, false);
+    }
+    if (root && log) {
+      char b[256];
+      std::snprintf(b, sizeof b, "HyperFLOW/DEEPS computation cycle time=%g sec ( average  speed %g step/sec).       \n",
+                    step_seconds, C.Nmax / step_seconds);
+      *log << b << std::flush;
     }
     I++;
     last_iter += iter;
@@ -651,36 +720,36 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
     on_cycle_roll();
     cycle++;
     cycles++;
-    if (root) {
-      if (opt.write_outputs && C.isOutHeatFluxX) save_x_heat_flux(dir + "/HeatFlux-X-" + C.out_file, cs, J);
-      if (opt.write_outputs && C.isOutHeatFluxY) save_y_heat_flux(dir + "/HeatFlux-Y-" + C.out_file, cs, J);
-      if (C.is_Cx_calc && log && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size()) {
-        const GasFlow& f = cs.flows2d[C.Cx_Flow_index - 1];
-        *log << "\nCx = " << calc_cx(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body, f)
-             << " Cy = " << calc_cy(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body, f)
-             << " Fx = " << x_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body)
-             << " Fy = " << y_force(cs, J, C.x0_body, C.y0_body, C.dx_body, C.dy_body) << "\n";
-      }
-      if (opt.write_checkpoint) {
-        PhaseScope ph(*this, "outputs.checkpoint");   // nested in "outputs"
-        write_hf2d(dir + "/" + C.swap_file, J);
-        write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
-      }
+    if (opt.write_outputs && C.isOutHeatFluxX)
+      strip_heat_flux_x(*comm, dir + "/HeatFlux-X-" + C.out_file, cs, J, own.first, own.second);
+    if (opt.write_outputs && C.isOutHeatFluxY)
+      strip_heat_flux_y(*comm, dir + "/HeatFlux-Y-" + C.out_file, cs, J, own.first, own.second);
+    if (C.is_Cx_calc && log_any && C.Cx_Flow_index >= 1 && C.Cx_Flow_index <= (int)cs.flows2d.size()) {
+      real F[4];
+      strip_body_forces(*comm, cs, J, own.first, own.second, cs.flows2d[C.Cx_Flow_index - 1], F);
+      if (root && log) *log << "\nCx = " << F[0] << " Cy = " << F[1] << " Fx = " << F[2] << " Fy = " << F[3] << "\n";
+    }
+    if (opt.write_checkpoint) {
+      PhaseScope ph(*this, "outputs.checkpoint");   // nested in "outputs"
+      strip_write_hf2d(*comm, dir + "/" + C.swap_file, J, own.first, own.second);
+      if (root) write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
     }
     if (opt.write_checkpoint && C.mech_mode()) {
       // versioned species sidecar (mechanism_io.hpp): each rank writes the
       // byte range of its own columns
       PhaseScope ph(*this, "outputs.checkpoint_species");
-      const auto own = owned_columns();
-      write_species_slab(dir + "/" + C.swap_file + ".species", *C.mech, J.nx, J.ny, cs.mech_rhoY.data(),
-                         (long)J.nx * J.ny, own.first, own.first, own.second - own.first);
+      write_species_slab(dir + "/" + C.swap_file + ".species", *C.mech, J.nx, J.ny, cs.mech_rhoY.data(), cs.mech_n(),
+                         own.first - J.i0, own.first, own.second - own.first);
     }
     if (C.MonitorIndex < 5)
       monitor_cond = last_res.max_rms > C.ExitMonitorValue ? 1 : 0;
     else
       monitor_cond = cs.global_time < C.ExitMonitorValue ? 1 : 0;
   } while (!interrupted && monitor_cond && (opt.max_cycles < 0 || cycles < opt.max_cycles));
-  if (root && opt.write_outputs) save_field_plt(dir + "/" + C.out_file, cs, cs.J, cs.global_time, true);
+  if (opt.write_outputs) {
+    const auto own = owned_columns();
+    strip_write_plt(*comm, dir + "/" + C.out_file, cs, cs.J, own.first, own.second, cs.global_time, true);
+  }
   return cycles;
 }
 
@@ -705,6 +774,7 @@ void RefSolver::poison_cell(int gi, int j) { cs.J.at(gi, j).S[I_RHOE] = -1.0e30;
 
 void CpuSolver::upload() {
   h.from_field(cs.J, gi0 - l_off);
+  h.wall_slots(cs, gi0 - l_off, gi0, gi1);
   h.mech_from_case(cs, gi0 - l_off);
   compute_generic_flags(cs, h);
   sbuf = 0;
@@ -997,12 +1067,19 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
 
 void CpuSolver::cycle_update() {
   if (cs.cfg.ProblemType != SM_NS || cs.cfg.semantics == Semantics::SERIAL) return;
-  StepParams P = make_params(last_iter);
-  P.nx = h.nx;
-  P.ny = h.ny;
   SoA s = h.view(0, dsbuf, pbuf);
-  for (int i = l_off; i < l_off + (gi1 - gi0); i++)
-    for (int j = 0; j < h.ny; j++) y_plus_cell(P, s, i, j, gi0 - l_off);
+  std::vector<int32_t> sl;
+  std::vector<real> v;
+  for (size_t k = 0; k < h.wall_own.size(); k++) {
+    if (!is_wall_gas(s.CT[h.wall_own[k]])) continue;
+    sl.push_back(h.wall_own_slot[k]);
+    v.push_back(wall_friction_velocity(s, h.wall_own[k]));
+  }
+  std::vector<real> uw;
+  std::vector<uint8_t> ok;
+  merge_wall_uw(sl, v, uw, ok);
+  for (long idx = (long)l_off * h.ny; idx < (long)(l_off + (gi1 - gi0)) * h.ny; idx++)
+    y_plus_apply(s, idx, uw.data(), ok.data());
 }
 
 // ---------------------------------------------------------------------------

@@ -42,7 +42,9 @@ struct HostArrays {
   std::vector<u64> CT, TT;
   std::vector<uint8_t> nb;
   std::vector<uint8_t> gf;  // GF_* traffic flags (compute_generic_flags)
-  std::vector<int32_t> iw, jw;
+  std::vector<int32_t> wslot;       // cell -> its wall's index in Case::wall_nodes (-1 none)
+  std::vector<long> wall_own;        // local index of each wall node this strip owns
+  std::vector<int32_t> wall_own_slot;   // ... and its index in Case::wall_nodes
   std::vector<real> time;   // per-cell record time (checkpoint only)
   // mechanism mode (SK_MECH): species block, species-major [s * N + idx]
   int nsp = 0;
@@ -60,6 +62,8 @@ struct HostArrays {
   SoA view(int sbuf, int dsbuf, int pbuf);
   // sets the species members of a view (ybuf: species state buffer)
   void mech_view(SoA& s, int ybuf, int dsbuf) const;
+  // wslot / wall_own for columns [gi0, gi1) owned, local column 0 = global gx0
+  void wall_slots(const Case& cs, int gx0, int gi0, int gi1);
 };
 
 // Communication hooks for multi-rank (strip) runs.  Single-rank: no-ops.
@@ -71,10 +75,13 @@ struct Comm {
   virtual void allreduce_residual(ResidualPack&) {}
   virtual int allreduce_max_int(int v) { return v; }
   virtual real allreduce_sum(real v) { return v; }
-  // Outputs of a strip-decomposed run: after every rank refreshed its own
-  // columns [gi0, gi1) of J, rank 0 receives all columns (x-major records of
-  // one column are contiguous, so a strip is one byte range).
-  virtual void gather_columns(Field& /*J*/, int /*gi0*/, int /*gi1*/) {}
+  // Variable-size all-gather: every rank receives every rank's bytes, in rank
+  // order.  Carries the outputs of a strip run (stripio.hpp: row lengths,
+  // ghost columns, integral terms) -- never a whole field.
+  virtual std::vector<std::string> allgather_bytes(const std::string& mine) { return {mine}; }
+  void barrier() {
+    if (size() > 1) (void)allgather_bytes(std::string());
+  }
 };
 
 struct RunOptions {
@@ -134,6 +141,10 @@ class SolverBase {
   // called after an outer-cycle roll-over (cur_time_part folded into global_time)
   virtual void on_cycle_roll() {}
   StepParams make_params(long it) const;
+  // y+ across strips: every wall node's friction velocity from its owner
+  // (slots/vals: this rank's gas wall nodes) -> uw/ok over Case::wall_nodes
+  void merge_wall_uw(const std::vector<int32_t>& slots, const std::vector<real>& vals, std::vector<real>& uw,
+                     std::vector<uint8_t>& ok);
   // Overwrite the energy of global cell (gi, j) (owned by this backend) with
   // a negative value: fault injection for the Tg < 0 failure path.
   virtual void poison_cell(int gi, int j) = 0;

@@ -76,8 +76,7 @@ struct SoA {
   u64* TT = nullptr;
   uint8_t* nb = nullptr;
   uint8_t* gf = nullptr;   // GF_* flags (nullptr: all set)
-  int32_t* iw = nullptr;
-  int32_t* jw = nullptr;
+  int32_t* wslot = nullptr;   // nearest wall of the cell: index into Case::wall_nodes (-1 none)
   // mechanism mode (SK_MECH): species partial densities and their fluxes,
   // blending factors and Cauchy dS, species-major [s * N + idx]
   const MechData* mech = nullptr;
@@ -901,19 +900,21 @@ HF_HD inline void wall_heat_wall_cell(const StepParams& P, const SoA& s, const r
 }
 
 // y+ from the friction velocity of the nearest wall node (the MPI build's
-// per-cycle ParallelRecalc_y_plus, deeps2d_core.cpp:2291-2322, in O(N) form).
-HF_HD inline void y_plus_cell(const StepParams& P, const SoA& s, int i, int j, int gx0) {
-  const long idx = (long)i * P.ny + j;
-  const u64 ct = s.CT[idx];
-  if (!has_all(ct, CT_NODE_IS_SET) || has_all(ct, CT_SOLID)) return;
-  const int iw = s.iw[idx] - gx0, jw = s.jw[idx];
-  if (iw < 0 || iw >= P.nx || jw < 0 || jw >= P.ny) return;
-  const long w = (long)iw * P.ny + jw;
-  if (!is_wall_gas(s.CT[w])) return;
+// per-cycle ParallelRecalc_y_plus, deeps2d_core.cpp:2291-2322, in O(N) form):
+// the owner of each wall node forms its friction velocity, the values of all
+// strips are merged (SolverBase::merge_wall_uw), then every cell takes its
+// wall's -- a cell whose wall lies in another strip sees that strip's value.
+HF_HD inline real wall_friction_velocity(const SoA& s, long w) {
   const long N = s.N;
   const real tau_w = (std::fabs(s.grad[G_DUDY * N + w]) + std::fabs(s.grad[G_DVDX * N + w])) * s.mu[w];
-  const real U_w = std::sqrt(tau_w / s.S[w] + 1e-30);
-  s.y_plus[idx] = std::fabs(U_w * s.l_min[idx] * s.S[idx] / s.mu[idx]);
+  return std::sqrt(tau_w / s.S[w] + 1e-30);
+}
+HF_HD inline void y_plus_apply(const SoA& s, long idx, const real* uw, const uint8_t* uw_ok) {
+  const u64 ct = s.CT[idx];
+  if (!has_all(ct, CT_NODE_IS_SET) || has_all(ct, CT_SOLID)) return;
+  const int k = s.wslot[idx];
+  if (k < 0 || !uw_ok[k]) return;
+  s.y_plus[idx] = std::fabs(uw[k] * s.l_min[idx] * s.S[idx] / s.mu[idx]);
 }
 
 }  // namespace hf2d

@@ -824,11 +824,20 @@ __global__ __launch_bounds__(BLOCK) void hf2d_wall_wall(StepParams P, SoA s, con
   wall_heat_wall_cell(P, s, qdir, i, j);
 }
 
-__global__ __launch_bounds__(BLOCK) void hf2d_yplus(StepParams P, SoA s, long c0, long c1, int gx0) {
+// K10 in two passes: friction velocity of the wall nodes this strip owns
+// (merged over the strips on the host), then y+ of every owned cell
+__global__ __launch_bounds__(BLOCK) void hf2d_wall_uw(SoA s, const long* own, int n, real* uw, uint8_t* ok) {
+  const int k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= n) return;
+  const long w = own[k];
+  const bool g = is_wall_gas(s.CT[w]);
+  ok[k] = g ? 1 : 0;
+  uw[k] = g ? wall_friction_velocity(s, w) : 0.;
+}
+__global__ __launch_bounds__(BLOCK) void hf2d_yplus(SoA s, long c0, long c1, const real* uw, const uint8_t* ok) {
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   if (c >= c1) return;
-  const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-  y_plus_cell(P, s, i, j, gx0);
+  y_plus_apply(s, c, uw, ok);
 }
 
 
@@ -1026,17 +1035,12 @@ struct LocalHostComm : Comm {
   std::shared_ptr<LocalGroup> g;
   int r;
   LocalHostComm(std::shared_ptr<LocalGroup> g_, int r_) : g(std::move(g_)), r(r_) {}
-  void gather_columns(Field& J, int gi0, int gi1) override {
-    g->fields[r] = &J;
-    g->cols[r] = {gi0, gi1};
+  std::vector<std::string> allgather_bytes(const std::string& mine) override {
+    g->blobs[r] = mine;
     g->barrier();
-    if (r == 0)
-      for (int q = 1; q < g->n; q++) {
-        const auto c = g->cols[q];
-        std::memcpy((void*)&J.at(c.first, 0), (const void*)&g->fields[q]->at(c.first, 0),
-                    (size_t)(c.second - c.first) * J.ny * sizeof(CellRecord));
-      }
+    std::vector<std::string> all(g->blobs.begin(), g->blobs.end());
     g->barrier();
+    return all;
   }
   int rank() const override { return r; }
   int size() const override { return g->n; }
@@ -1069,7 +1073,11 @@ struct DeviceSolver::Impl {
   real *Spre[2], *P2[2];
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
-  int32_t *iw, *jw;
+  int32_t* wslot;
+  // K10 (y+): owned wall nodes, their friction velocities, all strips' values
+  long* wall_own = nullptr;
+  real *wall_uw = nullptr, *uw_all = nullptr;
+  uint8_t *wall_ok = nullptr, *uw_all_ok = nullptr;
   // mechanism mode (SK_MECH): species block, Ys ping-pongs with S (sbuf)
   MechData* mech = nullptr;
   int nsp = 0;
@@ -1180,8 +1188,7 @@ struct DeviceSolver::Impl {
     s.TT = TT;
     s.nb = nb;
     s.gf = gf;
-    s.iw = iw;
-    s.jw = jw;
+    s.wslot = wslot;
     mech_view(s, sb, db);
     return s;
   }
@@ -1267,8 +1274,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.CT = m.mem.alloc<u64>(N);
   m.TT = m.mem.alloc<u64>(N);
   m.nb = m.mem.alloc<uint8_t>(N);
-  m.iw = m.mem.alloc<int32_t>(N);
-  m.jw = m.mem.alloc<int32_t>(N);
+  m.wslot = m.mem.alloc<int32_t>(N);
   h.allocate_mech(c);
   if (h.mech) {
     m.nsp = h.nsp;
@@ -1334,9 +1340,19 @@ void DeviceSolver::upload() {
   flush_pending();
   HIP_CHECK(hipSetDevice(dev));
   h.from_field(cs.J, gi0 - l_off);
+  h.wall_slots(cs, gi0 - l_off, gi0, gi1);
   Impl& m = *impl;
   hipStream_t st = m.stream;
   const long N = h.N;
+  if (!m.wall_own) {   // K10 buffers (sizes fixed by the grid's wall nodes)
+    m.wall_own = m.mem.alloc<long>(h.wall_own.size());
+    m.wall_uw = m.mem.alloc<real>(h.wall_own.size());
+    m.wall_ok = m.mem.alloc<uint8_t>(h.wall_own.size());
+    m.uw_all = m.mem.alloc<real>(cs.wall_nodes.size());
+    m.uw_all_ok = m.mem.alloc<uint8_t>(cs.wall_nodes.size());
+  }
+  if (!h.wall_own.empty())
+    HIP_CHECK(hipMemcpyAsync(m.wall_own, h.wall_own.data(), h.wall_own.size() * sizeof(long), hipMemcpyHostToDevice, st));
   auto cp = [&](void* d, const void* s, size_t bytes) { HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyHostToDevice, st)); };
   const size_t EQB = NEQ * N * sizeof(real), SB = N * sizeof(real);
   for (int b = 0; b < 2; b++) {
@@ -1390,8 +1406,7 @@ void DeviceSolver::upload() {
     cp(m.lb, lean_bytes.data(), N);
   }
   lean_state = 0;
-  cp(m.iw, h.iw.data(), N * sizeof(int32_t));
-  cp(m.jw, h.jw.data(), N * sizeof(int32_t));
+  cp(m.wslot, h.wslot.data(), N * sizeof(int32_t));
   cp(m.species, &cs.cfg.species, sizeof(SpeciesProps));
   if (h.mech) {
     h.mech_from_case(cs, gi0 - l_off);
@@ -1596,14 +1611,36 @@ void DeviceSolver::cycle_update() {
   p2p_complete();
   Impl& m = *impl;
   if (cs.cfg.ProblemType == SM_NS && cs.cfg.semantics != Semantics::SERIAL) {
-    StepParams P = make_params(last_iter);
-    P.nx = h.nx;
-    P.ny = h.ny;
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
-    const long c0 = (long)l_off * h.ny, c1 = (long)(l_off + (gi1 - gi0)) * h.ny;
-    const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL(hf2d_yplus, dim3(nb), dim3(BLOCK), 0, m.stream, P, s, c0, c1, gi0 - l_off);
-    HIP_CHECK(hipGetLastError());
+    const int nw = (int)h.wall_own.size(), nall = (int)cs.wall_nodes.size();
+    std::vector<real> v(nw);
+    std::vector<uint8_t> g(nw);
+    if (nw) {
+      hipLaunchKernelGGL(hf2d_wall_uw, dim3((nw + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, m.stream, s, m.wall_own, nw,
+                         m.wall_uw, m.wall_ok);
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipMemcpyAsync(v.data(), m.wall_uw, nw * sizeof(real), hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipMemcpyAsync(g.data(), m.wall_ok, nw, hipMemcpyDeviceToHost, m.stream));
+      HIP_CHECK(hipStreamSynchronize(m.stream));
+    }
+    std::vector<int32_t> sl;
+    std::vector<real> vals;
+    for (int k = 0; k < nw; k++)
+      if (g[k]) {
+        sl.push_back(h.wall_own_slot[k]);
+        vals.push_back(v[k]);
+      }
+    std::vector<real> uw;
+    std::vector<uint8_t> ok;
+    merge_wall_uw(sl, vals, uw, ok);
+    if (nall) {
+      HIP_CHECK(hipMemcpyAsync(m.uw_all, uw.data(), nall * sizeof(real), hipMemcpyHostToDevice, m.stream));
+      HIP_CHECK(hipMemcpyAsync(m.uw_all_ok, ok.data(), nall, hipMemcpyHostToDevice, m.stream));
+      const long c0 = (long)l_off * h.ny, c1 = (long)(l_off + (gi1 - gi0)) * h.ny;
+      const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+      hipLaunchKernelGGL(hf2d_yplus, dim3(nb), dim3(BLOCK), 0, m.stream, s, c0, c1, m.uw_all, m.uw_all_ok);
+      HIP_CHECK(hipGetLastError());
+    }
   }
   HIP_CHECK(hipStreamSynchronize(m.stream));
 }
@@ -1630,36 +1667,30 @@ struct RcclHostComm : Comm {
   real allreduce_min(real v) override { return reduce1(v, ncclMin); }
   real allreduce_sum(real v) override { return reduce1(v, ncclSum); }
   int allreduce_max_int(int v) override { return (int)reduce1((double)v, ncclMax); }
-  // rank 0 receives every strip through a device staging buffer (outputs
-  // only: once per outer cycle)
-  void gather_columns(Field& J, int gi0, int gi1) override {
-    const size_t col = (size_t)J.ny * sizeof(CellRecord);
-    // column ranges of all ranks
-    int* dcols = (int*)buf;
-    int mine[2] = {gi0, gi1};
-    HIP_CHECK(hipMemcpyAsync(dcols, mine, sizeof mine, hipMemcpyHostToDevice, st));
-    NCCL_CHECK(ncclAllGather(dcols, dcols + 2, 2, ncclInt32, c, st));
-    std::vector<int> cols(2 * n);
-    HIP_CHECK(hipMemcpyAsync(cols.data(), dcols + 2, sizeof(int) * 2 * n, hipMemcpyDeviceToHost, st));
+  // variable-size all-gather through a device staging buffer: the sizes
+  // first, then every rank's bytes padded to the largest (outputs only:
+  // row lengths, ghost columns and integral terms once per outer cycle)
+  std::vector<std::string> allgather_bytes(const std::string& mine) override {
+    long long* dsz = (long long*)buf;
+    const long long me = (long long)mine.size();
+    HIP_CHECK(hipMemcpyAsync(dsz, &me, sizeof me, hipMemcpyHostToDevice, st));
+    NCCL_CHECK(ncclAllGather(dsz, dsz + 1, 1, ncclInt64, c, st));
+    std::vector<long long> sz(n);
+    HIP_CHECK(hipMemcpyAsync(sz.data(), dsz + 1, sizeof(long long) * n, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    size_t maxb = 0;
-    for (int q = 0; q < n; q++) maxb = std::max(maxb, (size_t)(cols[2 * q + 1] - cols[2 * q]) * col);
+    size_t maxb = 1;
+    for (long long v : sz) maxb = std::max(maxb, (size_t)v);
     char* stage = nullptr;
-    HIP_CHECK(hipMalloc((void**)&stage, std::max<size_t>(maxb, 1)));
-    if (r == 0) {
-      for (int q = 1; q < n; q++) {
-        const size_t bytes = (size_t)(cols[2 * q + 1] - cols[2 * q]) * col;
-        NCCL_CHECK(ncclRecv(stage, bytes, ncclChar, q, c, st));
-        HIP_CHECK(hipMemcpyAsync((void*)&J.at(cols[2 * q], 0), stage, bytes, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-      }
-    } else {
-      const size_t bytes = (size_t)(gi1 - gi0) * col;
-      HIP_CHECK(hipMemcpyAsync(stage, (const void*)&J.at(gi0, 0), bytes, hipMemcpyHostToDevice, st));
-      NCCL_CHECK(ncclSend(stage, bytes, ncclChar, 0, c, st));
-      HIP_CHECK(hipStreamSynchronize(st));
-    }
+    HIP_CHECK(hipMalloc((void**)&stage, maxb * (n + 1)));
+    if (me) HIP_CHECK(hipMemcpyAsync(stage, mine.data(), (size_t)me, hipMemcpyHostToDevice, st));
+    NCCL_CHECK(ncclAllGather(stage, stage + maxb, maxb, ncclChar, c, st));
+    std::string flat(maxb * n, '\0');
+    HIP_CHECK(hipMemcpyAsync(&flat[0], stage + maxb, maxb * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
     HIP_CHECK(hipFree(stage));
+    std::vector<std::string> all(n);
+    for (int q = 0; q < n; q++) all[q] = flat.substr((size_t)q * maxb, (size_t)sz[q]);
+    return all;
   }
   void allreduce_residual(ResidualPack& p) override {
     std::vector<ResidualPack> all(n);

@@ -21,7 +21,7 @@ bool gpu_available();
 // (RCCL refuses two ranks on one device).
 struct LocalGroup {
   explicit LocalGroup(int n_)
-      : n(n_), send_l(n_), send_r(n_), dt_src(n_, nullptr), vals(n_), packs(n_), fields(n_, nullptr), cols(n_) {}
+      : n(n_), send_l(n_), send_r(n_), dt_src(n_, nullptr), vals(n_), packs(n_), blobs(n_) {}
   int n;
   std::mutex mu;
   std::condition_variable cv;
@@ -31,8 +31,7 @@ struct LocalGroup {
   std::vector<const unsigned long long*> dt_src;   // device dt slot of each rank
   std::vector<double> vals;
   std::vector<ResidualPack> packs;
-  std::vector<Field*> fields;
-  std::vector<std::pair<int, int>> cols;
+  std::vector<std::string> blobs;   // allgather_bytes slots
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     const long g = gen;

@@ -68,6 +68,10 @@ class DistributedSimulation:
                 self._wire_cpu()
         else:
             raise ValueError(backend)
+        if world > 1:
+            # the backend holds the strip now: keep only it and one ghost column
+            # each side on the host (outputs are written per strip, stripio.cpp)
+            self.case.trim_to_columns(gi0 - 1, gi1 + 1)
 
     # -- GPU transports -------------------------------------------------------
     def _wire_gpu(self, transport: str):
@@ -161,12 +165,12 @@ class DistributedSimulation:
             dist.all_gather(out, arr)
             return b"".join(bytes(o.numpy().tobytes()) for o in out)
 
-        def fgather(gi0, gi1, strip):
-            out = [None] * world if rank == 0 else None
-            dist.gather_object((gi0, gi1, bytes(strip)), out, dst=0)
+        def fallgather(b):
+            out = [None] * world
+            dist.all_gather_object(out, bytes(b))
             return out
 
-        return fmin, fsum, fmaxi, fres, fgather
+        return fmin, fsum, fmaxi, fres, fallgather
 
     # -- gloo wiring for the CPU stepper ------------------------------------
     def _wire_cpu(self):

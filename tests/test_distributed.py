@@ -76,7 +76,7 @@ def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
         np.testing.assert_array_equal(got[f.replace(":", "_")], ref.field(f), err_msg=f)
 
 
-def _run_worker(rank, world, port, text, outdir):
+def _run_worker(rank, world, port, text, outdir, lean=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -85,31 +85,68 @@ def _run_worker(rank, world, port, text, outdir):
     try:
         from openhyperflow2d_amd.parallel.dist import DistributedSimulation
 
-        # generic stepper: it maintains the full record incl. the dS scratch
-        sim = DistributedSimulation(text, "cpu", rank=rank, world=world, lean=False)
+        sim = DistributedSimulation(text, "cpu", rank=rank, world=world, lean=lean)
         os.makedirs(outdir, exist_ok=True)
-        sim.run(max_cycles=2, outdir=outdir)
+        _, log = sim.run(max_cycles=2, outdir=outdir)
+        # host RSS scales with the strip: only the strip and its ghost columns stay
+        a, b = sim.case.resident_columns
+        gi0, gi1 = sim.parts[rank]
+        assert a == max(gi0 - 1, 0) and b == min(gi1 + 1, sim.case.nx), (a, b, gi0, gi1)
+        if rank == 0:
+            with open(os.path.join(outdir, "driver.log"), "w") as f:
+                f.write(log)
     finally:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def test_two_strip_driver_outputs_match_single_rank(hf, tmp_path):
-    """Full driver (2 outer cycles): rank 0 gathers the strips and writes the
-    field dump and checkpoint; they must equal the single-rank run's bytes."""
-    text = decks.wedge15(90, 30, nmax=12, nout=4)
+def _outputs_deck():
+    """Turbulent wedge with every per-cycle output of the driver: field dump,
+    Tecplot series, checkpoint, X cuts, nozzle Cd/Cv in the RMS file, body
+    Cx/Cy/Fx/Fy, HeatFlux-X/Y and monitor points."""
+    t = decks.wedge15(96, 30, navier_stokes=True, turbulence=4, nmax=12, nout=4)
+    kv = {"NSaveStep": 1, "isOutHeatFluxX": 1, "isOutHeatFluxY": 1, "Cp_Flow_Index": 1, "y_max": 20, "y_min": 0,
+          "is_Cx_calc": 1, "x_body": 0.05, "y_body": 0.0, "dx_body": 0.04, "dy_body": 0.012, "Cx_Flow_Index": 1,
+          "is_Cd_calc": 1, "x_nozzle": 0.061, "y_nozzle": 0.0, "dy_nozzle": 0.02, "Cd_Flow_Index": 1,
+          "p_ambient": 101325.0, "NumXCut": 2, "CutX-1.x0": 0.0305, "CutX-1.y0": 0.0, "CutX-1.dy": 0.025,
+          "CutX-2.x0": 0.08, "CutX-2.y0": 0.005, "CutX-2.dy": 0.02, "NumMonitorPoints": 2,
+          "Point-1.X": 0.045, "Point-1.Y": 0.01, "Point-2.X": 0.07, "Point-2.Y": 0.02}
+    for k, v in kv.items():
+        t = decks.set_key(t, k, v)
+    return t
+
+
+def _driver_lines(log):
+    return [ln for ln in log.splitlines() if ln.startswith(("Cut(", "Cx =", "Step No"))]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_strip_driver_outputs_match_single_rank(hf, tmp_path, world):
+    """Full driver (2 outer cycles), no gather: every rank writes its share of
+    the field dumps and checkpoint and the integrals are folded from per-strip
+    term lists -- the files must equal the single-rank run's bytes, and the
+    Cut / Cx lines of the log must be identical."""
+    text = _outputs_deck()
     one = tmp_path / "one"
-    two = tmp_path / "two"
+    many = tmp_path / "many"
     one.mkdir()
-    sim = hf.Simulation(text, "cpu")
-    sim.run(max_cycles=2, outdir=str(one))
-    mp.start_processes(_run_worker, args=(2, _free_port(), text, str(two)), nprocs=2, join=True,
+    sim = hf.Simulation(text, "cpu", lean=False)
+    _, log1 = sim.run(max_cycles=2, outdir=str(one))
+    mp.start_processes(_run_worker, args=(world, _free_port(), text, str(many)), nprocs=world, join=True,
                        start_method="spawn")
-    for name in ["Wedge15_90x30.plt", "Wedge15_90x30.hf2d", "tp-Wedge15_90x30.plt"]:
-        assert (one / name).read_bytes() == (two / name).read_bytes(), name
-    r1 = (one / "RMS-Wedge15_90x30.plt").read_text().split()
-    r2 = (two / "RMS-Wedge15_90x30.plt").read_text().split()
-    assert len(r1) == len(r2)
+    stem = "Wedge15_96x30"
+    names = [stem + ".plt", stem + ".hf2d", "tp-" + stem + ".plt", "HeatFlux-X-" + stem + ".plt",
+             "HeatFlux-Y-" + stem + ".plt", "Monitors-" + stem + ".plt"]
+    for name in names:
+        assert (one / name).read_bytes() == (many / name).read_bytes(), name
+    # RMS lines: the residual columns are reduced in a different order; Cd / Cv exact
+    r1 = [ln.split() for ln in (one / ("RMS-" + stem + ".plt")).read_text().splitlines()]
+    r2 = [ln.split() for ln in (many / ("RMS-" + stem + ".plt")).read_text().splitlines()]
+    assert len(r1) == len(r2) and [a[-2:] for a in r1] == [b[-2:] for b in r2]
+    got = _driver_lines((many / "driver.log").read_text())
+    want = _driver_lines(log1)
+    assert [ln for ln in got if not ln.startswith("Step")] == [ln for ln in want if not ln.startswith("Step")]
+    assert any(ln.startswith("Cut(2)") for ln in got) and any(ln.startswith("Cx =") for ln in got)
 
 
 def _fault_worker(rank, world, port, text, outdir):

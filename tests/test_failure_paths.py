@@ -70,10 +70,10 @@ def test_profile_json_phases(hf, tmp_path):
     assert n == 2
     prof = json.loads((tmp_path / "p.json").read_text())
     ph = prof["phases"]
-    assert ph["steps"]["calls"] == 40 and ph["sync"]["calls"] == 2 and ph["gather"]["calls"] == 2
+    assert ph["steps"]["calls"] == 40 and ph["sync"]["calls"] == 2 and ph["download"]["calls"] == 2
     assert ph["outputs.checkpoint"]["calls"] == 2
     assert prof["iterations"] == 40 and prof["grid"] == [80, 30] and prof["mcells_it_per_s"] > 0
-    assert set(sim.solver.phase_times) >= {"steps", "sync", "gather", "outputs"}
+    assert set(sim.solver.phase_times) >= {"steps", "sync", "download", "outputs"}
 
 
 def test_kill_fault_then_restart_resumes(hf, tmp_path):
