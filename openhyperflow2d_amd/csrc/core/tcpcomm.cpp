@@ -1,0 +1,330 @@
+#include "tcpcomm.hpp"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace hf2d {
+
+namespace {
+
+[[noreturn]] void fail(const std::string& what) {
+  throw std::runtime_error("TcpComm: " + what + " (" + std::strerror(errno) + ")");
+}
+
+void send_all(int fd, const void* p, size_t n) {
+  const char* c = (const char*)p;
+  while (n) {
+    const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) fail("send");
+    c += k;
+    n -= (size_t)k;
+  }
+}
+
+void recv_all(int fd, void* p, size_t n) {
+  char* c = (char*)p;
+  while (n) {
+    const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) fail(k == 0 ? "peer closed the connection" : "recv");
+    c += k;
+    n -= (size_t)k;
+  }
+}
+
+void send_blob(int fd, const std::string& s) {
+  const unsigned long long n = s.size();
+  send_all(fd, &n, sizeof n);
+  if (n) send_all(fd, s.data(), s.size());
+}
+
+std::string recv_blob(int fd) {
+  unsigned long long n = 0;
+  recv_all(fd, &n, sizeof n);
+  std::string s(n, '\0');
+  if (n) recv_all(fd, &s[0], n);
+  return s;
+}
+
+void tune(int fd) {
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+}
+
+int listen_on(const std::string& addr, int port, int backlog, int* bound_port) {
+  const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) fail("socket");
+  int one = 1;
+  ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  if (::inet_pton(AF_INET, addr.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (::bind(fd, (sockaddr*)&a, sizeof a) != 0) {
+    ::close(fd);
+    fail("bind " + addr + ":" + std::to_string(port));
+  }
+  if (::listen(fd, backlog) != 0) {
+    ::close(fd);
+    fail("listen");
+  }
+  if (bound_port) {
+    socklen_t l = sizeof a;
+    ::getsockname(fd, (sockaddr*)&a, &l);
+    *bound_port = ntohs(a.sin_port);
+  }
+  return fd;
+}
+
+int accept_one(int lfd, double timeout_s) {
+  pollfd p{lfd, POLLIN, 0};
+  const int rc = ::poll(&p, 1, (int)(timeout_s * 1000));
+  if (rc <= 0) fail("timed out waiting for a peer to connect");
+  const int fd = ::accept(lfd, nullptr, nullptr);
+  if (fd < 0) fail("accept");
+  tune(fd);
+  return fd;
+}
+
+int connect_retry(const std::string& addr, int port, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  if (::inet_pton(AF_INET, addr.c_str(), &a.sin_addr) != 1) {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    if (::getaddrinfo(addr.c_str(), nullptr, &hints, &res) != 0 || !res)
+      throw std::runtime_error("TcpComm: cannot resolve " + addr);
+    a.sin_addr = ((sockaddr_in*)res->ai_addr)->sin_addr;
+    ::freeaddrinfo(res);
+  }
+  for (;;) {
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) fail("socket");
+    if (::connect(fd, (sockaddr*)&a, sizeof a) == 0) {
+      tune(fd);
+      return fd;
+    }
+    ::close(fd);
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+      fail("cannot connect to " + addr + ":" + std::to_string(port));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+}
+
+}  // namespace
+
+TcpComm::TcpComm(int rank, int size, const std::string& addr, int port, double timeout_s) : r_(rank), n_(size) {
+  if (size < 1 || rank < 0 || rank >= size) throw std::runtime_error("TcpComm: bad rank/size");
+  if (size == 1) return;
+  // every rank >= 1 listens for its left neighbour on an ephemeral port
+  int nb_lfd = -1, nb_port = 0;
+  if (r_ > 0) nb_lfd = listen_on(addr, 0, 1, &nb_port);
+  std::vector<int> nb_ports(n_, 0);
+  if (r_ == 0) {
+    const int lfd = listen_on(addr, port, n_, nullptr);
+    ctrl_.assign(n_, -1);
+    for (int k = 1; k < n_; k++) {
+      const int fd = accept_one(lfd, timeout_s);
+      int hello[2];
+      recv_all(fd, hello, sizeof hello);
+      if (hello[0] <= 0 || hello[0] >= n_ || ctrl_[hello[0]] >= 0) {
+        ::close(lfd);
+        throw std::runtime_error("TcpComm: bad or duplicate rank " + std::to_string(hello[0]));
+      }
+      ctrl_[hello[0]] = fd;
+      nb_ports[hello[0]] = hello[1];
+    }
+    ::close(lfd);
+    for (int k = 1; k < n_; k++) send_all(ctrl_[k], nb_ports.data(), sizeof(int) * n_);
+  } else {
+    ctrl_.assign(1, connect_retry(addr, port, timeout_s));
+    const int hello[2] = {r_, nb_port};
+    send_all(ctrl_[0], hello, sizeof hello);
+    recv_all(ctrl_[0], nb_ports.data(), sizeof(int) * n_);
+  }
+  // neighbour chain: rank r connects to r+1's listener, r+1 accepts it
+  if (r_ + 1 < n_) {
+    right_ = connect_retry(addr, nb_ports[r_ + 1], timeout_s);
+    send_all(right_, &r_, sizeof r_);
+  }
+  if (r_ > 0) {
+    left_ = accept_one(nb_lfd, timeout_s);
+    int who = -1;
+    recv_all(left_, &who, sizeof who);
+    ::close(nb_lfd);
+    if (who != r_ - 1) throw std::runtime_error("TcpComm: unexpected left neighbour " + std::to_string(who));
+  }
+  barrier();
+}
+
+TcpComm::~TcpComm() {
+  for (int fd : ctrl_)
+    if (fd >= 0) ::close(fd);
+  if (left_ >= 0) ::close(left_);
+  if (right_ >= 0) ::close(right_);
+}
+
+std::vector<std::string> TcpComm::allgather_bytes(const std::string& mine) {
+  if (n_ == 1) return {mine};
+  std::vector<std::string> all(n_);
+  if (r_ == 0) {
+    all[0] = mine;
+    for (int k = 1; k < n_; k++) all[k] = recv_blob(ctrl_[k]);
+    std::string pack;
+    for (const auto& s : all) {
+      const unsigned long long n = s.size();
+      pack.append((const char*)&n, sizeof n);
+      pack += s;
+    }
+    for (int k = 1; k < n_; k++) send_blob(ctrl_[k], pack);
+  } else {
+    send_blob(ctrl_[0], mine);
+    const std::string pack = recv_blob(ctrl_[0]);
+    size_t o = 0;
+    for (int k = 0; k < n_; k++) {
+      unsigned long long n = 0;
+      if (o + sizeof n > pack.size()) throw std::runtime_error("TcpComm: short all-gather");
+      std::memcpy(&n, pack.data() + o, sizeof n);
+      o += sizeof n;
+      all[k] = pack.substr(o, n);
+      o += n;
+    }
+  }
+  return all;
+}
+
+std::string TcpComm::broadcast(const std::string& s, int root) {
+  const auto all = allgather_bytes(r_ == root ? s : std::string());
+  return all[root];
+}
+
+namespace {
+template <class T, class F>
+T fold(TcpComm& c, T v, F f) {
+  const auto all = c.allgather_bytes(std::string((const char*)&v, sizeof v));
+  T acc;
+  std::memcpy(&acc, all[0].data(), sizeof acc);
+  for (size_t k = 1; k < all.size(); k++) {
+    T x;
+    std::memcpy(&x, all[k].data(), sizeof x);
+    acc = f(acc, x);
+  }
+  return acc;
+}
+}  // namespace
+
+real TcpComm::allreduce_min(real v) {
+  return n_ == 1 ? v : fold<real>(*this, v, [](real a, real b) { return std::min(a, b); });
+}
+real TcpComm::allreduce_sum(real v) {
+  return n_ == 1 ? v : fold<real>(*this, v, [](real a, real b) { return a + b; });
+}
+int TcpComm::allreduce_max_int(int v) {
+  return n_ == 1 ? v : fold<int>(*this, v, [](int a, int b) { return std::max(a, b); });
+}
+void TcpComm::allreduce_residual(ResidualPack& p) {
+  if (n_ == 1) return;
+  p = fold<ResidualPack>(*this, p, [](ResidualPack a, const ResidualPack& b) {
+    residual_merge_lex(a, b);
+    return a;
+  });
+}
+
+void TcpComm::neighbor_exchange(const void* to_left, void* from_left, size_t nleft, const void* to_right,
+                                void* from_right, size_t nright) {
+  struct Xfer {
+    int fd;
+    char* p;
+    size_t left;
+    bool send;
+  };
+  Xfer x[4];
+  int nx = 0;
+  if (nleft && left_ >= 0) {
+    x[nx++] = {left_, (char*)to_left, nleft, true};
+    x[nx++] = {left_, (char*)from_left, nleft, false};
+  }
+  if (nright && right_ >= 0) {
+    x[nx++] = {right_, (char*)to_right, nright, true};
+    x[nx++] = {right_, (char*)from_right, nright, false};
+  }
+  for (;;) {
+    pollfd p[4];
+    int np = 0, map[4];
+    for (int k = 0; k < nx; k++)
+      if (x[k].left) {
+        p[np] = {x[k].fd, (short)(x[k].send ? POLLOUT : POLLIN), 0};
+        map[np++] = k;
+      }
+    if (!np) return;
+    if (::poll(p, np, 300000) <= 0) fail("halo exchange timed out");
+    for (int q = 0; q < np; q++) {
+      if (!p[q].revents) continue;
+      Xfer& t = x[map[q]];
+      const ssize_t k = t.send ? ::send(t.fd, t.p, t.left, MSG_NOSIGNAL | MSG_DONTWAIT)
+                               : ::recv(t.fd, t.p, t.left, MSG_DONTWAIT);
+      if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) continue;
+      if (k <= 0) fail("halo exchange");
+      t.p += k;
+      t.left -= (size_t)k;
+    }
+  }
+}
+
+RankEnv RankEnv::from_environ() {
+  RankEnv e;
+  auto geti = [](const char* k, int d) {
+    const char* v = std::getenv(k);
+    return v && *v ? std::atoi(v) : d;
+  };
+  e.rank = geti("RANK", 0);
+  e.world = geti("WORLD_SIZE", 1);
+  e.local_rank = geti("LOCAL_RANK", e.rank);
+  e.port = geti("MASTER_PORT", 29613);
+  if (const char* a = std::getenv("MASTER_ADDR")) e.addr = (*a && std::string(a) != "localhost") ? a : "127.0.0.1";
+  return e;
+}
+
+std::vector<std::pair<int, int>> balanced_columns(const Field& J, int nparts) {
+  const int nx = J.nx;
+  if (nparts <= 1) return {{0, nx}};
+  if (nparts > nx) throw std::runtime_error("more strips than columns");
+  std::vector<double> cum(nx + 1, 0.0);
+  for (int i = 0; i < nx; i++) {
+    double a = 0;
+    for (int j = 0; j < J.ny; j++) a += J.at(i, j).is(CT_SOLID) ? 0.0 : 1.0;
+    cum[i + 1] = cum[i] + a;
+  }
+  const double total = cum[nx];
+  std::vector<int> cuts{0};
+  for (int k = 1; k < nparts; k++) {
+    const double target = total * k / nparts;
+    int c = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+    c = std::max(c, cuts.back() + 1);
+    c = std::min(c, nx - (nparts - k));
+    cuts.push_back(c);
+  }
+  cuts.push_back(nx);
+  std::vector<std::pair<int, int>> out;
+  for (int k = 0; k < nparts; k++) out.push_back({cuts[k], cuts[k + 1]});
+  return out;
+}
+
+}  // namespace hf2d

@@ -26,6 +26,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -2561,6 +2562,56 @@ std::string DeviceSolver::autotune(int steps) {
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device) {
   return std::unique_ptr<SolverBase>(new DeviceSolver(cs, device < 0 ? 0 : device));
+}
+
+// Strip rank of the native multi-process CLI (hf2d_main.cpp).  `boot` is the
+// host communicator that bootstraps the device transports: the RCCL unique
+// id travels through it, then (transport "p2p") every rank exports its xGMI
+// mailbox descriptor, the descriptors are all-gathered and imported, and the
+// ranks agree on the result -- if any rank cannot map its peers, every rank
+// keeps RCCL (grouped send/recv on the solver stream).  `used` reports it.
+std::unique_ptr<SolverBase> make_gpu_strip_solver(Case& cs, int device, int gi0, int gi1, Comm& boot,
+                                                  const std::string& transport, std::string& used) {
+  std::unique_ptr<DeviceSolver> s(new DeviceSolver(cs, device < 0 ? 0 : device, gi0, gi1));
+  used = "none";
+  if (cs.cfg.ThreadBlockSize == 0) {
+    const char* at = std::getenv("HF2D_AUTOTUNE");
+    if (!at || std::string(at) != "0") s->autotune();
+  }
+  if (boot.size() == 1) return std::unique_ptr<SolverBase>(s.release());
+  const int r = boot.rank(), n = boot.size();
+  const std::string uid = boot.allgather_bytes(r == 0 ? DeviceSolver::nccl_unique_id() : std::string())[0];
+  s->init_comm(uid, r, n);
+  used = "rccl";
+  if (transport == "p2p") {
+    std::string desc, why;
+    int bad = 0;
+    try {
+      desc = s->p2p_export(r, n);
+    } catch (const std::exception& e) {
+      bad = 1;
+      why = e.what();
+    }
+    const std::vector<std::string> descs = boot.allgather_bytes(bad ? std::string() : desc);
+    for (const std::string& d : descs) bad |= d.empty() ? 1 : 0;
+    if (!bad) {
+      try {
+        s->p2p_import(descs);
+      } catch (const std::exception& e) {
+        bad = 1;
+        why = e.what();
+      }
+    }
+    if (boot.allreduce_max_int(bad) == 0) {
+      used = "p2p";
+      const char* f = std::getenv("HF2D_P2P_FUSE");
+      s->p2p_fuse = !(f && std::string(f) == "0");
+    } else {
+      s->p2p_set(false);
+      if (!why.empty()) std::fprintf(stderr, "[hf2d rank %d] p2p transport unavailable (%s); using RCCL\n", r, why.c_str());
+    }
+  }
+  return std::unique_ptr<SolverBase>(s.release());
 }
 
 }  // namespace hf2d

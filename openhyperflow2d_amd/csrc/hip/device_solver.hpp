@@ -158,5 +158,7 @@ class DeviceSolver : public SolverBase {
 };
 
 std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device);
+std::unique_ptr<SolverBase> make_gpu_strip_solver(Case& cs, int device, int gi0, int gi1, Comm& boot,
+                                                  const std::string& transport, std::string& used);
 
 }  // namespace hf2d

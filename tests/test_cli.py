@@ -6,6 +6,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from tests.conftest import ROOT
 
 
@@ -49,17 +51,34 @@ def test_sigint_finishes_cycle_and_checkpoints(hf, tmp_path):
     assert meta["iteration"] > 0
 
 
-def test_launcher_script_one_and_two_ranks(hf, tmp_path):
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_native_ranks_match_one_rank(hf, tmp_path, n):
     """bin/OpenHyperFLOW2D.sh <Project> [n]: the reference's launcher contract
-    (Project -> Project.dat, outputs next to the deck), n ranks via torchrun."""
+    (Project -> Project.dat in the working directory) running n processes of
+    the native binary (TCP rendezvous from RANK/WORLD_SIZE/MASTER_*, no
+    Python): the outputs of n strip ranks equal one rank's byte for byte."""
     from openhyperflow2d_amd.models import decks
 
-    (tmp_path / "W.dat").write_text(decks.wedge15(60, 20, nmax=10, nout=5))
+    text = decks.wedge15(90, 30, navier_stokes=True, turbulence=4, nmax=8, nout=4)
+    for k, v in {"NSaveStep": 1, "is_Cx_calc": 1, "x_body": 0.03, "y_body": 0.0, "dx_body": 0.03,
+                 "dy_body": 0.01, "Cx_Flow_Index": 1, "NumXCut": 1, "CutX-1.x0": 0.0405, "CutX-1.y0": 0.0,
+                 "CutX-1.dy": 0.02}.items():
+        text = decks.set_key(text, k, v)
     sh = os.path.join(ROOT, "openhyperflow2d_amd", "bin", "OpenHyperFLOW2D.sh")
-    for n in ("1", "2"):
-        r = subprocess.run([sh, "W", n, "--backend", "cpu", "--cycles", "1", "--no-checkpoint"], cwd=tmp_path,
+    logs = {}
+    for k in (1, n):
+        d = tmp_path / ("r%d" % k)
+        d.mkdir()
+        (d / "W.dat").write_text(text)
+        r = subprocess.run([sh, "W", str(k), "--backend", "cpu", "--cycles", "2", "--no-checkpoint"], cwd=d,
                            capture_output=True, text=True, timeout=600,
-                           env=dict(os.environ, HF2D_MASTER_PORT=str(29700 + int(n))))
+                           env=dict(os.environ, HF2D_MASTER_PORT=str(29700 + 10 * n + k),
+                                    HF2D_BIN=os.path.join(ROOT, "openhyperflow2d_amd", "bin", "hf2d_cpu")))
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-        assert "Computation finished" in r.stdout
-    assert (tmp_path / "Wedge15_60x20.plt").exists()
+        assert r.stdout.count("Computation finished") == 1
+        logs[k] = r.stdout
+    assert "halo transport tcp" in logs[n]
+    for name in ["Wedge15_90x30.plt", "tp-Wedge15_90x30.plt", "Wedge15_90x30.hf2d"]:
+        assert (tmp_path / "r1" / name).read_bytes() == (tmp_path / ("r%d" % n) / name).read_bytes(), name
+    cut = [ln for ln in logs[1].splitlines() if ln.startswith(("Cut(", "Cx ="))]
+    assert cut and cut == [ln for ln in logs[n].splitlines() if ln.startswith(("Cut(", "Cx ="))]

@@ -184,7 +184,7 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
 
 
 @pytest.mark.parametrize("nranks,physics,lean", [(2, "euler", True), (3, "euler", True), (2, "euler", False),
-                                                 (3, "kes", False)])
+                                                 (3, "kes", False), (8, "euler", True), (8, "kes", False)])
 def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
     ns = physics != "euler"
     text = decks.wedge15(240, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)

@@ -1,0 +1,76 @@
+"""Strip-decomposed DEEPS driver on the GPU without a gather: N DeviceSolvers
+(in-process virtual ranks, one host thread each, LocalGroup transport) run the
+full driver into ONE output directory -- each writes its share of the field
+dumps and checkpoint, the Cut / Cx / heat-flux integrals are folded from
+per-strip term lists and y+ from the merged wall friction velocities.  The
+files must equal the single-GPU run's bytes."""
+import threading
+
+import numpy as np
+import pytest
+
+from openhyperflow2d_amd.models import decks
+
+pytestmark = pytest.mark.gpu
+
+
+def _outputs_deck():
+    t = decks.wedge15(160, 40, navier_stokes=True, turbulence=4, nmax=12, nout=4)
+    kv = {"NSaveStep": 1, "isOutHeatFluxX": 1, "isOutHeatFluxY": 1, "Cp_Flow_Index": 1, "y_max": 30, "y_min": 0,
+          "is_Cx_calc": 1, "x_body": 0.05, "y_body": 0.0, "dx_body": 0.06, "dy_body": 0.015, "Cx_Flow_Index": 1,
+          "NumXCut": 2, "CutX-1.x0": 0.0305, "CutX-1.y0": 0.0, "CutX-1.dy": 0.03, "CutX-2.x0": 0.12,
+          "CutX-2.y0": 0.005, "CutX-2.dy": 0.03}
+    for k, v in kv.items():
+        t = decks.set_key(t, k, v)
+    return t
+
+
+def _cut_lines(log):
+    return [ln for ln in log.splitlines() if ln.startswith(("Cut(", "Cx ="))]
+
+
+@pytest.mark.parametrize("nranks", [4, 8])
+def test_virtual_rank_driver_outputs_match_single_gpu(gpu, tmp_path, nranks):
+    from openhyperflow2d_amd.parallel.strips import balanced_columns
+
+    nat = gpu.native()
+    text = _outputs_deck()
+    one, many = tmp_path / "one", tmp_path / "many"
+    one.mkdir()
+    many.mkdir()
+    ref = gpu.Simulation(text, "gpu", lean=False)
+    _, log1 = ref.run(max_cycles=2, outdir=str(one))
+
+    cases = [nat.Case.from_deck(text, ".", False) for _ in range(nranks)]
+    parts = balanced_columns(np.asarray(cases[0].field("solid")), nranks)
+    group = nat.LocalGroup(nranks)
+    solvers = []
+    for r, (a, b) in enumerate(parts):
+        s = nat.DeviceSolver(cases[r], 0, a, b)
+        s.lean = False
+        s.init_local(group, r)
+        cases[r].trim_to_columns(a - 1, b + 1)
+        solvers.append(s)
+    logs, errors = {}, []
+
+    def run(r):
+        try:
+            logs[r] = solvers[r].run(2, str(many))[1]
+        except Exception as e:   # pragma: no cover - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    assert not errors, errors
+    assert not any(t.is_alive() for t in th), "virtual-rank driver hung"
+    stem = "Wedge15_160x40"
+    for name in [stem + ".plt", "tp-" + stem + ".plt", stem + ".hf2d", "HeatFlux-X-" + stem + ".plt",
+                 "HeatFlux-Y-" + stem + ".plt"]:
+        assert (one / name).read_bytes() == (many / name).read_bytes(), name
+    assert _cut_lines(logs[0]) == _cut_lines(log1) and len(_cut_lines(log1)) >= 3
+    # each host keeps only its strip and one ghost column each side
+    for r, (a, b) in enumerate(parts):
+        assert tuple(cases[r].resident_columns) == (max(a - 1, 0), min(b + 1, cases[r].nx))
