@@ -562,6 +562,26 @@ PYBIND11_MODULE(_hf2d, m) {
              for (const auto& b : d) v.push_back(std::string(b));
              s.p2p_import(v);
            })
+      .def("p2p_probe",
+           [](DeviceSolver& s) {
+             std::string b;
+             {
+               py::gil_scoped_release rel;   // waits for the peers' exchange
+               b = s.p2p_probe();
+             }
+             return py::bytes(b);
+           },
+           "p2p self-validation blob (collective; see p2p_probe_ok)")
+      .def_static("p2p_probe_ok",
+                  [](const std::vector<py::bytes>& d, int rank) {
+                    std::vector<std::string> v;
+                    for (const auto& b : d) v.push_back(std::string(b));
+                    std::string why;
+                    const bool ok = DeviceSolver::p2p_probe_ok(v, rank, &why);
+                    return py::make_tuple(ok, why);
+                  },
+                  py::arg("blobs"), py::arg("rank"))
+      .def("p2p_fallback", &DeviceSolver::p2p_fallback, py::call_guard<py::gil_scoped_release>())
       .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
       .def("comm_rank", &DeviceSolver::comm_rank)

@@ -41,7 +41,8 @@ void recv_all(int fd, void* p, size_t n) {
   while (n) {
     const ssize_t k = ::recv(fd, c, n, 0);
     if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) fail(k == 0 ? "peer closed the connection" : "recv");
+    if (k == 0) throw std::runtime_error("TcpComm: peer closed the connection (a rank exited)");
+    if (k < 0) fail("recv");
     c += k;
     n -= (size_t)k;
   }

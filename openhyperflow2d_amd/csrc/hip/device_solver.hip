@@ -287,6 +287,13 @@ struct ColList {
 constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
 constexpr int P2P_THREADS = 512;
 
+// Acquire load of a peer's publication flag at system scope: the poll loops
+// spin with relaxed loads (cheap) and finish with this one, so every later
+// load (mailbox data, peer dt) is ordered after the observed flag.
+__device__ inline unsigned long long p2p_acquire(const unsigned long long* f) {
+  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ inline double p2p_load(const double* p) {
   return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_SYSTEM));
@@ -509,6 +516,10 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
               break;
             }
           }
+          // acquire the peer's publication: its dt and mailbox stores
+          // (released by its vmcnt drain before the flag) are visible to
+          // every load ordered after this one, here and in later kernels
+          if (ok) (void)p2p_acquire(&X.my_flags[q]);
           if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
         }
         __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -972,6 +983,7 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
         break;
       }
     }
+    if (ok) (void)p2p_acquire(&a.my_flags[q]);   // order the mailbox reads after the flag
     if (ok) dmin = fmin(dmin, p2p_load(a.my_dtr + par * a.nranks + q));
   }
   s_dt[threadIdx.x] = dmin;
@@ -1842,51 +1854,60 @@ int DeviceSolver::comm_size() const { return impl->nranks; }
 // same RCCL group also sends this rank's dt of that slot to every other rank
 // and unpack folds the MIN in -- one grouped p2p launch per step instead of a
 // send/recv group plus an all-reduce.
-void DeviceSolver::exchange(int group, int dt_slot) {
-  Impl& m = *impl;
-  p2p_complete();
-  if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
-  const int ny = h.ny;
+// device columns of the fields a halo group carries (pack order)
+void DeviceSolver::halo_fields(int group, std::vector<real*>& f) const {
+  const Impl& m = *impl;
   const long N = h.N;
-  ColList L;
-  L.nf = 0;
+  f.clear();
   auto add_eq = [&](real* base) {
-    for (int k = 0; k < NEQ; k++) L.f[L.nf++] = base + (long)k * N;
+    for (int k = 0; k < NEQ; k++) f.push_back(base + (long)k * N);
   };
   if (group == CpuSolver::HALO_LEAN) {
     // single gas: the species (and their pre-chemistry copies) are +0 on
     // every rank; dS/dx only travels if some node applies d2/dx2 = 0
     const bool sg = lean_sg && lean_sg_ok;
-    for (int k = 0; k < (sg ? 4 : 4 + NCOMP); k++) L.f[L.nf++] = m.S[sbuf] + (long)k * N;
+    for (int k = 0; k < (sg ? 4 : 4 + NCOMP); k++) f.push_back(m.S[sbuf] + (long)k * N);
     if (!sg)
-      for (int k = 0; k < NCOMP; k++) L.f[L.nf++] = m.Spre[pbuf] + (long)k * N;
-    L.f[L.nf++] = m.U[pbuf];
-    L.f[L.nf++] = m.V[pbuf];
-    L.f[L.nf++] = m.P2[pbuf];
+      for (int k = 0; k < NCOMP; k++) f.push_back(m.Spre[pbuf] + (long)k * N);
+    f.push_back(m.U[pbuf]);
+    f.push_back(m.V[pbuf]);
+    f.push_back(m.P2[pbuf]);
     if (lean_has_cauchy_x) add_eq(m.dSdx[dsbuf]);
   } else if (group == CpuSolver::HALO_MID) {
     add_eq(m.S[1 - sbuf]);
-    for (int q = 0; q < m.nsp; q++) L.f[L.nf++] = m.Ys[1 - sbuf] + (long)q * N;
+    for (int q = 0; q < m.nsp; q++) f.push_back(m.Ys[1 - sbuf] + (long)q * N);
   } else if (group == CpuSolver::HALO_QDIR) {
-    for (int d = 0; d < 4; d++) L.f[L.nf++] = m.qdir + (long)d * N;
+    for (int d = 0; d < 4; d++) f.push_back(m.qdir + (long)d * N);
   } else {
     add_eq(m.S[sbuf]);
     add_eq(m.A[abuf]);
     add_eq(m.B[abuf]);
     add_eq(m.dSdx[dsbuf]);
-    L.f[L.nf++] = m.U[pbuf];
-    L.f[L.nf++] = m.V[pbuf];
-    L.f[L.nf++] = m.Tg[pbuf];
-    L.f[L.nf++] = m.lam;
-    L.f[L.nf++] = m.lam_t;
+    f.push_back(m.U[pbuf]);
+    f.push_back(m.V[pbuf]);
+    f.push_back(m.Tg[pbuf]);
+    f.push_back(m.lam);
+    f.push_back(m.lam_t);
     for (int q = 0; q < m.nsp; q++) {
-      L.f[L.nf++] = m.Ys[sbuf] + (long)q * N;
-      L.f[L.nf++] = m.As + (long)q * N;
-      L.f[L.nf++] = m.Bs + (long)q * N;
-      if (m.dSdxs[0]) L.f[L.nf++] = m.dSdxs[dsbuf] + (long)q * N;
+      f.push_back(m.Ys[sbuf] + (long)q * N);
+      f.push_back(m.As + (long)q * N);
+      f.push_back(m.Bs + (long)q * N);
+      if (m.dSdxs[0]) f.push_back(m.dSdxs[dsbuf] + (long)q * N);
     }
   }
-  if (L.nf > MAX_HALO_FIELDS) throw std::runtime_error("halo: too many exchanged fields");
+}
+
+void DeviceSolver::exchange(int group, int dt_slot) {
+  Impl& m = *impl;
+  p2p_complete();
+  if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
+  const int ny = h.ny;
+  std::vector<real*> fl;
+  halo_fields(group, fl);
+  if (fl.size() > (size_t)MAX_HALO_FIELDS) throw std::runtime_error("halo: too many exchanged fields");
+  ColList L;
+  L.nf = (int)fl.size();
+  for (int k = 0; k < L.nf; k++) L.f[k] = fl[k];
   const int cnt = L.nf * ny;
   const unsigned nb2 = (unsigned)((2 * cnt + BLOCK - 1) / BLOCK);
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
@@ -1967,6 +1988,113 @@ void DeviceSolver::exchange(int group, int dt_slot) {
                      m.halo_recv[0], m.halo_recv[1], sides, m.sc, gather_dt ? dt_slot : 0, m.dt_recv,
                      gather_dt ? m.nranks : 0, m.rank);
   HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+struct P2PProbe {
+  int32_t rank, sides, err, pad;
+  uint64_t sent_l, sent_r, recv_l, recv_r;
+  double dt;
+};
+uint64_t fnv1a(const std::vector<real>& v) {
+  uint64_t h = 1469598103934665603ULL;
+  const unsigned char* p = (const unsigned char*)v.data();
+  for (size_t k = 0; k < v.size() * sizeof(real); k++) h = (h ^ p[k]) * 1099511628211ULL;
+  return h;
+}
+constexpr double PROBE_DT0 = 1.0, PROBE_DT_STEP = 0.25;   // rank r offers 1 + r/4: the MIN is 1
+}  // namespace
+
+std::string DeviceSolver::p2p_probe() {
+  flush_pending();
+  p2p_complete();
+  HIP_CHECK(hipSetDevice(dev));
+  Impl& m = *impl;
+  if (!m.p2p.on) throw std::runtime_error("p2p_probe: p2p transport not active");
+  hipStream_t st = m.stream;
+  const int ny = h.ny;
+  const int first = l_off, last = l_off + (gi1 - gi0) - 1, gl = 0, gr = h.nx - 1;
+  const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
+  std::vector<real*> fl;
+  halo_fields(CpuSolver::HALO_STATE, fl);
+  DevScalars saved;
+  HIP_CHECK(hipMemcpyAsync(&saved, m.sc, sizeof saved, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  // poison the ghost columns (all-ones bytes: NaN) so a lost delivery shows
+  for (real* f : fl) {
+    if (has_left) HIP_CHECK(hipMemsetAsync(f + (long)gl * ny, 0xFF, ny * sizeof(real), st));
+    if (has_right) HIP_CHECK(hipMemsetAsync(f + (long)gr * ny, 0xFF, ny * sizeof(real), st));
+  }
+  const unsigned long long tag = [&] {
+    const double d = PROBE_DT0 + PROBE_DT_STEP * m.rank;
+    unsigned long long b;
+    std::memcpy(&b, &d, sizeof b);
+    return b;
+  }();
+  HIP_CHECK(hipMemcpyAsync(&m.sc->dt_bits[0], &tag, sizeof tag, hipMemcpyHostToDevice, st));
+  exchange(CpuSolver::HALO_STATE, 0);
+  auto column = [&](int col) {
+    std::vector<real> v(fl.size() * (size_t)ny);
+    for (size_t k = 0; k < fl.size(); k++)
+      HIP_CHECK(hipMemcpyAsync(v.data() + k * ny, fl[k] + (long)col * ny, ny * sizeof(real), hipMemcpyDeviceToHost, st));
+    return v;
+  };
+  std::vector<real> sl, sr, rl, rr;
+  if (has_left) {
+    sl = column(first);
+    rl = column(gl);
+  }
+  if (has_right) {
+    sr = column(last);
+    rr = column(gr);
+  }
+  DevScalars after;
+  HIP_CHECK(hipMemcpyAsync(&after, m.sc, sizeof after, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  HIP_CHECK(hipMemcpyAsync(m.sc, &saved, sizeof saved, hipMemcpyHostToDevice, st));   // dt slots, error flag
+  HIP_CHECK(hipStreamSynchronize(st));
+  P2PProbe b{};
+  b.rank = m.rank;
+  b.sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
+  b.err = after.neg_T & 2;
+  b.sent_l = has_left ? fnv1a(sl) : 0;
+  b.sent_r = has_right ? fnv1a(sr) : 0;
+  b.recv_l = has_left ? fnv1a(rl) : 0;
+  b.recv_r = has_right ? fnv1a(rr) : 0;
+  std::memcpy(&b.dt, &after.dt_bits[0], sizeof b.dt);
+  return std::string((const char*)&b, sizeof b);
+}
+
+bool DeviceSolver::p2p_probe_ok(const std::vector<std::string>& blobs, int rank, std::string* why) {
+  auto bad = [&](const std::string& w) {
+    if (why) *why = w;
+    return false;
+  };
+  std::vector<P2PProbe> p(blobs.size());
+  for (size_t q = 0; q < blobs.size(); q++) {
+    if (blobs[q].size() != sizeof(P2PProbe)) return bad("probe blob of rank " + std::to_string(q) + " missing");
+    std::memcpy(&p[q], blobs[q].data(), sizeof(P2PProbe));
+  }
+  const int n = (int)p.size();
+  (void)rank;
+  for (int q = 0; q < n; q++) {   // every rank judges all ranks: the verdict is identical everywhere
+    if (p[q].rank != q) return bad("probe rank mismatch");
+    if (p[q].err) return bad("rank " + std::to_string(q) + " timed out waiting for its peers");
+    if (p[q].dt != PROBE_DT0) return bad("rank " + std::to_string(q) + " folded dt " + std::to_string(p[q].dt));
+    if ((p[q].sides & 1) && (q == 0 || p[q].recv_l != p[q - 1].sent_r))
+      return bad("left halo of rank " + std::to_string(q) + " differs from what rank " + std::to_string(q - 1) + " sent");
+    if ((p[q].sides & 2) && (q == n - 1 || p[q].recv_r != p[q + 1].sent_l))
+      return bad("right halo of rank " + std::to_string(q) + " differs from what rank " + std::to_string(q + 1) + " sent");
+  }
+  return true;
+}
+
+// p2p failed validation: RCCL (or the in-process group) carries the halos
+// from now on; refill the ghost columns the probe poisoned
+void DeviceSolver::p2p_fallback() {
+  p2p_set(false);
+  exchange(CpuSolver::HALO_STATE, -1);
+  HIP_CHECK(hipStreamSynchronize(impl->stream));
 }
 
 FusedX DeviceSolver::fused_args() const {
@@ -2565,13 +2693,19 @@ std::unique_ptr<SolverBase> make_gpu_solver(Case& cs, int device) {
 }
 
 // Strip rank of the native multi-process CLI (hf2d_main.cpp).  `boot` is the
-// host communicator that bootstraps the device transports: the RCCL unique
-// id travels through it, then (transport "p2p") every rank exports its xGMI
-// mailbox descriptor, the descriptors are all-gathered and imported, and the
-// ranks agree on the result -- if any rank cannot map its peers, every rank
-// keeps RCCL (grouped send/recv on the solver stream).  `used` reports it.
+// host communicator (TCP): it carries the driver's host reductions and the
+// p2p bootstrap -- every rank exports its xGMI mailbox descriptor, the
+// descriptors are all-gathered and imported, one poisoned full-state exchange
+// is checksummed on every rank (p2p_probe), and the ranks agree on the
+// result.  If any rank fails (or transport "rccl" is asked for), the RCCL
+// unique id travels through `boot` and every rank uses grouped RCCL
+// send/recv on the solver stream instead.  `used` reports the transport.
 std::unique_ptr<SolverBase> make_gpu_strip_solver(Case& cs, int device, int gi0, int gi1, Comm& boot,
                                                   const std::string& transport, std::string& used) {
+  int ndev = 0;
+  HIP_CHECK(hipGetDeviceCount(&ndev));
+  // more local ranks than GPUs (tests on a one-GPU box): ranks share devices
+  if (device >= ndev && ndev > 0) device %= ndev;
   std::unique_ptr<DeviceSolver> s(new DeviceSolver(cs, device < 0 ? 0 : device, gi0, gi1));
   used = "none";
   if (cs.cfg.ThreadBlockSize == 0) {
@@ -2580,36 +2714,51 @@ std::unique_ptr<SolverBase> make_gpu_strip_solver(Case& cs, int device, int gi0,
   }
   if (boot.size() == 1) return std::unique_ptr<SolverBase>(s.release());
   const int r = boot.rank(), n = boot.size();
-  const std::string uid = boot.allgather_bytes(r == 0 ? DeviceSolver::nccl_unique_id() : std::string())[0];
-  s->init_comm(uid, r, n);
-  used = "rccl";
-  if (transport == "p2p") {
-    std::string desc, why;
-    int bad = 0;
+  auto use_rccl = [&] {
+    const std::string uid = boot.allgather_bytes(r == 0 ? DeviceSolver::nccl_unique_id() : std::string())[0];
+    s->init_comm(uid, r, n);
+    used = "rccl";
+  };
+  if (transport != "p2p") {
+    use_rccl();
+    return std::unique_ptr<SolverBase>(s.release());
+  }
+  // host-side reductions of the driver (output steps) over the bootstrap
+  // communicator; the halos and the per-step dt MIN go through the mailboxes
+  s->comm = &boot;
+  std::string desc, why;
+  int bad = 0;
+  try {
+    desc = s->p2p_export(r, n);
+  } catch (const std::exception& e) {
+    bad = 1;
+    why = e.what();
+  }
+  const std::vector<std::string> descs = boot.allgather_bytes(bad ? std::string() : desc);
+  for (const std::string& d : descs) bad |= d.empty() ? 1 : 0;
+  if (!bad) {
     try {
-      desc = s->p2p_export(r, n);
+      s->p2p_import(descs);
     } catch (const std::exception& e) {
       bad = 1;
       why = e.what();
     }
-    const std::vector<std::string> descs = boot.allgather_bytes(bad ? std::string() : desc);
-    for (const std::string& d : descs) bad |= d.empty() ? 1 : 0;
-    if (!bad) {
-      try {
-        s->p2p_import(descs);
-      } catch (const std::exception& e) {
-        bad = 1;
-        why = e.what();
-      }
-    }
-    if (boot.allreduce_max_int(bad) == 0) {
-      used = "p2p";
-      const char* f = std::getenv("HF2D_P2P_FUSE");
-      s->p2p_fuse = !(f && std::string(f) == "0");
-    } else {
-      s->p2p_set(false);
-      if (!why.empty()) std::fprintf(stderr, "[hf2d rank %d] p2p transport unavailable (%s); using RCCL\n", r, why.c_str());
-    }
+  }
+  if (boot.allreduce_max_int(bad) == 0) {
+    // self-validation: one poisoned full-state exchange, checksummed
+    const std::vector<std::string> probes = boot.allgather_bytes(s->p2p_probe());
+    if (!DeviceSolver::p2p_probe_ok(probes, r, &why)) bad = 1;
+  } else {
+    bad = 1;
+  }
+  if (boot.allreduce_max_int(bad) == 0) {
+    used = "p2p";
+    const char* f = std::getenv("HF2D_P2P_FUSE");
+    s->p2p_fuse = !(f && std::string(f) == "0");
+  } else {
+    use_rccl();
+    s->p2p_fallback();
+    if (!why.empty()) std::fprintf(stderr, "[hf2d rank %d] p2p transport unavailable (%s); using RCCL\n", r, why.c_str());
   }
   return std::unique_ptr<SolverBase>(s.release());
 }

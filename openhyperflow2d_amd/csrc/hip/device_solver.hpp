@@ -101,6 +101,16 @@ class DeviceSolver : public SolverBase {
   int comm_rank() const;
   int comm_size() const;
   void exchange(int group, int dt_slot = -1);
+  // device columns of the fields a halo group carries, in pack order
+  void halo_fields(int group, std::vector<real*>& f) const;
+  // p2p self-validation (collective over the strip ranks, before the first
+  // step): poisons the ghost columns, runs one mailbox exchange of the full
+  // state group with a rank-tagged dt, restores the device scalars and
+  // returns this rank's checksums of the columns it sent and received and of
+  // the folded dt.  p2p_probe_ok checks the all-gathered blobs of every rank.
+  std::string p2p_probe();
+  static bool p2p_probe_ok(const std::vector<std::string>& blobs, int rank, std::string* why);
+  void p2p_fallback();   // p2p off, ghost columns refilled over RCCL / the local group
 
   HostArrays h;           // host staging copy
   int dev = 0;

@@ -54,6 +54,8 @@ class DistributedSimulation:
         gi0, gi1 = self.parts[rank]
         self.backend = backend
         self.transport = "none"
+        self.p2p_validated = False
+        self.p2p_error = ""
         if backend == "gpu":
             self.solver = hf.DeviceSolver(self.case, device, gi0, gi1)
             self.solver.fused = fused
@@ -117,12 +119,17 @@ class DistributedSimulation:
                 ok, err = 0, str(e)
         else:
             ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32)
-        if nccl:
-            flag = flag.cuda()
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 1:
+        if self._all_ok(ok, nccl):
+            # self-validation: one exchange of the full state with poisoned
+            # ghost columns and a rank-tagged dt, checksummed on every rank
+            blobs = [None] * world
+            dist.all_gather_object(blobs, s.p2p_probe())
+            ok, why = self.hf.DeviceSolver.p2p_probe_ok(blobs, rank)
+            if not ok:
+                err = "self-validation failed: " + why
+        if self._all_ok(ok, nccl):
             self.transport = "p2p"
+            self.p2p_validated = True
             # the exchange is folded into the lean tile kernel (one kernel per
             # step, the last workgroup publishes and waits); HF2D_P2P_FUSE=0
             # selects tile kernel + hf2d_p2p_xchg.  One-GPU proxy
@@ -130,13 +137,25 @@ class DistributedSimulation:
             # strip (profiles/p2p_fused_virtual2_kernels.md)
             s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "1") == "1"
         else:
-            s.p2p_active = False
             if not nccl:
                 obj = [self.hf.DeviceSolver.nccl_unique_id() if rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
                 s.init_comm(obj[0], rank, world)
+            s.p2p_fallback()
+            self.p2p_error = err
             if err:
                 print("[hf2d rank %d] p2p transport unavailable (%s); using RCCL" % (rank, err), flush=True)
+
+    @staticmethod
+    def _all_ok(ok: int, nccl: bool) -> bool:
+        import torch
+        import torch.distributed as dist
+
+        flag = torch.tensor([int(bool(ok))], dtype=torch.int32)
+        if nccl:
+            flag = flag.cuda()
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return int(flag.item()) == 1
 
     def _py_comm_funcs(self):
         import torch

@@ -58,15 +58,13 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("case", list(CASES))
-@pytest.mark.parametrize("lean", [False, True])
-def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
+def _strips_vs_single(hf, case, lean, tmp_path, world):
     mk, steps = CASES[case]
     text = mk()
     ref = hf.Simulation(text, "cpu", lean=lean)
     for s in range(3):
         ref.step(steps, residual=(s != 1))
-    mp.start_processes(_worker, args=(2, _free_port(), text, steps, lean, str(tmp_path)), nprocs=2,
+    mp.start_processes(_worker, args=(world, _free_port(), text, steps, lean, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(tmp_path / "res.npz")
     summ = ref.summary()
@@ -74,6 +72,19 @@ def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
     np.testing.assert_allclose(got["rms"], summ["rms"], rtol=1e-12, atol=0)
     for f in _fields(text):
         np.testing.assert_array_equal(got[f.replace(":", "_")], ref.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("case", list(CASES))
+@pytest.mark.parametrize("lean", [False, True])
+def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
+    _strips_vs_single(hf, case, lean, tmp_path, 2)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("case", ["wedge15_euler", "wedge15_ns_keps", "scramjet_mech"])
+def test_many_strips_match_single_rank(hf, case, world, tmp_path):
+    """4 and 8 gloo ranks (strips of 11..30 columns): bit-identical to one rank."""
+    _strips_vs_single(hf, case, case == "wedge15_euler", tmp_path, world)
 
 
 def _run_worker(rank, world, port, text, outdir, lean=False):

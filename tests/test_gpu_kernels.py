@@ -124,7 +124,7 @@ def test_lean_bitwise_with_switches(gpu):
     np.testing.assert_array_equal(rg, rc)
 
 
-def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False):
+def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False, corrupt=False):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
     host thread each, halos through the in-process LocalGroup transport (or,
     p2p=True, the device-side mailbox transport: one exchange kernel per step,
@@ -149,6 +149,35 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
             s.p2p_import(descs)
             s.p2p_fuse = fuse
             assert s.p2p_active
+        # start-up self-validation (collective: one thread per rank)
+        blobs = [None] * nranks
+
+        def probe(r):
+            blobs[r] = solvers[r].p2p_probe()
+
+        th = [threading.Thread(target=probe, args=(r,), daemon=True) for r in range(nranks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+        assert all(b is not None for b in blobs), "p2p probe hung"
+        ok, why = nat.DeviceSolver.p2p_probe_ok(blobs, 0)
+        if corrupt:
+            # a wrong halo on one rank must be caught; every rank falls back
+            bad = bytearray(blobs[1])
+            bad[16] ^= 1   # sent_l checksum of rank 1 -> rank 0's right halo mismatches
+            ok, why = nat.DeviceSolver.p2p_probe_ok([bytes(b) if k != 1 else bytes(bad) for k, b in enumerate(blobs)], 0)
+            assert not ok and "right halo of rank 0" in why, why
+            th = [threading.Thread(target=s.p2p_fallback, daemon=True) for s in solvers]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=60)
+            assert not any(t.is_alive() for t in th), "p2p fallback hung"
+            assert not any(s.p2p_active for s in solvers)
+            p2p = False
+        else:
+            assert ok, why
     errors = []
 
     def run(s, n, res):
@@ -220,6 +249,21 @@ def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse):
         ref.step(n, residual=res)
     assert summ["dt"] == ref.summary()["dt"]
     assert summ["time"] == ref.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def test_p2p_self_validation_failure_falls_back(gpu):
+    """A checksum mismatch in the start-up probe makes every rank drop the
+    xGMI mailboxes for the host-side group transport; the poisoned ghost
+    columns are refilled and the run still equals one GPU bit for bit."""
+    text = decks.wedge15(240, 60, nmax=10 ** 6, nout=10 ** 5)
+    schedule = [(5, True), (20, False), (7, True)]
+    got, summ = _virtual_ranks(gpu, text, 3, schedule, lean=True, p2p=True, fuse=True, corrupt=True)
+    ref = gpu.Simulation(text, "gpu", lean=True)
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
     for f in FIELDS:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 

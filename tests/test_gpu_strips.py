@@ -74,3 +74,31 @@ def test_virtual_rank_driver_outputs_match_single_gpu(gpu, tmp_path, nranks):
     # each host keeps only its strip and one ghost column each side
     for r, (a, b) in enumerate(parts):
         assert tuple(cases[r].resident_columns) == (max(a - 1, 0), min(b + 1, cases[r].nx))
+
+
+def test_native_cli_two_gpu_ranks_match_one(gpu, tmp_path):
+    """bin/OpenHyperFLOW2D.sh <Project> 2 with the GPU backend: two native
+    processes (TCP rendezvous, IPC-mapped xGMI mailboxes validated at start-up
+    -- here both ranks share the box's one GPU) write the same bytes as one."""
+    import os
+    import subprocess
+
+    from tests.conftest import ROOT
+
+    text = _outputs_deck()
+    sh = os.path.join(ROOT, "openhyperflow2d_amd", "bin", "OpenHyperFLOW2D.sh")
+    logs = {}
+    for k in (1, 2):
+        d = tmp_path / ("r%d" % k)
+        d.mkdir()
+        (d / "W.dat").write_text(text)
+        r = subprocess.run(["timeout", "-k", "10", "240", sh, "W", str(k), "--backend", "gpu", "--cycles", "2",
+                            "--no-checkpoint"], cwd=d, capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, HF2D_MASTER_PORT=str(29800 + k), HF2D_AUTOTUNE="0"))
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        logs[k] = r.stdout
+    assert "halo transport p2p" in logs[2], logs[2][-2000:]
+    stem = "Wedge15_160x40"
+    for name in [stem + ".plt", "tp-" + stem + ".plt", stem + ".hf2d", "HeatFlux-X-" + stem + ".plt"]:
+        assert (tmp_path / "r1" / name).read_bytes() == (tmp_path / "r2" / name).read_bytes(), name
+    assert _cut_lines(logs[1]) == _cut_lines(logs[2])
