@@ -584,6 +584,13 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("p2p_fallback", &DeviceSolver::p2p_fallback, py::call_guard<py::gil_scoped_release>())
       .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
+      .def_readwrite("lean_persist", &DeviceSolver::lean_persist)
+      .def_readwrite("persist_steps", &DeviceSolver::persist_steps)
+      .def_readonly("persist_launches", &DeviceSolver::persist_launches)
+      .def_readonly("persist_why", &DeviceSolver::persist_why)
+      .def("persist_trace", &DeviceSolver::persist_trace, py::arg("steps") = 8,
+           py::call_guard<py::gil_scoped_release>())
+      .def_readonly("persist_trace_tiles", &DeviceSolver::persist_trace_tiles)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())

@@ -166,6 +166,16 @@ struct LeanIOCommon {
     if (lb & LB_DX_OUT) L.dSdx_out[k * N + idx] = L.dSdx_in[k * N + idx];
     if (lb & LB_DY_OUT) L.dSdy_out[k * N + idx] = L.dSdy_in[k * N + idx];
   }
+  // the node's new lean state (the persistent kernel keeps it on chip)
+  HF_HD void out_S(int k, real v) const { L.Sout[k * N + idx] = v; }
+  HF_HD void out_Ps(int k, real v) const { L.Pout_s[k * N + idx] = v; }
+  HF_HD void out_UVP(real u, real v, real p) const {
+    L.Uout[idx] = u;
+    L.Vout[idx] = v;
+    L.Pout[idx] = p;
+  }
+  HF_HD void out_CP(real v) const { L.CP[idx] = v; }
+  HF_HD void out_R(real v) const { L.R[idx] = v; }
 };
 
 // Global-memory IO.  FROMG: the previous step was generic, read its A/B/F.
@@ -257,11 +267,9 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
   io.obeta = own.beta;
   if (!own.filled) {
     // neither transported nor filled: carry the state into the other buffers
-    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = io.S(k);
-    if (lb & LB_DX_OUT)
-      for (int k = 0; k < NEQ; k++) L.dSdx_out[k * N + idx] = L.dSdx_in[k * N + idx];
-    if (lb & LB_DY_OUT)
-      for (int k = 0; k < NEQ; k++) L.dSdy_out[k * N + idx] = L.dSdy_in[k * N + idx];
+    for (int k = 0; k < NE; k++) io.out_S(k, io.S(k));
+    if (lb & (LB_DX_OUT | LB_DY_OUT))
+      for (int k = 0; k < NEQ; k++) io.keep_dS(k);
     return 1.0;
   }
   const bool active = !has_all(CT, NT_FC);
@@ -302,12 +310,10 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
   const real k_old = own.kk;
   if (s[I_RHO] == 0 || k_old < 1) {
     // fill_node() skipped the node: keep the previous primitives
-    for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = s[k];
+    for (int k = 0; k < NE; k++) io.out_S(k, s[k]);
     if (!SG)
-      for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
-    L.Uout[idx] = u_old;
-    L.Vout[idx] = v_old;
-    L.Pout[idx] = io.P0();
+      for (int k = 0; k < NCOMP; k++) io.out_Ps(k, s[4 + k]);
+    io.out_UVP(u_old, v_old, io.P0());
     return 1.0;
   }
   const real kk = c.CP / (c.CP - c.R);
@@ -361,7 +367,7 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
   const real Tg = p / c.R / s[I_RHO];
   // fluxes of this fill are built from the pre-chemistry species
   if (!SG)
-    for (int k = 0; k < NCOMP; k++) L.Pout_s[k * N + idx] = s[4 + k];
+    for (int k = 0; k < NCOMP; k++) io.out_Ps(k, s[4 + k]);
   real dt_local = 1.0;
   if (active) {
     if (Tg < 0.) {
@@ -378,18 +384,16 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
           chemistry_single_gas(c, *P.species);
         else
           chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
-        if (c.R != own.R) L.R[idx] = c.R;   // constant for a frozen mixture
-        L.CP[idx] = c.CP;
+        if (c.R != own.R) io.out_R(c.R);   // constant for a frozen mixture
+        io.out_CP(c.CP);
         // Y is output-only except for the no-slip SrcAdd of the next step
         if (OUT || noslip)
           for (int q = 0; q < NSPEC; q++) L.Y[q * N + idx] = c.Y[q];
       }
     }
   }
-  for (int k = 0; k < NE; k++) L.Sout[k * N + idx] = s[k];
-  L.Uout[idx] = U;
-  L.Vout[idx] = V;
-  L.Pout[idx] = p;
+  for (int k = 0; k < NE; k++) io.out_S(k, s[k]);
+  io.out_UVP(U, V, p);
   if (OUT) {
     L.Tout[idx] = Tg;
     L.kk[idx] = kk;

@@ -595,6 +595,263 @@ void hf2d_lean_tile_occ(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc, int
   lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent multi-step lean kernel (one rank, single GPU).  The one-shot
+// tile kernel re-stages every tile from HBM each step and the whole chip runs
+// "all staging, then all compute" (profiles/tile_phase_trace.md).  Here one
+// cooperative launch runs a window of plain steps: every workgroup keeps its
+// tile's lean state (S, U, V, p) in LDS and its cells' own persistent values
+// (beta, Cp, R, flags) in registers for the whole window, publishes only the
+// tile-border cells of each step to the global ping-pong arrays, and meets the
+// other workgroups at one grid barrier per step (the global dt MIN and the
+// halo are the only cross-tile dependencies), after which it reads its halo
+// ring.  Cross-workgroup traffic (border cells, dt, scenario values, Cauchy
+// dS) uses system-coherent loads/stores: the tiles of one step live on all
+// eight XCDs, whose L2s are not coherent with each other.  Same lean_cell()
+// arithmetic through PersistIO: bitwise equal to the per-step kernels.
+// ---------------------------------------------------------------------------
+constexpr int PERSIST_ERR = 4;               // neg_T bit: a grid barrier timed out
+constexpr int PERSIST_TRACE_STEPS = 8;       // steps recorded by the phase trace
+constexpr long PERSIST_SPIN_LIMIT = 1L << 24;
+
+__device__ inline unsigned long long load_sys_u64(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void store_sys_u64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The per-step tile kernel's IO, except that a tile-border node publishes its
+// new lean state with system-coherent stores (other XCDs read it as halo after
+// the grid barrier) and Cauchy nodes exchange dS the same way.
+template <bool SG>
+struct PersistIO : TileIO<SG> {
+  using Base = TileIO<SG>;
+  bool border;
+  HF_HD PersistIO(const LeanSoA& l, long i, const real* s, int nc, int w, int cc, bool b)
+      : Base(l, i, s, nc, w, cc), border(b) {}
+  HF_HD void out_S(int k, real v) const {
+    real* d = &this->L.Sout[k * this->N + this->idx];
+    if (border) p2p_store(d, v);
+    else *d = v;
+  }
+  HF_HD void out_Ps(int k, real v) const {
+    real* d = &this->L.Pout_s[k * this->N + this->idx];
+    if (border) p2p_store(d, v);
+    else *d = v;
+  }
+  HF_HD void out_UVP(real u, real v, real p) const {
+    if (border) {
+      p2p_store(&this->L.Uout[this->idx], u);
+      p2p_store(&this->L.Vout[this->idx], v);
+      p2p_store(&this->L.Pout[this->idx], p);
+    } else {
+      this->L.Uout[this->idx] = u;
+      this->L.Vout[this->idx] = v;
+      this->L.Pout[this->idx] = p;
+    }
+  }
+  // Cauchy nodes read dS/dx, dS/dy published by another tile in the previous step
+  HF_HD real dxL(int k) const { return p2p_load(&this->L.dSdx_in[k * this->N + this->iL]); }
+  HF_HD real dxR(int k) const { return p2p_load(&this->L.dSdx_in[k * this->N + this->iR]); }
+  HF_HD real dyU(int k) const { return p2p_load(&this->L.dSdy_in[k * this->N + this->iU]); }
+  HF_HD real dyD(int k) const { return p2p_load(&this->L.dSdy_in[k * this->N + this->iD]); }
+  HF_HD void put_dS(int k, real a, real b) const {
+    if (this->lb & LB_DX_OUT) p2p_store(&this->L.dSdx_out[k * this->N + this->idx], a);
+    if (this->lb & LB_DY_OUT) p2p_store(&this->L.dSdy_out[k * this->N + this->idx], b);
+  }
+  HF_HD void keep_dS(int k) const {
+    const long o2 = k * this->N + this->idx;
+    if (this->lb & LB_DX_OUT) p2p_store(&this->L.dSdx_out[o2], p2p_load(&this->L.dSdx_in[o2]));
+    if (this->lb & LB_DY_OUT) p2p_store(&this->L.dSdy_out[o2], p2p_load(&this->L.dSdy_in[o2]));
+  }
+};
+
+template <bool SG, int CPT>
+// 4 waves per SIMD: every tile of the headline grid must be co-resident
+__global__ __launch_bounds__(BLOCK, 4) void hf2d_lean_persist(StepParams P, LeanSoA L, LeanTile T,
+                                                           DevScalars* sc, int slot0, int nsteps, int serial,
+                                                           unsigned long long* bar, int dbg,
+                                                           unsigned long long* trace) {
+  extern __shared__ real lds[];
+  constexpr int NS = SG ? 4 : 4 + NCOMP;
+  constexpr int FU = SG ? 4 : 10;
+  __shared__ int s_abort;
+  __shared__ double sdt[BLOCK / WAVE];
+  __shared__ double s_scal[3];
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  const unsigned long long nwg = gridDim.x;
+  const int t = threadIdx.x;
+  const int NC = T.NC;
+  const long N = L.N;
+  // (cell coordinates are recomputed where used: fewer registers live
+  // across the step loop, which must fit 128 VGPRs for co-residency)
+  int i0, j0;
+  {
+    int ti, tjj, tc;
+    (void)lean_tile_cell(P, T, (int)b, t, &ti, &tjj, &tc, &i0, &j0, 0);
+  }
+  lean_tile_stage<SG>(P, L, T, i0, j0, lds, t, BLOCK);
+  if (t == 0) s_abort = 0;
+  __syncthreads();
+  int done = 0;   // steps completed
+  for (int s = 0; s < nsteps; s++) {
+    if (s > 0) {   // ping-pong: last step's outputs are this step's inputs
+      const real* in;
+      in = L.Sin; L.Sin = L.Sout; L.Sout = const_cast<real*>(in);
+      in = L.Pin_s; L.Pin_s = L.Pout_s; L.Pout_s = const_cast<real*>(in);
+      in = L.Uin; L.Uin = L.Uout; L.Uout = const_cast<real*>(in);
+      in = L.Vin; L.Vin = L.Vout; L.Vout = const_cast<real*>(in);
+      in = L.Pin; L.Pin = L.Pout; L.Pout = const_cast<real*>(in);
+      in = L.dSdx_in; L.dSdx_in = L.dSdx_out; L.dSdx_out = const_cast<real*>(in);
+      in = L.dSdy_in; L.dSdy_in = L.dSdy_out; L.dSdy_out = const_cast<real*>(in);
+    }
+    const int slot = (slot0 + s) % 3, slot_next = (slot + 1) % 3;
+    // dt and scenario values of this step (folded / written by the previous
+    // step): one coherent load per workgroup, broadcast through LDS (204k
+    // uncached loads of one address per step would serialise on its channel)
+    if (t == 0) {
+      s_scal[0] = bits_to_d(load_sys_u64(&sc->dt_bits[slot]));
+      if (P.scen) {
+        s_scal[1] = p2p_load(&sc->beta_min[slot]);
+        s_scal[2] = p2p_load(&sc->cfl_min[slot]);
+      }
+    }
+    __syncthreads();
+    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 0] = rt_clock();
+    P.dt = s_scal[0];
+    P.dtdx = P.dt / P.dx;
+    P.dtdy = P.dt / P.dy;
+    if (P.scen) {
+      P.beta_min = s_scal[1];
+      P.CFL_min = s_scal[2];
+    }
+    if (b == 0 && t == 0) {
+      store_sys_u64(&sc->dt_bits[slot_reset(slot)], d_to_bits(1.0));
+      sc->time_part += P.dt;   // block 0 only; the host reads it after the kernel
+      const double it = p2p_load(&sc->iter[slot]) + 1.0;
+      p2p_store(&sc->iter[slot_next], it);
+      if (P.scen) {
+        const real bs = table_eval(P.scen->beta, it), cs = table_eval(P.scen->cfl, it);
+        p2p_store(&sc->beta_min[slot_next], (bs < P.scen->beta0) ? bs : P.scen->beta0);
+        p2p_store(&sc->cfl_min[slot_next], (cs < P.scen->CFL) ? cs : P.scen->CFL);
+      }
+    }
+    double dtl = 1.0;
+    int neg = 0;
+    ResidualPack r;
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      int ci, cj, cc, a0, b0;
+      if (!lean_tile_cell(P, T, (int)b, t, &ci, &cj, &cc, &a0, &b0, q)) continue;
+      LeanOwn own;
+      lean_load_own<NS>(L, (long)ci * P.ny + cj, own);
+      const int ii = ci - a0, jj = cj - b0;
+      PersistIO<SG> io(L, (long)ci * P.ny + cj, lds, NC, T.W, cc,
+                       !(dbg & 8) && (ii == 0 || ii == T.TI - 1 || jj == 0 || jj == T.TJ - 1));
+      dtl = fmin(dtl, lean_cell<false, false>(P, L, io, own, ci, cj, r, &neg));
+    }
+    for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+    if ((t & (WAVE - 1)) == 0) sdt[t / WAVE] = dtl;
+    if (neg) atomicOr(&sc->neg_T, 1);
+    __syncthreads();   // every LDS read of this step is done
+    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 1] = rt_clock();
+    if (t == 0) {
+      double m = sdt[0];
+      for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+      if (serial) m = fmin(m, P.dt);
+      if (dbg & 4)
+        atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+      else
+        __hip_atomic_fetch_min(&sc->dt_bits[slot_next], d_to_bits(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // this step's state of the own cells back into LDS: exactly what the
+    // per-step kernel would stage next (nodes the step does not fill keep
+    // whatever the output arrays hold).  Written by this very thread, so
+    // L2/L1-resident; border nodes were stored system-coherent -> read alike.
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+      int ci, cj, cc, a0, b0;
+      if (s + 1 == nsteps || !lean_tile_cell(P, T, (int)b, t, &ci, &cj, &cc, &a0, &b0, q)) continue;
+      const long g = (long)ci * P.ny + cj;
+      const int ii = ci - a0, jj = cj - b0;
+      if (!(dbg & 8) && (ii == 0 || ii == T.TI - 1 || jj == 0 || jj == T.TJ - 1)) {
+#pragma unroll
+        for (int f = 0; f < NS; f++) lds[f * NC + cc] = p2p_load(&L.Sout[f * N + g]);
+        if (!SG)
+#pragma unroll
+          for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = p2p_load(&L.Pout_s[f * N + g]);
+        lds[FU * NC + cc] = p2p_load(&L.Uout[g]);
+        lds[(FU + 1) * NC + cc] = p2p_load(&L.Vout[g]);
+        lds[(FU + 2) * NC + cc] = p2p_load(&L.Pout[g]);
+      } else {
+#pragma unroll
+        for (int f = 0; f < NS; f++) lds[f * NC + cc] = L.Sout[f * N + g];
+        if (!SG)
+#pragma unroll
+          for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = L.Pout_s[f * N + g];
+        lds[FU * NC + cc] = L.Uout[g];
+        lds[(FU + 1) * NC + cc] = L.Vout[g];
+        lds[(FU + 2) * NC + cc] = L.Pout[g];
+      }
+    }
+    vm_drain();
+    __syncthreads();
+    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 2] = rt_clock();
+    // grid barrier: monotonic arrival counter, bounded wait
+    if (t == 0 && !(dbg & 1)) {
+      if (dbg & 2)
+        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const unsigned long long target = (unsigned long long)(s + 1) * nwg;
+      long spins = 0;
+      while (((dbg & 2) ? __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : load_sys_u64(bar)) <
+             target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > PERSIST_SPIN_LIMIT) {
+          atomicOr(&sc->neg_T, PERSIST_ERR);
+          break;
+        }
+      }
+      (void)__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_abort = (__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & PERSIST_ERR) ? 1 : 0;
+    }
+    __syncthreads();
+    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 3] = rt_clock();
+    done = s + 1;
+    if (s_abort || done == nsteps) break;   // the last step's output arrays are complete
+    // the next step's halo ring: the neighbour tiles' border cells of this step
+    for (int cc = t; cc < NC; cc += BLOCK) {
+      const int ii = cc / T.W - 1, jj = cc - (ii + 1) * T.W - 1;
+      const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
+      const int gi = i0 + ii, gj = j0 + jj;
+      if (!(xh || yh) || (xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
+      const long g = (long)gi * P.ny + gj;
+      if (dbg & 8) {
+#pragma unroll
+        for (int f = 0; f < NS; f++) lds[f * NC + cc] = L.Sout[f * N + g];
+        lds[FU * NC + cc] = L.Uout[g];
+        lds[(FU + 1) * NC + cc] = L.Vout[g];
+        lds[(FU + 2) * NC + cc] = L.Pout[g];
+        continue;
+      }
+#pragma unroll
+      for (int f = 0; f < NS; f++) lds[f * NC + cc] = p2p_load(&L.Sout[f * N + g]);
+      if (!SG)
+#pragma unroll
+        for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = p2p_load(&L.Pout_s[f * N + g]);
+      lds[FU * NC + cc] = p2p_load(&L.Uout[g]);
+      lds[(FU + 1) * NC + cc] = p2p_load(&L.Vout[g]);
+      lds[(FU + 2) * NC + cc] = p2p_load(&L.Pout[g]);
+    }
+    __syncthreads();
+    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 4] = rt_clock();
+    if (trace && t == 0 && s == 0) trace[((size_t)b * PERSIST_TRACE_STEPS) * 6 + 5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
+  (void)done;   // the output arrays of the last step hold the complete state
+}
+
 // Software-pipelined lean step: a persistent grid (a few workgroups per CU)
 // walks the CPT=1 tiles tile = b, b + G, b + 2G, ...; while tile k is
 // computed from LDS, the staged fields and own-cell data of tile k+G are
@@ -1086,6 +1343,12 @@ struct DeviceSolver::Impl {
   real *Spre[2], *P2[2];
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
+  unsigned long long* persist_bar = nullptr;   // grid-barrier counter of hf2d_lean_persist
+  // hf2d_lean_persist launch geometry, cached per strip shape
+  long persist_key = -1;
+  LeanTile persist_T{};
+  const void* persist_fn = nullptr;
+  size_t persist_shmem = 0;
   int32_t* wslot;
   // K10 (y+): owned wall nodes, their friction velocities, all strips' values
   long* wall_own = nullptr;
@@ -1608,6 +1871,12 @@ void DeviceSolver::sync_scalars() {
   if (err & 2) {
     char b[256];
     std::snprintf(b, sizeof b, "ERROR: P2P halo exchange timed out (peer rank not responding) before iteration %ld",
+                  last_iter + iter);
+    throw std::runtime_error(b);
+  }
+  if (err & PERSIST_ERR) {
+    char b[256];
+    std::snprintf(b, sizeof b, "ERROR: persistent step kernel: grid barrier timed out before iteration %ld",
                   last_iter + iter);
     throw std::runtime_error(b);
   }
@@ -2183,9 +2452,156 @@ struct DeviceSolver::GraphCache {
 
 void DeviceSolver::flush_pending() {
   if (pending.empty()) return;
+  if (pending_persist && pending.size() >= 2) {
+    run_persist();
+    return;
+  }
+  pending_persist = false;
   std::vector<StepParams> q;
   q.swap(pending);
   for (const StepParams& p : q) do_step_eager(p, false);
+}
+
+// The lean tile step of one rank, eligible for the persistent window kernel.
+bool DeviceSolver::persist_eligible() const {
+  const Impl& m = *impl;
+  // single-gas only: the multi-gas variant spills heavily at 4 waves / SIMD
+  return lean_persist > 0 && persist_steps >= 2 && lean && lean_ok && lean_sg && lean_sg_ok && lean_tile &&
+         lean_march <= 0 &&
+         lean_pipe <= 0 && lean_state == 1 && h.ny >= LEAN_TILE_MIN_TJ && cs.cfg.ProblemType != SM_NS &&
+         m.nranks <= 1 && !m.p2p.on && !m.local && !m.comm && !tile_trace && lean_wgcu <= 0 && lean_occ == 0;
+}
+
+void DeviceSolver::run_persist() {
+  Impl& m = *impl;
+  std::vector<StepParams> q;
+  q.swap(pending);
+  pending_persist = false;
+  auto eager = [&](const std::string& why) {
+    if (!why.empty()) {
+      lean_persist = 0;
+      persist_why = why;
+    }
+    for (const StepParams& p : q) do_step_eager(p, false);
+  };
+  const uint64_t sig = graph_signature(q[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
+                                       lean_tj, 0, 0, 0, 0);
+  for (const StepParams& p : q)
+    if (graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt, lean_tj, 0, 0, 0, 0) !=
+        sig)
+      return eager("");
+  StepParams P = q[0];
+  P.nx = h.nx;
+  P.ny = h.ny;
+  P.i0 = l_off;
+  P.i1 = l_off + (gi1 - gi0);
+  P.gx0 = gi0 - l_off;
+  P.do_residual = 0;
+  P.species = m.species;
+  P.scen = m.scen;
+  const bool sg = lean_sg && lean_sg_ok;
+  if (!sg) return eager("multi-gas lean state");
+  // geometry of its own (the per-step autotuner's choice may not fit): two
+  // cells per thread, the auto tile height, then taller tiles until every
+  // tile is co-resident
+  const long key = (long)(P.i1 - P.i0) * 100000 + P.ny;
+  if (m.persist_key != key) {
+    int ncu = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    int ntile = 0, per_cu = 0;
+    bool fits = false;
+    std::string tried;
+    const char* fc = std::getenv("HF2D_PERSIST_CPT");   // tuning / diagnosis: force 1 or 2 cells per thread
+    const int only_cpt = fc ? std::atoi(fc) : 0;
+    for (int tj : {0, 32, 40, 50, 64}) {
+      for (int cpt : {2, 1}) {
+        if (only_cpt && cpt != only_cpt) continue;
+        m.persist_T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, tj, cpt);
+        ntile = m.persist_T.nbi * m.persist_T.nbj;
+        m.persist_shmem = (size_t)lean_tile_fields(true) * m.persist_T.NC * sizeof(real);
+        m.persist_fn = cpt == 2 ? (const void*)hf2d_lean_persist<true, 2> : (const void*)hf2d_lean_persist<true, 1>;
+        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m.persist_fn, BLOCK, m.persist_shmem));
+        char b[96];
+        std::snprintf(b, sizeof b, "%scpt=%d TJ=%d: %d tiles, %d/CU", tried.empty() ? "" : "; ", cpt, m.persist_T.TJ,
+                      ntile, per_cu);
+        tried += b;
+        if ((long)per_cu * ncu >= ntile) {
+          fits = true;
+          break;
+        }
+      }
+      if (fits) break;
+    }
+    if (!fits) return eager("no tile geometry is co-resident on " + std::to_string(ncu) + " CUs (" + tried + ")");
+    m.persist_key = key;
+  }
+  const LeanTile T = m.persist_T;
+  const void* fn = m.persist_fn;
+  const size_t shmem = m.persist_shmem;
+  const int ntile = T.nbi * T.nbj;
+  if (!m.persist_bar) m.persist_bar = m.mem.alloc<unsigned long long>(1);
+  LeanSoA L0 = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+  int slot0 = (int)(nstep % 3), n = (int)q.size();
+  int serial = cs.cfg.semantics == Semantics::SERIAL ? 1 : 0;
+  DevScalars* sc = m.sc;
+  unsigned long long* bar = m.persist_bar;
+  LeanTile Tt = T;
+  static const int dbg = [] {
+    const char* e = std::getenv("HF2D_PERSIST_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  int dbgv = dbg;
+  unsigned long long* trace = persist_trace_buf;
+  void* args[] = {&P, &L0, &Tt, &sc, &slot0, &n, &serial, &bar, &dbgv, &trace};
+  HIP_CHECK(hipMemsetAsync(bar, 0, sizeof(unsigned long long), m.stream));
+  const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(ntile), dim3(BLOCK), args, (unsigned)shmem, m.stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return eager(std::string("cooperative launch failed: ") + hipGetErrorString(e));
+  }
+  nstep += n;
+  if (n & 1) {
+    sbuf = 1 - sbuf;
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+  }
+  persist_launches++;
+  persist_trace_tiles = ntile;
+}
+
+std::vector<unsigned long long> DeviceSolver::persist_trace(int steps) {
+  Impl& m = *impl;
+  flush_pending();
+  std::vector<unsigned long long> out;
+  if (!persist_eligible()) return out;
+  // the window's geometry is known after one launch
+  if (m.persist_key < 0) {
+    run_steps(std::max(steps, 2), false);
+    flush_pending();
+  }
+  const int ntile = m.persist_T.nbi * m.persist_T.nbj;
+  const size_t words = (size_t)ntile * 8 * 6;
+  unsigned long long* d = nullptr;
+  HIP_CHECK(hipMalloc((void**)&d, words * sizeof(unsigned long long)));
+  HIP_CHECK(hipMemset(d, 0, words * sizeof(unsigned long long)));
+  persist_trace_buf = d;
+  const int ps = persist_steps;
+  persist_steps = 8;
+  try {
+    run_steps(9, false);   // one window of 8 plain steps + the eager last step
+  } catch (...) {
+    persist_steps = ps;
+    persist_trace_buf = nullptr;
+    (void)hipFree(d);
+    throw;
+  }
+  persist_steps = ps;
+  persist_trace_buf = nullptr;
+  HIP_CHECK(hipDeviceSynchronize());
+  out.resize(words);
+  HIP_CHECK(hipMemcpy(out.data(), d, words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipFree(d));
+  return out;
 }
 
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
@@ -2193,6 +2609,16 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   // (the in-process host transport synchronises on the host: eager only)
   const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
                      !(lean && lean_ok && lean_state == 0);
+  if (plain && persist_eligible()) {
+    if (!pending.empty() && !pending_persist) flush_pending();
+    pending_persist = true;
+    pending.push_back(P0);
+    if ((int)pending.size() >= persist_steps) run_persist();
+    StepResult r;
+    r.async = true;
+    return r;
+  }
+  if (pending_persist) flush_pending();
   if (!plain || (pending.empty() && nstep % GRAPH_STEPS != 0)) {
     flush_pending();
     return do_step_eager(P0, want_res);

@@ -155,6 +155,19 @@ class DeviceSolver : public SolverBase {
   bool use_graph = true;
   long graph_launches = 0;
   void flush_pending();
+  // persistent multi-step lean kernel (hf2d_lean_persist): windows of up to
+  // persist_steps plain steps in one cooperative launch.  Off by default:
+  // bitwise equal but 3-5x slower per step than the per-step tile kernel on
+  // MI355X (profiles/persistent_kernel_trace.md)
+  int lean_persist = 0;
+  int persist_steps = 48;
+  long persist_launches = 0;
+  std::string persist_why;   // why the persistent kernel was disabled ("" if it was not)
+  // phase trace of one 8-step window: per tile and step [start, computed,
+  // committed, barrier passed, halo loaded, XCC_ID] (s_memrealtime, 100 MHz)
+  std::vector<unsigned long long> persist_trace(int steps = 8);
+  unsigned long long* persist_trace_buf = nullptr;
+  int persist_trace_tiles = 0;
 
  private:
   struct Impl;
@@ -162,7 +175,10 @@ class DeviceSolver : public SolverBase {
   struct GraphCache;
   std::unique_ptr<GraphCache> graph;
   std::vector<StepParams> pending;
+  bool pending_persist = false;   // `pending` holds a persistent window (else a graph window)
   void run_graph();
+  bool persist_eligible() const;
+  void run_persist();
   // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
   void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };

@@ -478,3 +478,28 @@ def test_autotune_thread_block_size_zero(gpu, monkeypatch):
     assert a.summary()["time"] == b.summary()["time"]
     for f in FIELDS:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("nx,ny,steps", [(2000, 200, 101), (300, 64, 57)])
+def test_persistent_window_kernel_matches_per_step(gpu, nx, ny, steps):
+    """hf2d_lean_persist (one cooperative launch per window of plain steps,
+    tile state resident in LDS, grid barrier per step) == the per-step tile
+    kernel, bit for bit, including dt and the accumulated time."""
+    text = decks.wedge15(nx, ny, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu", lean=True)
+    b = gpu.Simulation(text, "gpu", lean=True)
+    a.solver.lean_persist = 1   # opt-in (slower than the per-step kernel, see its docstring)
+    b.solver.lean_persist = 0
+    n0 = (a.solver.persist_launches, b.solver.persist_launches)   # (the autotuner may have stepped)
+    for sim in (a, b):
+        sim.step(3)                  # generic -> lean hand-over outside the window
+        sim.step(steps, residual=True)
+    assert a.solver.persist_launches > n0[0], a.solver.persist_why
+    assert b.solver.persist_launches == n0[1]
+    sa, sb = a.summary(), b.summary()
+    assert sa["dt"] == sb["dt"] and sa["time"] == sb["time"]
+    # (the residual partials are summed per tile: the two solvers' autotuned
+    # tile shapes may differ, so the sums may differ in the last bit)
+    np.testing.assert_allclose(np.array(sa["rms"]), np.array(sb["rms"]), rtol=1e-12, atol=0)
+    for f in FIELDS + ["mach"]:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
