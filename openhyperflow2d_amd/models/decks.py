@@ -123,6 +123,50 @@ def wedge15(nx: int = 200, ny: int = 40, *, navier_stokes: bool = False, turbule
     return t
 
 
+def flat_plate(nx: int = 250, ny: int = 100, *, dx: float = 1.0e-3, dy: float = 1.0e-4, x_le: float = 0.2,
+               mach: float = 2.5, p: float = 1.0e3, T: float = 288.9, turbulence: int = 0,
+               nmax: int = 200, nout: int = 100, project: Optional[str] = None, cfl: Optional[float] = None) -> str:
+    """Zero-pressure-gradient flat plate (validation): the Wedge template with a
+    0-degree ramp, so the no-slip bound runs along y = 0 from ``x_le*L`` to
+    the outlet, a symmetry line ahead of it, far-field inflow and top, a
+    non-reflecting outlet.  ``turbulence``: the deck's TurbulenceModel code
+    (0 laminar, 4 k-eps, 6 k-omega SST)."""
+    t = remove_commented_directives(template_text("Wedge.dat"))
+    project = project or "FlatPlate_%dx%d" % (nx, ny)
+    t = _rename(t, project)
+    L, H = nx * dx, ny * dy
+    x0 = x_le * L
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", dx)
+    t = set_key(t, "dy", dy)
+    t = set_key(t, "ProblemType", 1)
+    t = set_key(t, "TurbulenceModel", turbulence)
+    t = set_key(t, "TurbExtModel", 4)
+    t = set_key(t, "isTurbulenceReset", 1 if turbulence else 0)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", 1.0e-30)
+    t = set_key(t, "isAdiabaticWall", 0)
+    t = set_key(t, "Ts0", T)
+    for f in (1, 2):
+        t = set_key(t, "Flow2D-%d.p" % f, p)
+        t = set_key(t, "Flow2D-%d.T" % f, T)
+    t = set_key(t, "Flow2D-1.Mach", mach)
+    if cfl is not None:
+        t = set_key(t, "CFL", cfl)
+        t = set_table(t, "CFL_Scenario", [(0.0, cfl), (1.0e9, cfl)])
+    eps = 1e-9
+    t = set_table(t, "Contour1", [(0.0, H), (L - eps, H), (L - eps, 0.0), (x0, 0.0), (0.0, 0.0)])
+    for b in range(1, 6):
+        t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, turbulence)
+    t = set_table(t, "Area1", [(3, ny // 2)])
+    t = set_key(t, "Area1.TurbulenceModel", turbulence)
+    t = set_key(t, "NumArea", 1)   # no solid under the plate: it is the domain edge
+    return t
+
+
 def step(nx: int = 1200, ny: int = 400, *, navier_stokes: bool = True, nmax: int = 200, nout: int = 100,
          project: Optional[str] = None, exit_time: float = 1.0e-30) -> str:
     """Mach-3 forward-facing step (TestCases/Step.dat rescaled)."""
@@ -524,4 +568,4 @@ def with_mechanism(text: str, mechanism: str = "h2_air_li2004", substeps: int = 
 
 
 GENERATORS = {"wedge15": wedge15, "step": step, "triple_point": triple_point, "resonator": resonator,
-              "scramjet": scramjet, "reactor0d": reactor0d}
+              "scramjet": scramjet, "reactor0d": reactor0d, "flat_plate": flat_plate}
