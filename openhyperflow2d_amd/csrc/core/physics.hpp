@@ -365,14 +365,19 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (n.k < 1) return false;
   real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
   if (!MX::MECH) n.k = n.CP / (n.CP - n.R);
-  if (has_all(n.CT, CT_U_CONST))
-    n.S[I_RHOU] = n.U * n.S[I_RHO];
-  else
-    n.U = n.S[I_RHOU] / n.S[I_RHO];
-  if (has_all(n.CT, CT_V_CONST))
-    n.S[I_RHOV] = n.V * n.S[I_RHO];
-  else
-    n.V = n.S[I_RHOV] / n.S[I_RHO];
+  {
+    // every branch writes both members (same values as "if U const: rho*U,
+    // else U = rhoU/rho"): two stores to different members under a branch
+    // are merged by the compiler into one store through a selected address,
+    // which puts the whole node struct in scratch memory on the GPU
+    const bool uc = has_all(n.CT, CT_U_CONST), vc = has_all(n.CT, CT_V_CONST);
+    const real r = n.S[I_RHO], su = n.S[I_RHOU], sv = n.S[I_RHOV];
+    const real u = uc ? n.U : su / r, v = vc ? n.V : sv / r;
+    n.S[I_RHOU] = uc ? u * r : su;
+    n.S[I_RHOV] = vc ? v * r : sv;
+    n.U = u;
+    n.V = v;
+  }
 
   if (P.sm == SM_NS) {
     if (P.is_init && n.TurbType > 0) {

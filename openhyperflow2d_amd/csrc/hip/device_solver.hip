@@ -140,10 +140,31 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
   }
 }
 
+template <int MODE, int NSB>
+__device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const SoA& pold, const SoA& out, long c0,
+                                          long c1, DevScalars* sc, int slot, int slot_next, int serial,
+                                          int store_grad);
+
 template <int MODE = SK_GENERIC, int NSB = 1>
 __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1,
                                                     DevScalars* sc, int slot, int slot_next, int serial,
                                                     int store_grad) {
+  fill_body<MODE, NSB>(P, sin, pold, out, c0, c1, sc, slot, slot_next, serial, store_grad);
+}
+
+// The same fill with a register budget of OCC waves per SIMD (the split N-S
+// fills compile to 165-255 VGPRs, i.e. 1-3 waves; DeviceSolver::fill_occ)
+template <int MODE, int NSB, int OCC>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_fill_occ(
+    StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1, DevScalars* sc, int slot, int slot_next, int serial,
+    int store_grad) {
+  fill_body<MODE, NSB>(P, sin, pold, out, c0, c1, sc, slot, slot_next, serial, store_grad);
+}
+
+template <int MODE, int NSB>
+__device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const SoA& pold, const SoA& out, long c0,
+                                          long c1, DevScalars* sc, int slot, int slot_next, int serial,
+                                          int store_grad) {
   apply_dt(P, sc, slot);
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   double dtl = 1.0;
@@ -2915,22 +2936,39 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     }
     // SGL: gradients / Diff only when the host reads the record (or y+ follows)
     const int sg_out = (step_outputs || want_res) ? 1 : 0;
+    // register budget: measured on 1x MI355X (tools/fill_occ_sweep.sh): the
+    // mechanism fill is 10 % faster at 2 waves/SIMD (256 VGPRs, a few spills)
+    // than at the compiler's 1; SGL / SGT are fastest at the default
+    const int focc = fill_occ >= 0 ? fill_occ : (mode == SK_MECH ? 2 : 0);
+#define HF2D_FILL(MD, NS, SGO)                                                                                  \
+  do {                                                                                                          \
+    if (focc == 2)                                                                                          \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 2>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else if (focc == 3)                                                                                         \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 3>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else if (focc == 4)                                                                                         \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 4>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((hf2d_fill<MD, NS>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,  \
+                         slot, slot_next, serial, SGO);                                                        \
+  } while (0)
     if (mode == SK_MECH) {
       if (m.nsp <= 9)
-        hipLaunchKernelGGL((hf2d_fill<SK_MECH, 9>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,
-                           slot, slot_next, serial, 1);
+        HF2D_FILL(SK_MECH, 9, 1);
       else
         hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
                            m.sc, slot, slot_next, serial, 1);
     } else if (mode == SK_SGL)
-      hipLaunchKernelGGL(hf2d_fill<SK_SGL>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
-                         slot_next, serial, sg_out);
+      HF2D_FILL(SK_SGL, 1, sg_out);
     else if (mode == SK_SGT)
-      hipLaunchKernelGGL(hf2d_fill<SK_SGT>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
-                         slot_next, serial, 1);
+      HF2D_FILL(SK_SGT, 1, 1);
     else
       hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
                          slot_next, serial, 1);
+#undef HF2D_FILL
     HIP_CHECK(hipGetLastError());
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;

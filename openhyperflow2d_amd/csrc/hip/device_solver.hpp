@@ -145,6 +145,7 @@ class DeviceSolver : public SolverBase {
   bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
   bool sgl_ok = false;
   int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)
+  int fill_occ = -1;      // split fill kernels: -1 auto, 0 compiler default, 2/3/4 waves-per-SIMD register budget
   std::string sgl_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
   std::vector<uint8_t> lean_bytes;
