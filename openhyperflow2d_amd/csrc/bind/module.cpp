@@ -586,6 +586,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
       .def_readwrite("lean_persist", &DeviceSolver::lean_persist)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
+      .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
       .def_readwrite("persist_steps", &DeviceSolver::persist_steps)
       .def_readonly("persist_launches", &DeviceSolver::persist_launches)
       .def_readonly("persist_why", &DeviceSolver::persist_why)

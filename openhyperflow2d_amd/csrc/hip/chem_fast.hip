@@ -1,3 +1,4 @@
+#include <algorithm>
 // K12 (mechanism mode): operator-split kinetics with a compiled mechanism,
 // one cell per lane, everything in registers (gfx950, FP64).
 //
@@ -286,6 +287,62 @@ __global__ __launch_bounds__(256) void hf2d_chem_fast(StepParams P, SoA mid, SoA
   for (int s = 0; s < NS; s++) out.Ys[(long)s * N + idx] = y[s];
 }
 
+// Compacted form.  On the scramjet only 2-5 % of the cells are above Tchem,
+// but 16-20 % of the 64-cell wavefronts hold at least one of them, and a
+// wavefront costs as much as its slowest lane.  Pass 1 copies the species of
+// every cell that stays frozen and appends the reacting cells to a list
+// (one atomic per wavefront); pass 2 integrates the listed cells densely.
+// Cells are independent, so the result does not depend on the list order.
+__device__ inline bool chem_hot(const StepParams& P, const SoA& mid, const real* Tprev, long idx, double Tchem) {
+  return is_active(mid.CT[idx]) && mid.S[idx] > 0.0 && Tprev[idx] >= Tchem && P.dt > 0.0;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void hf2d_chem_fast_mark(StepParams P, SoA mid, SoA out, const real* Tprev, long c0,
+                                                           long c1, DevScalars* sc, int slot, double Tchem,
+                                                           int* list, unsigned* count) {
+  apply_dt(P, sc, slot);
+  const long idx = c0 + (long)blockIdx.x * 256 + threadIdx.x;
+  const bool in = idx < c1;
+  const bool hot = in && chem_hot(P, mid, Tprev, idx, Tchem);
+  const long N = mid.N;
+  if (in && !hot) {
+#pragma unroll
+    for (int s = 0; s < M::NS; s++) out.Ys[(long)s * N + idx] = mid.Ys[(long)s * N + idx];
+  }
+  const unsigned long long ball = __ballot(hot);
+  if (!ball) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)ball) - 1;
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(count, (unsigned)__popcll(ball));
+  base = __shfl(base, leader, 64);
+  if (hot) list[base + __popcll(ball & ((1ull << lane) - 1ull))] = (int)idx;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void hf2d_chem_fast_list(StepParams P, SoA mid, SoA out, const real* Tprev,
+                                                           DevScalars* sc, int slot, int nsub, const int* list,
+                                                           const unsigned* count) {
+  apply_dt(P, sc, slot);
+  const unsigned n = *count;
+  constexpr int NS = M::NS;
+  const long N = mid.N;
+  for (unsigned k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+    const long idx = list[k];
+    double y[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) y[s] = mid.Ys[(long)s * N + idx];
+    const double rho = mid.S[idx];
+    const double ru = mid.S[(long)I_RHOU * N + idx], rv = mid.S[(long)I_RHOV * N + idx];
+    const double e = (mid.S[(long)I_RHOE * N + idx] - 0.5 * (ru * ru + rv * rv) / rho) / rho;
+    double T = Tprev[idx];
+    chem_cell<M>(rho, e, y, &T, P.dt, nsub);
+#pragma unroll
+    for (int s = 0; s < NS; s++) out.Ys[(long)s * N + idx] = y[s];
+  }
+}
+
 // standalone operator (tests / benchmarks): rhoY [ns][n] in place at (rho, e)
 template <class M>
 __global__ __launch_bounds__(256) void hf2d_chem_fast_op(double* rhoY, const double* rho, const double* e, double* T,
@@ -307,10 +364,22 @@ __global__ __launch_bounds__(256) void hf2d_chem_fast_op(double* rhoY, const dou
 bool chem_fast_available(const std::string& mech) { return mech == "h2_air_li2004"; }
 
 bool chem_fast_launch(const std::string& mech, const StepParams& P, const SoA& mid, const SoA& out, const real* Tprev,
-                      long c0, long c1, DevScalars* sc, int slot, double Tchem, int nsub, hipStream_t st) {
+                      long c0, long c1, DevScalars* sc, int slot, double Tchem, int nsub, hipStream_t st, int* list,
+                      unsigned* count) {
   if (mech != "h2_air_li2004" || mid.nsp != Mech_h2_air_li2004::NS) return false;
   const unsigned nb = (unsigned)((c1 - c0 + 255) / 256);
   if (nb == 0) return true;
+  if (list && count) {   // compacted: frozen cells copied, reacting cells integrated densely
+    if (hipMemsetAsync(count, 0, sizeof(unsigned), st) != hipSuccess) return false;
+    hipLaunchKernelGGL(hf2d_chem_fast_mark<Mech_h2_air_li2004>, dim3(nb), dim3(256), 0, st, P, mid, out, Tprev, c0, c1,
+                       sc, slot, Tchem, list, count);
+    // grid-stride over the list: enough workgroups for a fully reacting grid
+    // to fill the chip several times, without knowing the count on the host
+    const unsigned gl = std::min(nb, 4096u);
+    hipLaunchKernelGGL(hf2d_chem_fast_list<Mech_h2_air_li2004>, dim3(gl), dim3(256), 0, st, P, mid, out, Tprev, sc,
+                       slot, nsub, list, count);
+    return hipGetLastError() == hipSuccess;
+  }
   hipLaunchKernelGGL(hf2d_chem_fast<Mech_h2_air_li2004>, dim3(nb), dim3(256), 0, st, P, mid, out, Tprev, c0, c1, sc,
                      slot, Tchem, nsub);
   return hipGetLastError() == hipSuccess;

@@ -11,9 +11,11 @@ struct SoA;
 struct DevScalars;
 
 bool chem_fast_available(const std::string& mech);
-// mechanism-mode step kernel over linear cells [c0, c1): mid.Ys -> out.Ys
+// mechanism-mode step kernel over linear cells [c0, c1): mid.Ys -> out.Ys.
+// list (>= c1 - c0 ints) + count: compacted form (reacting cells only do work)
 bool chem_fast_launch(const std::string& mech, const StepParams& P, const SoA& mid, const SoA& out, const double* Tprev,
-                      long c0, long c1, DevScalars* sc, int slot, double Tchem, int nsub, ihipStream_t* st);
+                      long c0, long c1, DevScalars* sc, int slot, double Tchem, int nsub, ihipStream_t* st,
+                      int* list = nullptr, unsigned* count = nullptr);
 // standalone operator on n cells (rhoY [ns][n] and T updated in place); mean kernel ms
 double chem_fast_run_host(const std::string& mech, double* rhoY, const double* rho, const double* e, double* T, long n,
                           double dt, int nsub, int repeats);

@@ -1379,6 +1379,8 @@ struct DeviceSolver::Impl {
   MechData* mech = nullptr;
   int nsp = 0;
   std::unique_ptr<ChemMechPack> chem_pack;   // MFMA kinetics kernel's mechanism image
+  int* chem_list = nullptr;                  // compacted kinetics: reacting cells of the step
+  unsigned* chem_count = nullptr;
   real *Ys[2] = {nullptr, nullptr}, *As = nullptr, *Bs = nullptr, *Fs = nullptr, *betas = nullptr;
   real *dSdxs[2] = {nullptr, nullptr}, *dSdys[2] = {nullptr, nullptr};
   SpeciesProps* species = nullptr;
@@ -3010,7 +3012,12 @@ void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& o
   // compiled mechanism: register-resident VALU kernel (chem_fast.hip)
   if (kind == 1) {
     if (!chem_fast_ok) throw std::runtime_error("chem_kernel=1: no compiled kernel for mechanism " + cs.cfg.mech->name);
-    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, out, Tprev, k0, k1, m.sc, slot, md.Tchem, md.nsub, m.stream))
+    if (chem_compact && !m.chem_list) {
+      m.chem_list = m.mem.alloc<int>(h.N);
+      m.chem_count = m.mem.alloc<unsigned>(1);
+    }
+    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, out, Tprev, k0, k1, m.sc, slot, md.Tchem, md.nsub, m.stream,
+                          chem_compact ? m.chem_list : nullptr, chem_compact ? m.chem_count : nullptr))
       throw std::runtime_error("hf2d_chem_fast launch failed");
     chem_kernel_used = "hf2d_chem_fast";
     return;

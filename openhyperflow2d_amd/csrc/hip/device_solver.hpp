@@ -138,6 +138,7 @@ class DeviceSolver : public SolverBase {
   std::string lean_why;
   bool chem_fast = true;  // mechanism mode: compiled-mechanism kinetics kernel when one exists
   bool chem_fast_ok = false;   // the loaded mechanism equals a compiled one
+  bool chem_compact = true;    // compiled kinetics over a compacted list of the reacting cells
   // kinetics kernel: 0 auto (compiled VALU kernel if the mechanism has one, else
   // the MFMA kernel), 1 compiled, 2 MFMA, 3 generic runtime-data VALU
   int chem_kernel = 0;

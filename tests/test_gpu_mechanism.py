@@ -85,3 +85,26 @@ def test_gpu_mech_transport_bitwise_without_kinetics(gpu):
     c.step(30, residual=True)
     for f in ("rho", "U", "V", "p", "T", "mu", "Y:H2", "Y:N2"):
         assert np.array_equal(g.field(f), c.field(f)), f
+
+
+@pytest.mark.parametrize("deck", ["reactor", "scramjet"])
+def test_compacted_kinetics_match_per_cell_kernel(gpu, deck):
+    """hf2d_chem_fast over a compacted list of the reacting cells (mark pass +
+    dense pass) == the one-cell-per-lane kernel over the grid, bit for bit."""
+    from openhyperflow2d_amd.models import decks
+
+    if deck == "reactor":
+        text = decks.with_mechanism(decks.reactor0d(16, 16, T=1300.0, p=101325.0), substeps=2)
+        n = 200
+    else:
+        text = decks.scramjet(600, 60, nmax=10 ** 9, nout=10 ** 8)
+        n = 300
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    b.solver.chem_compact = False
+    a.step(n)
+    b.step(n)
+    assert a.solver.chem_kernel_used == b.solver.chem_kernel_used == "hf2d_chem_fast"
+    np.testing.assert_array_equal(a.field("T"), b.field("T"))
+    for s in ("H2", "O2", "H2O", "OH", "N2"):
+        np.testing.assert_array_equal(a.field("Y:" + s), b.field("Y:" + s), err_msg=s)
