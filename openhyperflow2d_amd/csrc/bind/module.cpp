@@ -587,6 +587,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_persist", &DeviceSolver::lean_persist)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
+      .def_readwrite("comm_overlap", &DeviceSolver::comm_overlap)
+      .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
       .def_readwrite("persist_steps", &DeviceSolver::persist_steps)
       .def_readonly("persist_launches", &DeviceSolver::persist_launches)
       .def_readonly("persist_why", &DeviceSolver::persist_why)

@@ -385,14 +385,24 @@ constexpr int TILE_TRACE_WORDS = 8;
 constexpr int LDS_PER_CU = 160 * 1024;
 __device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
+// part: 0 every tile; 1 the tiles of the strip's first and last tile column
+// (their results feed the halo exchange); 2 the other tiles.  The grid of a
+// part launch has exactly that many workgroups (DeviceSolver comm overlap).
+__device__ inline unsigned tile_of_part(unsigned bl, int part, const LeanTile& T) {
+  if (part == 1) return bl < (unsigned)T.nbj ? bl : (unsigned)((T.nbi - 1) * T.nbj) + (bl - T.nbj);
+  if (part == 2) return (unsigned)T.nbj + bl;
+  return bl;
+}
+
 template <bool RES, bool OUT, bool SG, int CPT, bool FX = false, bool TR = false>
 __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, const LeanTile& T, DevScalars* sc,
                                                int slot, int slot_next, int serial, ResidualPack* partials,
-                                               const FusedX& X = FusedX{}, unsigned long long* trace = nullptr) {
+                                               const FusedX& X = FusedX{}, unsigned long long* trace = nullptr,
+                                               int part = 0) {
   extern __shared__ real lds[];
   unsigned long long tr[5];
   if (TR) tr[0] = rt_clock();
-  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
   apply_dt(P, sc, slot);
@@ -555,8 +565,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
 template <bool RES, bool OUT, bool SG, int OCC = 0, int CPT = 1>
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
                                                          int slot, int slot_next, int serial,
-                                                         ResidualPack* partials) {
-  lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
+                                                         ResidualPack* partials, int part = 0) {
+  lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials, FusedX{}, nullptr, part);
 }
 
 // Phase-traced plain step (profiling only, DeviceSolver::trace_tile).
@@ -1144,6 +1154,15 @@ __global__ void hf2d_unpack(ColList L, int col, int ny, const real* buf) {
   L.f[f][(long)col * ny + j] = buf[t];
 }
 // Both sides in one launch (sides: bit 0 left, bit 1 right).
+// MIN of the peers' dt into this rank's slot (exchange_dt, in-process group)
+__global__ void hf2d_fold_dt(DevScalars* sc, int slot, const double* dt_recv, int nranks, int rank) {
+  if (threadIdx.x != 0) return;
+  double m = bits_to_d(sc->dt_bits[slot]);
+  for (int q = 0; q < nranks; q++)
+    if (q != rank) m = fmin(m, dt_recv[q]);
+  sc->dt_bits[slot] = d_to_bits(m);
+}
+
 __global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, real* bufR, int sides) {
   const int cnt = L.nf * ny;
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1353,6 +1372,10 @@ std::shared_ptr<LocalGroup> make_local_group(int n) { return std::make_shared<Lo
 struct DeviceSolver::Impl {
   DevBuf mem;
   hipStream_t stream = nullptr;
+  // comm overlap: the halo of the edge tiles travels on comm_stream while the
+  // interior tiles compute on `stream` (events ev_edge / ev_halo join them)
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t ev_edge = nullptr, ev_halo = nullptr;
   // device arrays (same roles as HostArrays)
   real *S[2], *A[2], *B[2], *F, *Src, *SrcAdd, *beta, *dSdx[2], *dSdy[2];
   real *U[2], *V[2], *Tg[2], *p, *kk, *R, *CP, *lam, *mu, *mu_t, *lam_t, *Diff, *Y;
@@ -1629,6 +1652,10 @@ DeviceSolver::~DeviceSolver() {
     if (impl->comm) ncclCommDestroy(impl->comm);
     if (impl->sc_host) (void)hipHostFree(impl->sc_host);
     if (impl->res_host) (void)hipHostFree(impl->res_host);
+    if (impl->comm_stream) (void)hipStreamSynchronize(impl->comm_stream);
+    if (impl->ev_edge) (void)hipEventDestroy(impl->ev_edge);
+    if (impl->ev_halo) (void)hipEventDestroy(impl->ev_halo);
+    if (impl->comm_stream) (void)hipStreamDestroy(impl->comm_stream);
     if (impl->stream) (void)hipStreamDestroy(impl->stream);
   }
 }
@@ -2189,7 +2216,7 @@ void DeviceSolver::halo_fields(int group, std::vector<real*>& f) const {
   }
 }
 
-void DeviceSolver::exchange(int group, int dt_slot) {
+void DeviceSolver::exchange(int group, int dt_slot, void* on_stream) {
   Impl& m = *impl;
   p2p_complete();
   if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
@@ -2205,6 +2232,7 @@ void DeviceSolver::exchange(int group, int dt_slot) {
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   const int sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
+  hipStream_t st = on_stream ? (hipStream_t)on_stream : m.stream;
   if (m.p2p.on) {
     if (L.nf * ny > m.halo_cap) throw std::runtime_error("p2p halo exceeds mailbox capacity");
     Impl::P2P& p = m.p2p;
@@ -2235,13 +2263,13 @@ void DeviceSolver::exchange(int group, int dt_slot) {
     HIP_CHECK(hipGetLastError());
     return;
   }
-  hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, m.stream, L, first, last, ny, m.halo_send[0],
+  hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, st, L, first, last, ny, m.halo_send[0],
                      m.halo_send[1], sides);
   const bool gather_dt = dt_slot >= 0;
   unsigned long long* my_dt = gather_dt ? &m.sc->dt_bits[dt_slot] : nullptr;
   if (m.local) {
     LocalGroup& g = *m.local;
-    HIP_CHECK(hipStreamSynchronize(m.stream));
+    HIP_CHECK(hipStreamSynchronize(st));
     g.send_l[m.rank] = m.halo_send[0];
     g.send_r[m.rank] = m.halo_send[1];
     g.dt_src[m.rank] = my_dt;
@@ -2249,34 +2277,34 @@ void DeviceSolver::exchange(int group, int dt_slot) {
     if (gather_dt)
       for (int q = 0; q < m.nranks; q++)
         if (q != m.rank)
-          HIP_CHECK(hipMemcpyAsync(m.dt_recv + q, g.dt_src[q], sizeof(double), hipMemcpyDeviceToDevice, m.stream));
+          HIP_CHECK(hipMemcpyAsync(m.dt_recv + q, g.dt_src[q], sizeof(double), hipMemcpyDeviceToDevice, st));
     if (has_left)
       HIP_CHECK(hipMemcpyAsync(m.halo_recv[0], g.send_r[m.rank - 1], (size_t)cnt * sizeof(real),
-                               hipMemcpyDeviceToDevice, m.stream));
+                               hipMemcpyDeviceToDevice, st));
     if (has_right)
       HIP_CHECK(hipMemcpyAsync(m.halo_recv[1], g.send_l[m.rank + 1], (size_t)cnt * sizeof(real),
-                               hipMemcpyDeviceToDevice, m.stream));
-    HIP_CHECK(hipStreamSynchronize(m.stream));
+                               hipMemcpyDeviceToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
     g.barrier();
   } else {
   NCCL_CHECK(ncclGroupStart());
   if (has_left) {
-    NCCL_CHECK(ncclSend(m.halo_send[0], cnt, ncclDouble, m.rank - 1, m.comm, m.stream));
-    NCCL_CHECK(ncclRecv(m.halo_recv[0], cnt, ncclDouble, m.rank - 1, m.comm, m.stream));
+    NCCL_CHECK(ncclSend(m.halo_send[0], cnt, ncclDouble, m.rank - 1, m.comm, st));
+    NCCL_CHECK(ncclRecv(m.halo_recv[0], cnt, ncclDouble, m.rank - 1, m.comm, st));
   }
   if (has_right) {
-    NCCL_CHECK(ncclSend(m.halo_send[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
-    NCCL_CHECK(ncclRecv(m.halo_recv[1], cnt, ncclDouble, m.rank + 1, m.comm, m.stream));
+    NCCL_CHECK(ncclSend(m.halo_send[1], cnt, ncclDouble, m.rank + 1, m.comm, st));
+    NCCL_CHECK(ncclRecv(m.halo_recv[1], cnt, ncclDouble, m.rank + 1, m.comm, st));
   }
   if (gather_dt)
     for (int q = 0; q < m.nranks; q++)
       if (q != m.rank) {
-        NCCL_CHECK(ncclSend(my_dt, 1, ncclDouble, q, m.comm, m.stream));
-        NCCL_CHECK(ncclRecv(m.dt_recv + q, 1, ncclDouble, q, m.comm, m.stream));
+        NCCL_CHECK(ncclSend(my_dt, 1, ncclDouble, q, m.comm, st));
+        NCCL_CHECK(ncclRecv(m.dt_recv + q, 1, ncclDouble, q, m.comm, st));
       }
   NCCL_CHECK(ncclGroupEnd());
   }
-  hipLaunchKernelGGL(hf2d_unpack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, m.stream, L, 0, h.nx - 1, ny,
+  hipLaunchKernelGGL(hf2d_unpack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, st, L, 0, h.nx - 1, ny,
                      m.halo_recv[0], m.halo_recv[1], sides, m.sc, gather_dt ? dt_slot : 0, m.dt_recv,
                      gather_dt ? m.nranks : 0, m.rank);
   HIP_CHECK(hipGetLastError());
@@ -2387,6 +2415,31 @@ void DeviceSolver::p2p_fallback() {
   p2p_set(false);
   exchange(CpuSolver::HALO_STATE, -1);
   HIP_CHECK(hipStreamSynchronize(impl->stream));
+}
+
+// The global dt MIN alone (comm-overlap steps exchange the halo before the
+// interior tiles have produced their dt): RCCL all-reduce (MIN) on the IEEE
+// bits of the positive doubles, or the in-process group's device copies.
+void DeviceSolver::exchange_dt(int dt_slot) {
+  Impl& m = *impl;
+  if (m.nranks <= 1) return;
+  unsigned long long* my_dt = &m.sc->dt_bits[dt_slot];
+  if (m.comm) {
+    NCCL_CHECK(ncclAllReduce(my_dt, my_dt, 1, ncclUint64, ncclMin, m.comm, m.stream));
+    return;
+  }
+  if (!m.local) throw std::runtime_error("exchange_dt: no transport");
+  LocalGroup& g = *m.local;
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  g.dt_src[m.rank] = my_dt;
+  g.barrier();
+  for (int q = 0; q < m.nranks; q++)
+    if (q != m.rank)
+      HIP_CHECK(hipMemcpyAsync(m.dt_recv + q, g.dt_src[q], sizeof(double), hipMemcpyDeviceToDevice, m.stream));
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  g.barrier();
+  hipLaunchKernelGGL(hf2d_fold_dt, dim3(1), dim3(64), 0, m.stream, m.sc, dt_slot, m.dt_recv, m.nranks, m.rank);
+  HIP_CHECK(hipGetLastError());
 }
 
 FusedX DeviceSolver::fused_args() const {
@@ -2808,6 +2861,64 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
+    // RCCL / in-process transports: edge tiles first, their halo on the comm
+    // stream while the interior tiles compute, then the dt MIN
+    // (the decision must be the same on every rank -- the exchange sequence
+    // differs -- so a strip too narrow to split runs all its tiles at once)
+    const bool split = comm_overlap && !fx_step && !m.p2p.on && (m.comm || m.local) && m.nranks > 1 &&
+                       !want_res && !out && !tile_trace && lean_occ == 0;
+    if (split) {
+      if (!m.comm_stream) {
+        HIP_CHECK(hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&m.ev_halo, hipEventDisableTiming));
+      }
+      const bool parts = T.nbi >= 3;
+      const unsigned ne = parts ? (unsigned)(2 * T.nbj) : ntile, ni = parts ? (unsigned)((T.nbi - 2) * T.nbj) : 0u;
+#define HF2D_PART(G, C, PART, NB)                                                                               \
+  hipLaunchKernelGGL((hf2d_lean_tile<false, false, G, 0, C>), dim3(NB), dim3(BLOCK), shmem, st, P, L, T, m.sc,  \
+                     slot, slot_next, serial, m.partials, PART)
+      const int p1 = parts ? 1 : 0;
+      if (sg && cpt == 2) HF2D_PART(true, 2, p1, ne);
+      else if (sg) HF2D_PART(true, 1, p1, ne);
+      else if (cpt == 2) HF2D_PART(false, 2, p1, ne);
+      else HF2D_PART(false, 1, p1, ne);
+      HIP_CHECK(hipGetLastError());
+      sbuf = 1 - sbuf;   // the new state is this step's output arrays
+      dsbuf = 1 - dsbuf;
+      pbuf = 1 - pbuf;
+      HIP_CHECK(hipEventRecord(m.ev_edge, st));
+      // interior tiles in flight before the (possibly host-blocking) exchange
+      // is issued; they write neither the edge columns nor the ghost columns
+      if (ni > 0) {
+        if (sg && cpt == 2) HF2D_PART(true, 2, 2, ni);
+        else if (sg) HF2D_PART(true, 1, 2, ni);
+        else if (cpt == 2) HF2D_PART(false, 2, 2, ni);
+        else HF2D_PART(false, 1, 2, ni);
+      }
+#undef HF2D_PART
+      HIP_CHECK(hipGetLastError());
+      if (m.local) {
+        // in-process group: the host orders the two streams (waits on it).
+        // Device-side cross-stream waits would put barrier packets in hardware
+        // queues that several virtual ranks' streams share, and a wait cycle
+        // across those queues can deadlock.
+        HIP_CHECK(hipEventSynchronize(m.ev_edge));
+        exchange(CpuSolver::HALO_LEAN, -1, (void*)m.comm_stream);
+        HIP_CHECK(hipStreamSynchronize(m.comm_stream));
+      } else {
+        HIP_CHECK(hipStreamWaitEvent(m.comm_stream, m.ev_edge, 0));
+        exchange(CpuSolver::HALO_LEAN, -1, (void*)m.comm_stream);
+        HIP_CHECK(hipEventRecord(m.ev_halo, m.comm_stream));
+        HIP_CHECK(hipStreamWaitEvent(st, m.ev_halo, 0));
+      }
+      exchange_dt(slot_next);
+      overlap_steps++;
+      nstep++;
+      StepResult r;
+      r.async = true;
+      return r;
+    }
 #define HF2D_LEAN_TILE(R, O, G, C)                                                                                 \
   do {                                                                                                               \
     if (tile_trace && !R && !O && !fx_step)                                                                          \

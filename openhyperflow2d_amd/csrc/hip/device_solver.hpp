@@ -100,7 +100,12 @@ class DeviceSolver : public SolverBase {
   void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import
   int comm_rank() const;
   int comm_size() const;
-  void exchange(int group, int dt_slot = -1);
+  void exchange(int group, int dt_slot = -1, void* on_stream = nullptr);
+  void exchange_dt(int dt_slot);
+  // RCCL / in-process transports: halo of the edge tiles on a comm stream while
+  // the interior tiles compute, then the dt MIN (lean tile steps)
+  bool comm_overlap = true;
+  long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
   void halo_fields(int group, std::vector<real*>& f) const;
   // p2p self-validation (collective over the strip ranks, before the first

@@ -124,7 +124,8 @@ def test_lean_bitwise_with_switches(gpu):
     np.testing.assert_array_equal(rg, rc)
 
 
-def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False, corrupt=False):
+def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False, corrupt=False,
+                   stats=None):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
     host thread each, halos through the in-process LocalGroup transport (or,
     p2p=True, the device-side mailbox transport: one exchange kernel per step,
@@ -199,6 +200,8 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
         assert not any(t.is_alive() for t in th), "virtual-rank step hung"
     if p2p:
         assert all(s.graph_launches > 0 for s in solvers) or max(n for n, _ in schedule) < 12
+    if stats is not None:
+        stats["overlap_steps"] = [s.overlap_steps for s in solvers]
     out = {}
     for f in FIELDS:
         full = None
@@ -220,6 +223,23 @@ def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
     schedule = [(5, True), (6, False), (5, True)]
     got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean)
     ref = gpu.Simulation(text, "gpu", lean=lean)
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def test_comm_overlap_split_step_matches_single_gpu(gpu):
+    """Host-transport strips (the RCCL fallback's structure): edge tiles first,
+    their halo on a comm stream while the interior tiles compute, then the dt
+    MIN -- bitwise equal to one GPU, and the split path really ran."""
+    text = decks.wedge15(480, 60, nmax=10 ** 6, nout=10 ** 5)
+    schedule = [(5, True), (16, False), (5, True)]
+    stats = {}
+    got, summ = _virtual_ranks(gpu, text, 3, schedule, lean=True, stats=stats)
+    assert min(stats["overlap_steps"]) > 0, stats
+    ref = gpu.Simulation(text, "gpu", lean=True)
     for n, res in schedule:
         ref.step(n, residual=res)
     assert summ["dt"] == ref.summary()["dt"]
