@@ -588,6 +588,11 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
       .def_readwrite("comm_overlap", &DeviceSolver::comm_overlap)
+      .def_readwrite("lean_ns", &DeviceSolver::lean_ns)
+      .def_readonly("lns_ok", &DeviceSolver::lns_ok)
+      .def_readonly("lns_why", &DeviceSolver::lns_why)
+      .def_readonly("lns_state", &DeviceSolver::lns_state)
+      .def_readonly("lns_steps", &DeviceSolver::lns_steps)
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
       .def_readwrite("persist_steps", &DeviceSolver::persist_steps)
       .def_readonly("persist_launches", &DeviceSolver::persist_launches)

@@ -358,7 +358,10 @@ struct RefMix {
   HF_HD void heat_flux(const N&, real&, real&) const {}
 };
 
-template <class N, class MX = RefMix>
+// TURB = false: the caller guarantees that no node carries a turbulence-model
+// bit (SK_SGL, lean.cpp sk_eligible), so turb_model() is a no-op and is not
+// compiled in (its Spalart-Allmaras branch alone put the node in scratch).
+template <class N, class MX = RefMix, bool TURB = true>
 HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (has_all(n.CT, CT_SOLID)) return false;
   if (n.S[I_RHO] == 0) return false;
@@ -385,7 +388,7 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
     } else if (P.is_init) {
       n.mu_t = n.lam_t = 0.;
     }
-    if (n.TurbType > 0) turb_model(n, P, P.is_mu_t, P.is_init);
+    if (TURB && n.TurbType > 0) turb_model(n, P, P.is_mu_t, P.is_init);
   }
 
   if (!MX::MECH) {

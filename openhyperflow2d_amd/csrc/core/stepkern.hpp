@@ -17,6 +17,7 @@
 
 #include "physics.hpp"
 #include "mechanism.hpp"
+#include "mechanism_io.hpp"
 #include "residual.hpp"
 
 namespace hf2d {
@@ -535,28 +536,89 @@ struct MechMix {
   }
 };
 
-template <int MODE = SK_GENERIC, int NSB = 1>
-HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
-                            int* neg_T, bool store_grad) {
-  const long N = sin.N;
-  const long idx = (long)i * P.ny + j;
-  const u64 CT = sin.CT[idx];
+// Input accessor of fill_compute() over the split stepper's SoA arrays:
+// `sin` the committed state (and the per-cell fields of the last fill),
+// `pold` the previous fill's primitives.  Neighbour reads go through the
+// direction codes ND_* after set_nb() (a missing neighbour resolves to the
+// cell itself).  The lean N-S kernel (lean_ns.hpp) supplies the same values
+// from its own buffers / LDS, so both paths run the same arithmetic.
+enum { ND_L = 0, ND_R, ND_U, ND_D };
+struct FillSoAIO {
+  const SoA& sin;
+  const SoA& pold;
+  long N, idx, nbi[4];
+  HF_HD FillSoAIO(const SoA& s, const SoA& po, long i) : sin(s), pold(po), N(s.N), idx(i), nbi{i, i, i, i} {}
+  HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
+    nbi[ND_L] = (long)(i - n1) * ny + j;
+    nbi[ND_R] = (long)(i + n2) * ny + j;
+    nbi[ND_U] = idx + n3;
+    nbi[ND_D] = idx - n4;
+  }
+  HF_HD u64 CT() const { return sin.CT[idx]; }
+  HF_HD u64 TT() const { return sin.TT[idx]; }
+  HF_HD uint8_t gf() const { return sin.gf ? sin.gf[idx] : (uint8_t)0xff; }
+  HF_HD uint8_t nb() const { return sin.nb[idx]; }
+  HF_HD bool inplace(const SoA& out) const { return sin.A == out.A && sin.B == out.B && sin.F == out.F; }
+  HF_HD real S(int k) const { return sin.S[k * N + idx]; }
+  HF_HD real Sn(int k, int d) const { return sin.S[k * N + nbi[d]]; }
+  HF_HD real A(int k) const { return sin.A[k * N + idx]; }
+  HF_HD real B(int k) const { return sin.B[k * N + idx]; }
+  HF_HD real F(int k) const { return sin.F[k * N + idx]; }
+  HF_HD real Src(int k) const { return sin.Src[k * N + idx]; }
+  HF_HD real SrcAdd(int k) const { return sin.SrcAdd[k * N + idx]; }
+  HF_HD real Uo() const { return pold.U[idx]; }
+  HF_HD real Vo() const { return pold.V[idx]; }
+  HF_HD real To() const { return pold.Tg[idx]; }
+  HF_HD real Uon(int d) const { return pold.U[nbi[d]]; }
+  HF_HD real Von(int d) const { return pold.V[nbi[d]]; }
+  HF_HD real Ton(int d) const { return pold.Tg[nbi[d]]; }
+  HF_HD real p() const { return sin.p[idx]; }
+  HF_HD real kk() const { return sin.kk[idx]; }
+  HF_HD real R() const { return sin.R[idx]; }
+  HF_HD real CP() const { return sin.CP[idx]; }
+  HF_HD real lam() const { return sin.lam[idx]; }
+  HF_HD real mu() const { return sin.mu[idx]; }
+  HF_HD real Diff() const { return sin.Diff[idx]; }
+  HF_HD real mu_t() const { return sin.mu_t[idx]; }
+  HF_HD real lam_t() const { return sin.lam_t[idx]; }
+  HF_HD real l_min() const { return sin.l_min[idx]; }
+  HF_HD real y_plus() const { return sin.y_plus[idx]; }
+  HF_HD real Re_local() const { return sin.Re_local[idx]; }
+  HF_HD real BGX() const { return sin.BGX[idx]; }
+  HF_HD real BGY() const { return sin.BGY[idx]; }
+  HF_HD real Tf() const { return sin.Tf[idx]; }
+  HF_HD real Y(int s) const { return sin.Y[s * N + idx]; }
+  HF_HD real grad(int g) const { return sin.grad[g * N + idx]; }
+  HF_HD real Ys(int s) const { return sin.Ys[(long)s * N + idx]; }
+  HF_HD real Ysn(int s, int d) const { return sin.Ys[(long)s * N + nbi[d]]; }
+};
+
+// Gradients + FillNode2D + dt + chemistry of one cell into the register node
+// `c` (no stores).  Returns the local dt (1.0 when the cell does not limit
+// dt); *early: solid / unset node (only S is carried); *filled: fill_node()
+// did not skip the node.  `inplace`: the fluxes are updated in place, so
+// those of the flow and species equations need not be loaded (fill_node
+// rewrites them on every node it does not skip).
+template <int MODE, int NSB, class IO>
+HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* mY, real* mgx, real* mgy,
+                               const MechData* mech, int nsp, int i, int j, bool inplace, int* neg_T,
+                               bool* early, bool* filled_out) {
+  const u64 CT = io.CT();
   constexpr bool MECH = MODE == SK_MECH;
   constexpr bool SGL = MODE == SK_SGL, SG = MODE == SK_SGL || MODE == SK_SGT;
-  CellLocal c;
-  for (int k = 0; k < NEQ; k++) c.S[k] = sk_live(MODE, k) ? sin.S[k * N + idx] : 0.0;
+  for (int k = 0; k < NEQ; k++) c.S[k] = sk_live(MODE, k) ? io.S(k) : 0.0;
+  *early = false;
+  *filled_out = false;
   if (has_all(CT, CT_SOLID) || !has_all(CT, CT_NODE_IS_SET)) {
-    for (int k = 0; k < NEQ; k++)
-      if (sk_live(MODE, k)) out.S[k * N + idx] = c.S[k];
+    *early = true;
     return 1.0;
   }
   const bool active = !has_all(CT, NT_FC);
-  const uint8_t gf = sin.gf ? sin.gf[idx] : (uint8_t)0xff;
+  const uint8_t gf = io.gf();
   const bool axi = P.fpa.FT != 0;   // F is only read by the axisymmetric predictor
-  const bool inplace = sin.A == out.A && sin.B == out.B && sin.F == out.F;
   const bool ns = P.sm == SM_NS;    // turbulence sources live in Src[I_K], Src[I_EPS]
   c.CT = CT;
-  c.TurbType = sin.TT[idx];
+  c.TurbType = io.TT();
   for (int k = 0; k < NEQ; k++) {
     const bool ld = sk_live(MODE, k);
     // fill_node() rewrites A, B (and F) of the flow and species equations of
@@ -564,95 +626,92 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     // are not updated in place (fused Euler ping-pong); a skipped node keeps
     // the stored ones (see the store below)
     const bool fld = ld && (!inplace || k >= 4 + NCOMP);
-    c.A[k] = fld ? sin.A[k * N + idx] : 0.0;
-    c.B[k] = fld ? sin.B[k * N + idx] : 0.0;
-    c.F[k] = (axi && fld) ? sin.F[k * N + idx] : 0.0;
-    c.Src[k] = (ld && ((k >= 4 + NCOMP && ns) || (gf & GF_SRC))) ? sin.Src[k * N + idx] : 0.0;
-    c.SrcAdd[k] = (ld && (gf & GF_SRCADD)) ? sin.SrcAdd[k * N + idx] : 0.0;
+    c.A[k] = fld ? io.A(k) : 0.0;
+    c.B[k] = fld ? io.B(k) : 0.0;
+    c.F[k] = (axi && fld) ? io.F(k) : 0.0;
+    c.Src[k] = (ld && ((k >= 4 + NCOMP && ns) || (gf & GF_SRC))) ? io.Src(k) : 0.0;
+    c.SrcAdd[k] = (ld && (gf & GF_SRCADD)) ? io.SrcAdd(k) : 0.0;
     c.RX[k] = c.RY[k] = 0;
   }
-  c.U = prim_old.U[idx];
-  c.V = prim_old.V[idx];
-  c.Tg = prim_old.Tg[idx];
-  c.p = sin.p[idx];
-  c.k = sin.kk[idx];
-  c.R = sin.R[idx];
-  c.CP = sin.CP[idx];
-  c.lam = sin.lam[idx];
-  c.mu = sin.mu[idx];
+  c.U = io.Uo();
+  c.V = io.Vo();
+  c.Tg = io.To();
+  c.p = io.p();
+  c.k = io.kk();
+  c.R = io.R();
+  c.CP = io.CP();
+  c.lam = io.lam();
+  c.mu = io.mu();
   const bool wall = has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW);
   if (SGL) {   // recomputed before use, zero, or turbulence/chemistry-only
     c.Diff = c.mu_t = c.lam_t = c.l_min = c.y_plus = c.Re_local = c.Tf = 0.0;
-    c.BGX = wall ? sin.BGX[idx] : 0.0;
-    c.BGY = wall ? sin.BGY[idx] : 0.0;
+    c.BGX = wall ? io.BGX() : 0.0;
+    c.BGY = wall ? io.BGY() : 0.0;
   } else {
-    c.Diff = sin.Diff[idx];
-    c.mu_t = sin.mu_t[idx];
-    c.lam_t = sin.lam_t[idx];
-    c.l_min = sin.l_min[idx];
-    c.y_plus = sin.y_plus[idx];
-    c.Re_local = sin.Re_local[idx];
-    c.BGX = sin.BGX[idx];
-    c.BGY = sin.BGY[idx];
-    c.Tf = sin.Tf[idx];
+    c.Diff = io.Diff();
+    c.mu_t = io.mu_t();
+    c.lam_t = io.lam_t();
+    c.l_min = io.l_min();
+    c.y_plus = io.y_plus();
+    c.Re_local = io.Re_local();
+    c.BGX = io.BGX();
+    c.BGY = io.BGY();
+    c.Tf = io.Tf();
   }
   c.Uw = c.Vw = 0;
   c.y = (j + 0.5) * P.dy;
   for (int s = 0; s < NSPEC; s++) {
-    c.Y[s] = SG ? (s == NCOMP ? 1.0 : 0.0) : sin.Y[s * N + idx];
+    c.Y[s] = SG ? (s == NCOMP ? 1.0 : 0.0) : io.Y(s);
     c.droYdx[s] = c.droYdy[s] = 0;
   }
   // mechanism species: mass fractions and d(rho Y_s)/dx,y (active viscous nodes)
-  real mY[MECH ? NSB : 1], mgx[MECH ? NSB : 1], mgy[MECH ? NSB : 1];
   if (MECH) {
     const real rho = c.S[I_RHO];
 #pragma unroll
     for (int s = 0; s < (MECH ? NSB : 1); s++) {
-      mY[s] = (s < sin.nsp && rho != 0) ? sin.Ys[(long)s * N + idx] / rho : 0.0;
+      mY[s] = (s < nsp && rho != 0) ? io.Ys(s) / rho : 0.0;
       mgx[s] = mgy[s] = 0.0;
     }
   }
   if (!(active && ns)) {   // velocity/temperature gradients are recomputed below for active viscous nodes
-    c.dUdx = sin.grad[G_DUDX * N + idx];
-    c.dUdy = sin.grad[G_DUDY * N + idx];
-    c.dVdx = sin.grad[G_DVDX * N + idx];
-    c.dVdy = sin.grad[G_DVDY * N + idx];
-    c.dTdx = sin.grad[G_DTDX * N + idx];
-    c.dTdy = sin.grad[G_DTDY * N + idx];
+    c.dUdx = io.grad(G_DUDX);
+    c.dUdy = io.grad(G_DUDY);
+    c.dVdx = io.grad(G_DVDX);
+    c.dVdy = io.grad(G_DVDY);
+    c.dTdx = io.grad(G_DTDX);
+    c.dTdy = io.grad(G_DTDY);
   }
   if (SGL) {
     c.dkdx = c.dkdy = c.depsdx = c.depsdy = 0.0;
   } else {
-    c.dkdx = sin.grad[G_DKDX * N + idx];
-    c.dkdy = sin.grad[G_DKDY * N + idx];
-    c.depsdx = sin.grad[G_DEDX * N + idx];
-    c.depsdy = sin.grad[G_DEDY * N + idx];
+    c.dkdx = io.grad(G_DKDX);
+    c.dkdy = io.grad(G_DKDY);
+    c.depsdx = io.grad(G_DEDX);
+    c.depsdy = io.grad(G_DEDY);
   }
 
   if (active && P.sm == SM_NS) {
-    const uint8_t nbm = sin.nb[idx];
+    const uint8_t nbm = io.nb();
     const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
     const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-    const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j;
-    const long iU = idx + n3, iD = idx - n4;
+    io.set_nb(i, j, P.ny, n1, n2, n3, n4);
     const real dx_1_n = (1.0 / P.dx) / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
     const real dy_1_m = (1.0 / P.dy) / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
-    real aR = sin.S[iR], aL = sin.S[iL], aU = sin.S[iU], aD = sin.S[iD];
+    real aR = io.Sn(0, ND_R), aL = io.Sn(0, ND_L), aU = io.Sn(0, ND_U), aD = io.Sn(0, ND_D);
     c.droYdx[NCOMP] = c.droYdy[NCOMP] = 0.;
     const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
     // SGL: species partial densities are +0, so aR - 0 - 0 - 0 == aR and the
     // species gradients are (0 - 0) * d == +0
     for (int k = 4; k < ((SG || MECH) ? 4 : 4 + NCOMP); k++) {
-      const long o = k * N;
       if (!nx0) {
-        c.droYdx[k - 4] = (sin.S[o + iR] - sin.S[o + iL]) * dx_1_n;
-        aR -= sin.S[o + iR];
-        aL -= sin.S[o + iL];
+        c.droYdx[k - 4] = (io.Sn(k, ND_R) - io.Sn(k, ND_L)) * dx_1_n;
+        aR -= io.Sn(k, ND_R);
+        aL -= io.Sn(k, ND_L);
       }
       if (!ny0) {
-        c.droYdy[k - 4] = (sin.S[o + iU] - sin.S[o + iD]) * dy_1_m;
-        aU -= sin.S[o + iU];
-        aD -= sin.S[o + iD];
+        c.droYdy[k - 4] = (io.Sn(k, ND_U) - io.Sn(k, ND_D)) * dy_1_m;
+        aU -= io.Sn(k, ND_U);
+        aD -= io.Sn(k, ND_D);
       }
     }
     if (!nx0) c.droYdx[NCOMP] = (aR - aL) * dx_1_n;
@@ -660,47 +719,43 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     if (MECH) {
 #pragma unroll
       for (int s = 0; s < (MECH ? NSB : 1); s++) {
-        if (s >= sin.nsp) break;
-        const long o = (long)s * N;
-        if (!nx0) mgx[s] = (sin.Ys[o + iR] - sin.Ys[o + iL]) * dx_1_n;
-        if (!ny0) mgy[s] = (sin.Ys[o + iU] - sin.Ys[o + iD]) * dy_1_m;
+        if (s >= nsp) break;
+        if (!nx0) mgx[s] = (io.Ysn(s, ND_R) - io.Ysn(s, ND_L)) * dx_1_n;
+        if (!ny0) mgy[s] = (io.Ysn(s, ND_U) - io.Ysn(s, ND_D)) * dy_1_m;
       }
     }
-    const real* Uo = prim_old.U;
-    const real* Vo = prim_old.V;
     const real rho = c.S[I_RHO];
-    const long oK = (long)I_K * N, oE = (long)I_EPS * N;
     if (has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW)) {
-      c.dUdx = (Uo[iR] * n1 - Uo[iL] * n2) * dx_1_n;
-      c.dVdx = (Vo[iR] * n1 - Vo[iL] * n2) * dx_1_n;
-      c.dUdy = (Uo[iU] * n3 - Uo[iD] * n4) * dy_1_m;
-      c.dVdy = (Vo[iU] * n3 - Vo[iD] * n4) * dy_1_m;
+      c.dUdx = (io.Uon(ND_R) * n1 - io.Uon(ND_L) * n2) * dx_1_n;
+      c.dVdx = (io.Von(ND_R) * n1 - io.Von(ND_L) * n2) * dx_1_n;
+      c.dUdy = (io.Uon(ND_U) * n3 - io.Uon(ND_D) * n4) * dy_1_m;
+      c.dVdy = (io.Von(ND_U) * n3 - io.Von(ND_D) * n4) * dy_1_m;
       if (is_two_eq(c.TurbType)) {
-        c.dkdx = (sin.S[oK + iR] * n1 - sin.S[oK + iL] * n2) * dx_1_n / rho;
-        c.depsdx = (sin.S[oE + iR] * n1 - sin.S[oE + iL] * n2) * dx_1_n / rho;
-        c.dkdy = (sin.S[oK + iU] * n3 - sin.S[oK + iD] * n4) * dy_1_m / rho;
-        c.depsdy = (sin.S[oE + iU] * n3 - sin.S[oE + iD] * n4) * dy_1_m / rho;
+        c.dkdx = (io.Sn(I_K, ND_R) * n1 - io.Sn(I_K, ND_L) * n2) * dx_1_n / rho;
+        c.depsdx = (io.Sn(I_EPS, ND_R) * n1 - io.Sn(I_EPS, ND_L) * n2) * dx_1_n / rho;
+        c.dkdy = (io.Sn(I_K, ND_U) * n3 - io.Sn(I_K, ND_D) * n4) * dy_1_m / rho;
+        c.depsdy = (io.Sn(I_EPS, ND_U) * n3 - io.Sn(I_EPS, ND_D) * n4) * dy_1_m / rho;
       } else if (has_all(c.TurbType, TCT_Spalart_Allmaras_Model)) {
-        c.dkdx = (sin.S[oK + iR] * n1 - sin.S[oK + iL] * n2) * dx_1_n / rho;
-        c.dkdy = (sin.S[oK + iU] * n3 - sin.S[oK + iD] * n4) * dy_1_m / rho;
+        c.dkdx = (io.Sn(I_K, ND_R) * n1 - io.Sn(I_K, ND_L) * n2) * dx_1_n / rho;
+        c.dkdy = (io.Sn(I_K, ND_U) * n3 - io.Sn(I_K, ND_D) * n4) * dy_1_m / rho;
       }
     } else {
-      c.dUdx = (Uo[iR] - Uo[iL]) * dx_1_n;
-      c.dVdx = (Vo[iR] - Vo[iL]) * dx_1_n;
-      c.dUdy = (Uo[iU] - Uo[iD]) * dy_1_m;
-      c.dVdy = (Vo[iU] - Vo[iD]) * dy_1_m;
+      c.dUdx = (io.Uon(ND_R) - io.Uon(ND_L)) * dx_1_n;
+      c.dVdx = (io.Von(ND_R) - io.Von(ND_L)) * dx_1_n;
+      c.dUdy = (io.Uon(ND_U) - io.Uon(ND_D)) * dy_1_m;
+      c.dVdy = (io.Von(ND_U) - io.Von(ND_D)) * dy_1_m;
       if (is_two_eq(c.TurbType)) {
-        c.dkdx = (sin.S[oK + iR] - sin.S[oK + iL]) * dx_1_n / rho;
-        c.depsdx = (sin.S[oE + iR] - sin.S[oE + iL]) * dx_1_n / rho;
-        c.dkdy = (sin.S[oK + iU] - sin.S[oK + iD]) * dy_1_m / rho;
-        c.depsdy = (sin.S[oE + iU] - sin.S[oE + iD]) * dy_1_m / rho;
+        c.dkdx = (io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n / rho;
+        c.depsdx = (io.Sn(I_EPS, ND_R) - io.Sn(I_EPS, ND_L)) * dx_1_n / rho;
+        c.dkdy = (io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m / rho;
+        c.depsdy = (io.Sn(I_EPS, ND_U) - io.Sn(I_EPS, ND_D)) * dy_1_m / rho;
       } else if (has_all(c.TurbType, TCT_Spalart_Allmaras_Model)) {
-        c.dkdx = (sin.S[oK + iR] - sin.S[oK + iL]) * dx_1_n / rho;
-        c.dkdy = (sin.S[oK + iU] - sin.S[oK + iD]) * dy_1_m / rho;
+        c.dkdx = (io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n / rho;
+        c.dkdy = (io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m / rho;
       }
     }
-    c.dTdx = (prim_old.Tg[iR] - prim_old.Tg[iL]) * dx_1_n;
-    c.dTdy = (prim_old.Tg[iU] - prim_old.Tg[iD]) * dy_1_m;
+    c.dTdx = (io.Ton(ND_R) - io.Ton(ND_L)) * dx_1_n;
+    c.dTdy = (io.Ton(ND_U) - io.Ton(ND_D)) * dy_1_m;
   }
 
   // P.ffc (NT_FC nodes) differs from P.fpa only in is_mu_t / is_init; patch
@@ -714,11 +769,12 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   }
   bool filled;
   if (MECH) {
-    MechMix<NSB> mx{sin.mech, mY, mgx, mgy};
+    MechMix<NSB> mx{mech, mY, mgx, mgy};
     filled = fill_node(c, fp, mx);
   } else {
-    filled = fill_node(c, fp);
+    filled = fill_node<CellLocal, RefMix, MODE != SK_SGL>(c, fp);
   }
+  *filled_out = filled;
 
   real dt_local = 1.0;
   if (active) {
@@ -736,8 +792,8 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
       if (MECH) {
         // mixture transport at the new T (the reference's lagged update) and
         // the Tecplot slot fractions
-        mech_transport<NSB>(*sin.mech, mY, c.Tg, &c.mu, &c.lam);
-        mech_slot_fractions(*sin.mech, mY, c.Y);
+        mech_transport<NSB>(*mech, mY, c.Tg, &c.mu, &c.lam);
+        mech_slot_fractions(*mech, mY, c.Y);
       } else if (SG) {
         if (P.chem_model != NO_REACTIONS) chemistry_single_gas_ns(c, *P.species);
       } else {
@@ -746,6 +802,32 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
       }
     }
   }
+  return dt_local;
+}
+
+template <int MODE = SK_GENERIC, int NSB = 1>
+HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
+                            int* neg_T, bool store_grad) {
+  const long N = sin.N;
+  const long idx = (long)i * P.ny + j;
+  constexpr bool MECH = MODE == SK_MECH;
+  constexpr bool SGL = MODE == SK_SGL, SG = MODE == SK_SGL || MODE == SK_SGT;
+  CellLocal c;
+  real mY[MECH ? NSB : 1], mgx[MECH ? NSB : 1], mgy[MECH ? NSB : 1];
+  FillSoAIO io(sin, prim_old, idx);
+  const bool inplace = io.inplace(out);
+  bool early, filled;
+  const real dt_local =
+      fill_compute<MODE, NSB>(P, io, c, mY, mgx, mgy, sin.mech, sin.nsp, i, j, inplace, neg_T, &early, &filled);
+  if (early) {
+    for (int k = 0; k < NEQ; k++)
+      if (sk_live(MODE, k)) out.S[k * N + idx] = c.S[k];
+    return 1.0;
+  }
+  const uint8_t gf = io.gf();
+  const bool axi = P.fpa.FT != 0;
+  const bool ns = P.sm == SM_NS;
+  const bool active = !has_all(c.CT, NT_FC);
   // SGL: a skipped node (fill_node returned false) keeps its stored fluxes
   for (int k = 0; k < NEQ; k++) {
     if (!sk_live(MODE, k)) continue;

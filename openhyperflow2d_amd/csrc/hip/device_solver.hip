@@ -40,6 +40,7 @@
 #include "dev_common.hpp"
 #include "chem_fast.hpp"
 #include "chem_mech.hpp"
+#include "lean_ns.hpp"
 
 #define HIP_CHECK(x)                                                                             \
   do {                                                                                           \
@@ -182,7 +183,7 @@ __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const S
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    if (slot_next >= 0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));   // < 0: lean N-S materialize
   }
 }
 
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    if (slot_next >= 0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));   // < 0: lean N-S materialize
   }
 }
 
@@ -1108,6 +1109,142 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
   lean_materialize_cell(P, L, g, i, j);
 }
 
+// ---------------------------------------------------------------------------
+// Lean single-gas N-S step (lean_ns.hpp): F_m of the tile + ring into LDS,
+// predict_m from LDS, own-cell part of F_{m+1} for dt_{m+1}.  One workgroup
+// per TI x TJ tile (lean_tile_geom, one cell per thread).
+// ---------------------------------------------------------------------------
+constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
+
+template <bool RES>
+__global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
+                                                        int slot, int slot_next, int serial, ResidualPack* partials) {
+  extern __shared__ real lds[];
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  apply_dt(P, sc, slot);
+  if (b == 0 && threadIdx.x == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += P.dt;
+    scenario_next(P, sc, slot, slot_next);
+  }
+  const int NC = T.NC;
+  int i, j, c, i0, j0;
+  const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
+  int dummy = 0, skip = 0;
+  // 1a. ring cells first (only their S, A, B are kept)
+  const int nring = 2 * (T.TI + T.TJ);
+  if ((int)threadIdx.x < nring) {
+    int ii, jj;
+    lns_ring_cell(T, (int)threadIdx.x, &ii, &jj);
+    const int gi = i0 + ii, gj = j0 + jj;
+    if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
+      CellLocal rc;
+      bool early, filled;
+      lns_fill_to_lds(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
+    }
+  }
+  // 1b. own cell: F_m, its level-m outputs, kept values for 2./3.
+  LnsLevel lv;
+  u64 CT = 0, TT = 0;
+  uint8_t gf = 0, nbm = 0;
+  bool early = true, filled = false;
+  const long N = a.N;
+  const long idx = (long)i * P.ny + j;
+  if (mine) {
+    CellLocal oc;
+    lns_fill_to_lds(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
+    CT = oc.CT;
+    gf = a.gf[idx];
+    nbm = a.nb[idx];
+    TT = a.TT[idx];
+    if (!early) {
+      if (!filled) skip = 1;
+      a.Uo[idx] = oc.U;
+      a.Vo[idx] = oc.V;
+      a.To[idx] = oc.Tg;
+      a.kko[idx] = oc.k;
+      a.CPo[idx] = oc.CP;
+      a.lamo[idx] = oc.lam;
+      a.muo[idx] = oc.mu;
+      if (gf & GF_SRCADD)
+#pragma unroll
+        for (int k = 0; k < LNS_NL; k++) a.SrcAdd[k * N + idx] = oc.SrcAdd[k];
+      lv.U = oc.U;
+      lv.V = oc.V;
+      lv.Tg = oc.Tg;
+      lv.p = oc.p;
+      lv.k = oc.k;
+      lv.R = oc.R;
+      lv.CP = oc.CP;
+      lv.lam = oc.lam;
+      lv.mu = oc.mu;
+      lv.BGX = oc.BGX;
+      lv.BGY = oc.BGY;
+#pragma unroll
+      for (int k = 0; k < LNS_NL; k++) lv.SrcAdd[k] = oc.SrcAdd[k];
+    }
+  }
+  __syncthreads();
+  // 2. predict_m
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+#pragma unroll
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  if (mine) {
+    LnsPredictIO io{a, lds, lv.SrcAdd, N, idx, idx, idx, idx, idx, NC, c, c, c, c, c, gf, {0, 0, 0, 0}};
+    if (!is_active(CT)) {
+#pragma unroll
+      for (int k = 0; k < LNS_NL; k++) {
+        io.sn[k] = io.S(k);
+        io.keep_dS(k);
+      }
+    } else {
+      const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+      const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+      io.iL = (long)(i - n1) * P.ny + j;
+      io.iR = (long)(i + n2) * P.ny + j;
+      io.iU = idx + n3;
+      io.iD = idx - n4;
+      io.cL = c - n1 * T.W;
+      io.cR = c + n2 * T.W;
+      io.cU = c + n3;
+      io.cD = c - n4;
+      predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, r);
+    }
+#pragma unroll
+    for (int k = 0; k < LNS_NL; k++) a.Sp_out[k * N + idx] = io.sn[k];
+    // 3. own-cell part of F_{m+1}: dt_{m+1}
+    if (!early) {
+      LnsOwnIO oio(io.sn, lv, CT, TT, gf, nbm);
+      CellLocal nc;
+      real mY[1], mgx[1], mgy[1];
+      bool e2, f2;
+      dtl = fill_compute<SK_SGL, 1>(P, oio, nc, mY, mgx, mgy, nullptr, 0, i, j, true, &neg, &e2, &f2);
+    }
+  }
+  if (RES) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  if (skip) atomicOr(&sc->neg_T, LNS_SKIP_ERR);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    if (serial) m = fmin(m, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   if (c >= c1) return;
@@ -1385,6 +1522,8 @@ struct DeviceSolver::Impl {
   // lean inviscid state: pre-chemistry species and pressure (ping-pong with
   // U/V on pbuf), per-cell neighbour/publish byte
   real *Spre[2], *P2[2];
+  // lean N-S: second level of CP / mu / lam / k (the first is the generic array)
+  real *CP2 = nullptr, *mu2 = nullptr, *lam2 = nullptr, *kk2 = nullptr;
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   unsigned long long* persist_bar = nullptr;   // grid-barrier counter of hf2d_lean_persist
@@ -1469,6 +1608,50 @@ struct DeviceSolver::Impl {
     L.gB = B[ab];
     L.gF = F;
     return L;
+  }
+
+  // lean N-S kernel arguments: Sp^m in S[1-sb], level m-1 primitives in
+  // U/V/Tg[1-pb] and CPx[1-cb]; K_m writes Sp^{m+1} into S[sb], level m into
+  // U/V/Tg[pb] and CPx[cb] (CPx[0] = the generic arrays)
+  LnsArrays lns_arrays(const HostArrays& h, int sb, int pb, int cb, int db) const {
+    LnsArrays a;
+    a.N = h.N;
+    a.Sp = S[1 - sb];
+    a.Sp_out = S[sb];
+    a.beta = beta;
+    a.Ui = U[1 - pb];
+    a.Vi = V[1 - pb];
+    a.Ti = Tg[1 - pb];
+    a.Uo = U[pb];
+    a.Vo = V[pb];
+    a.To = Tg[pb];
+    real* const cpx[2] = {CP, CP2};
+    real* const mux[2] = {mu, mu2};
+    real* const lamx[2] = {lam, lam2};
+    real* const kkx[2] = {kk, kk2};
+    a.CPi = cpx[1 - cb];
+    a.mui = mux[1 - cb];
+    a.lami = lamx[1 - cb];
+    a.kki = kkx[1 - cb];
+    a.CPo = cpx[cb];
+    a.muo = mux[cb];
+    a.lamo = lamx[cb];
+    a.kko = kkx[cb];
+    a.pi = p;
+    a.R = R;
+    a.BGX = BGX;
+    a.BGY = BGY;
+    a.grad = grad;
+    a.SrcAdd = SrcAdd;
+    a.dSdx_in = dSdx[db];
+    a.dSdy_in = dSdy[db];
+    a.dSdx_out = dSdx[1 - db];
+    a.dSdy_out = dSdy[1 - db];
+    a.CT = CT;
+    a.TT = TT;
+    a.nb = nb;
+    a.gf = gf;
+    return a;
   }
 
   SoA view(const HostArrays& h, int sb, int ab, int db, int pb) const {
@@ -1723,6 +1906,40 @@ void DeviceSolver::upload() {
   lean_ok = lean_eligible(cs, &lean_why);
   sk_mode = sk_eligible(cs, &sgl_why);
   sgl_ok = sk_mode != SK_GENERIC;
+  {
+    // lean N-S (lean_ns.hpp): laminar single gas, flat, adiabatic walls, no
+    // volume sources, every non-solid node set (fluxes of skipped or unset
+    // nodes are not recomputable), one strip (no 2-column halo)
+    auto no = [&](const char* w) {
+      lns_ok = false;
+      lns_why = w;
+    };
+    lns_ok = true;
+    lns_why.clear();
+    if (sk_mode != SK_SGL) no("not single-gas laminar N-S");
+    else if (cs.cfg.FT != FT_FLAT) no("axisymmetric");
+    else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
+    else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
+    else
+      for (long q = 0; q < N && lns_ok; q++) {
+        if (h.gf[q] & GF_SRC) no("volume sources");
+        else if (!has_all(h.CT[q], CT_SOLID) && !has_all(h.CT[q], CT_NODE_IS_SET)) no("unset non-solid node");
+      }
+    if (lns_ok && !m.CP2) {
+      m.CP2 = m.mem.alloc<real>(N);
+      m.mu2 = m.mem.alloc<real>(N);
+      m.lam2 = m.mem.alloc<real>(N);
+      m.kk2 = m.mem.alloc<real>(N);
+    }
+    if (m.CP2) {
+      cp(m.CP2, h.CP.data(), SB);
+      cp(m.mu2, h.mu.data(), SB);
+      cp(m.lam2, h.lam.data(), SB);
+      cp(m.kk2, h.kk.data(), SB);
+    }
+    lns_state = 0;
+    cbuf = 0;
+  }
   lean_sg_ok = lean_ok && lean_single_gas(cs);
   lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
   if (lean_ok) {
@@ -1806,12 +2023,47 @@ void DeviceSolver::lean_materialize() {
   lean_state = 0;
 }
 
+// Lean N-S -> generic record: the split fill F_m over every cell from the
+// lean state (Sp^m, level m-1 primitives), i.e. exactly the fill the split
+// stepper ran (committed S, A/B/F, SrcAdd, level-m primitives, Diff and
+// gradients); its dt is already in the next slot (no dt update here).
+void DeviceSolver::lns_materialize() {
+  p2p_complete();
+  Impl& m = *impl;
+  StepParams P = make_params(last_iter + iter);
+  P.nx = h.nx;
+  P.ny = h.ny;
+  P.i0 = l_off;
+  P.i1 = l_off + (gi1 - gi0);
+  P.gx0 = gi0 - l_off;
+  P.species = m.species;
+  P.scen = m.scen;
+  SoA sin = m.view(h, 1 - sbuf, abuf, dsbuf, 1 - pbuf);
+  real* const cpx[2] = {m.CP, m.CP2};
+  real* const mux[2] = {m.mu, m.mu2};
+  real* const lamx[2] = {m.lam, m.lam2};
+  real* const kkx[2] = {m.kk, m.kk2};
+  sin.CP = cpx[1 - cbuf];
+  sin.mu = mux[1 - cbuf];
+  sin.lam = lamx[1 - cbuf];
+  sin.kk = kkx[1 - cbuf];
+  SoA out = m.view(h, sbuf, abuf, dsbuf, pbuf);
+  const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
+  const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+  hipLaunchKernelGGL((hf2d_fill<SK_SGL, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
+                     (int)(nstep % 3), -1, 0, 1);
+  HIP_CHECK(hipGetLastError());
+  lns_state = 0;
+  cbuf = 0;
+}
+
 void DeviceSolver::download(Field& J) {
   flush_pending();
   p2p_complete();
   HIP_CHECK(hipSetDevice(dev));
   Impl& m = *impl;
   if (lean_state) lean_materialize();
+  if (lns_state) lns_materialize();
   hipStream_t st = m.stream;
   const long N = h.N;
   auto cp = [&](void* d, const void* s, size_t bytes) { HIP_CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, st)); };
@@ -1856,6 +2108,7 @@ void DeviceSolver::sample_monitors(std::vector<MonitorPoint>& mp) {
   flush_pending();
   p2p_complete();
   Impl& m = *impl;
+  if (lns_state) lns_materialize();
   const int n = (int)mp.size();
   std::vector<long> idx(n, -1);
   for (int q = 0; q < n; q++) {
@@ -1897,6 +2150,7 @@ void DeviceSolver::sample_monitors(std::vector<MonitorPoint>& mp) {
 void DeviceSolver::poison_cell(int gi, int j) {
   flush_pending();
   Impl& m = *impl;
+  if (lns_state) lns_materialize();
   const long idx = (long)(gi - gi0 + l_off) * h.ny + j;
   static const real bad = -1.0e30;
   HIP_CHECK(hipMemcpyAsync(m.S[sbuf] + (long)I_RHOE * h.N + idx, &bad, sizeof bad, hipMemcpyHostToDevice, m.stream));
@@ -1924,6 +2178,12 @@ void DeviceSolver::sync_scalars() {
                   last_iter + iter);
     throw std::runtime_error(b);
   }
+  if (err & LNS_SKIP_ERR) {
+    char b[256];
+    std::snprintf(b, sizeof b, "ERROR: lean N-S step: FillNode2D skipped a node (rho = 0 or k < 1) before iteration %ld",
+                  last_iter + iter);
+    throw std::runtime_error(b);
+  }
   if (err & PERSIST_ERR) {
     char b[256];
     std::snprintf(b, sizeof b, "ERROR: persistent step kernel: grid barrier timed out before iteration %ld",
@@ -1942,6 +2202,7 @@ void DeviceSolver::cycle_update() {
   flush_pending();
   p2p_complete();
   Impl& m = *impl;
+  if (lns_state) lns_materialize();
   if (cs.cfg.ProblemType == SM_NS && cs.cfg.semantics != Semantics::SERIAL) {
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);
     const int nw = (int)h.wall_own.size(), nall = (int)cs.wall_nodes.size();
@@ -2684,7 +2945,8 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   Impl& m = *impl;
   // (the in-process host transport synchronises on the host: eager only)
   const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
-                     !(lean && lean_ok && lean_state == 0);
+                     !(lean && lean_ok && lean_state == 0) &&
+                     !(lean_ns && lns_ok && lns_state == 0 && P0.sm == SM_NS);   // lean N-S entry step: eager
   if (plain && persist_eligible()) {
     if (!pending.empty() && !pending_persist) flush_pending();
     pending_persist = true;
@@ -2709,11 +2971,11 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
   const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok));
+                                       lean_cpt, lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok) + 2 * lns_state + 4 * (int)lean_ns);
   bool same = true;
   for (const StepParams& p : pending)
     same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok)) == sig;
+                                   lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok) + 2 * lns_state + 4 * (int)lean_ns) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -2767,6 +3029,99 @@ void DeviceSolver::run_graph() {
   HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
   nstep += GRAPH_STEPS;
   graph_launches++;
+}
+
+// Split predict + fill step (every N-S / mechanism / generic case).
+void DeviceSolver::step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk,
+                              bool to_lns) {
+  Impl& m = *impl;
+  hipStream_t st = m.stream;
+  const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
+    SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
+    SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
+    // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
+    // mechanism mode: SK_MECH (Euler and N-S)
+    const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+#define HF2D_PRED(R, M)                                                                                     \
+  hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
+                     serial, m.partials)
+    if (want_res) {
+      if (mode == SK_SGL) HF2D_PRED(true, SK_SGL);
+      else if (mode == SK_SGT) HF2D_PRED(true, SK_SGT);
+      else if (mode == SK_MECH) HF2D_PRED(true, SK_MECH);
+      else HF2D_PRED(true, SK_GENERIC);
+    } else {
+      if (mode == SK_SGL) HF2D_PRED(false, SK_SGL);
+      else if (mode == SK_SGT) HF2D_PRED(false, SK_SGT);
+      else if (mode == SK_MECH) HF2D_PRED(false, SK_MECH);
+      else HF2D_PRED(false, SK_GENERIC);
+    }
+#undef HF2D_PRED
+    HIP_CHECK(hipGetLastError());
+    const bool multi = (m.comm || m.local || m.p2p.on) && m.nranks > 1;
+    if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
+    SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
+    SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
+    if (to_lns) {   // entering the lean N-S path: level n+1 into the second buffers
+      out.CP = m.CP2;
+      out.mu = m.mu2;
+      out.lam = m.lam2;
+      out.kk = m.kk2;
+    }
+    if (mode == SK_MECH) {
+      // operator-split kinetics: Ys[1-sbuf] -> Ys[sbuf]; N-S strips also react
+      // their ghost columns (exchanged above; same inputs as on the owner)
+      const bool ghosts = multi && P.sm == SM_NS;
+      const long k0 = ghosts ? 0 : c0, k1 = ghosts ? h.N : c1;
+      const unsigned nbk = (unsigned)((k1 - k0 + BLOCK - 1) / BLOCK);
+      launch_chem(P, sin, out, k0, k1, nbk, slot);
+      m.mech_view(sin, sbuf, 1 - dsbuf);   // the fill reads the post-chemistry species
+    }
+    // SGL: gradients / Diff only when the host reads the record (or y+ follows)
+    const int sg_out = (step_outputs || want_res) ? 1 : 0;
+    // register budget: measured on 1x MI355X (tools/fill_occ_sweep.sh): the
+    // mechanism fill is 10 % faster at 2 waves/SIMD (256 VGPRs, a few spills)
+    // than at the compiler's 1; SGL / SGT are fastest at the default
+    const int focc = fill_occ >= 0 ? fill_occ : (mode == SK_MECH ? 2 : 0);
+#define HF2D_FILL(MD, NS, SGO)                                                                                  \
+  do {                                                                                                          \
+    if (focc == 2)                                                                                          \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 2>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else if (focc == 3)                                                                                         \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 3>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else if (focc == 4)                                                                                         \
+      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 4>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
+                         m.sc, slot, slot_next, serial, SGO);                                                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((hf2d_fill<MD, NS>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,  \
+                         slot, slot_next, serial, SGO);                                                        \
+  } while (0)
+    if (mode == SK_MECH) {
+      if (m.nsp <= 9)
+        HF2D_FILL(SK_MECH, 9, 1);
+      else
+        hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
+                           m.sc, slot, slot_next, serial, 1);
+    } else if (mode == SK_SGL)
+      HF2D_FILL(SK_SGL, 1, sg_out);
+    else if (mode == SK_SGT)
+      HF2D_FILL(SK_SGT, 1, 1);
+    else
+      hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
+                         slot_next, serial, 1);
+#undef HF2D_FILL
+    HIP_CHECK(hipGetLastError());
+    dsbuf = 1 - dsbuf;
+    pbuf = 1 - pbuf;
+}
+
+// The lean N-S kernel applies to this step (lean_ns.hpp; eligibility lns_ok)
+bool DeviceSolver::lns_step_ok(const StepParams& P) const {
+  const Impl& m = *impl;
+  return lean_ns && lns_ok && P.sm == SM_NS && sgl && sgl_ok && sk_mode == SK_SGL && !m.mech && m.nranks == 1 &&
+         !m.p2p.on && !P.fpa.is_init && !P.ffc.is_init && P.ny >= LEAN_TILE_MIN_TJ;
 }
 
 StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
@@ -3011,80 +3366,37 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     abuf = 1 - abuf;
     dsbuf = 1 - dsbuf;
     sbuf = 1 - sbuf;
+  } else if (lns_step_ok(P)) {
+    if (lean_state) lean_materialize();
+    if (lns_state == 0) {
+      // first lean N-S step: the split step with the fill's CP/mu/lam/k going
+      // to the second level buffers (the level it read stays for K_{n+1})
+      step_split(P, want_res, slot, slot_next, serial, nblk, true);
+      lns_state = 1;
+      cbuf = 1;
+    } else {
+      const LnsArrays a = m.lns_arrays(h, sbuf, pbuf, cbuf, dsbuf);
+      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 1);
+      const int ntile = T.nbi * T.nbj;
+      const size_t shmem = (size_t)LNS_PLANES * T.NC * sizeof(real);
+      if (want_res)
+        hipLaunchKernelGGL(hf2d_lns_step<true>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
+                           serial, m.partials);
+      else
+        hipLaunchKernelGGL(hf2d_lns_step<false>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
+                           serial, m.partials);
+      HIP_CHECK(hipGetLastError());
+      nres = (unsigned)ntile;
+      sbuf = 1 - sbuf;
+      pbuf = 1 - pbuf;
+      cbuf = 1 - cbuf;
+      dsbuf = 1 - dsbuf;
+      lns_steps++;
+    }
   } else {
     if (lean_state) lean_materialize();
-    SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
-    SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
-    // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
-    // mechanism mode: SK_MECH (Euler and N-S)
-    const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
-#define HF2D_PRED(R, M)                                                                                     \
-  hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
-                     serial, m.partials)
-    if (want_res) {
-      if (mode == SK_SGL) HF2D_PRED(true, SK_SGL);
-      else if (mode == SK_SGT) HF2D_PRED(true, SK_SGT);
-      else if (mode == SK_MECH) HF2D_PRED(true, SK_MECH);
-      else HF2D_PRED(true, SK_GENERIC);
-    } else {
-      if (mode == SK_SGL) HF2D_PRED(false, SK_SGL);
-      else if (mode == SK_SGT) HF2D_PRED(false, SK_SGT);
-      else if (mode == SK_MECH) HF2D_PRED(false, SK_MECH);
-      else HF2D_PRED(false, SK_GENERIC);
-    }
-#undef HF2D_PRED
-    HIP_CHECK(hipGetLastError());
-    const bool multi = (m.comm || m.local || m.p2p.on) && m.nranks > 1;
-    if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
-    SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
-    SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
-    if (mode == SK_MECH) {
-      // operator-split kinetics: Ys[1-sbuf] -> Ys[sbuf]; N-S strips also react
-      // their ghost columns (exchanged above; same inputs as on the owner)
-      const bool ghosts = multi && P.sm == SM_NS;
-      const long k0 = ghosts ? 0 : c0, k1 = ghosts ? h.N : c1;
-      const unsigned nbk = (unsigned)((k1 - k0 + BLOCK - 1) / BLOCK);
-      launch_chem(P, sin, out, k0, k1, nbk, slot);
-      m.mech_view(sin, sbuf, 1 - dsbuf);   // the fill reads the post-chemistry species
-    }
-    // SGL: gradients / Diff only when the host reads the record (or y+ follows)
-    const int sg_out = (step_outputs || want_res) ? 1 : 0;
-    // register budget: measured on 1x MI355X (tools/fill_occ_sweep.sh): the
-    // mechanism fill is 10 % faster at 2 waves/SIMD (256 VGPRs, a few spills)
-    // than at the compiler's 1; SGL / SGT are fastest at the default
-    const int focc = fill_occ >= 0 ? fill_occ : (mode == SK_MECH ? 2 : 0);
-#define HF2D_FILL(MD, NS, SGO)                                                                                  \
-  do {                                                                                                          \
-    if (focc == 2)                                                                                          \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 2>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else if (focc == 3)                                                                                         \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 3>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else if (focc == 4)                                                                                         \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 4>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else                                                                                                        \
-      hipLaunchKernelGGL((hf2d_fill<MD, NS>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,  \
-                         slot, slot_next, serial, SGO);                                                        \
-  } while (0)
-    if (mode == SK_MECH) {
-      if (m.nsp <= 9)
-        HF2D_FILL(SK_MECH, 9, 1);
-      else
-        hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
-                           m.sc, slot, slot_next, serial, 1);
-    } else if (mode == SK_SGL)
-      HF2D_FILL(SK_SGL, 1, sg_out);
-    else if (mode == SK_SGT)
-      HF2D_FILL(SK_SGT, 1, 1);
-    else
-      hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
-                         slot_next, serial, 1);
-#undef HF2D_FILL
-    HIP_CHECK(hipGetLastError());
-    dsbuf = 1 - dsbuf;
-    pbuf = 1 - pbuf;
+    if (lns_state) lns_materialize();
+    step_split(P, want_res, slot, slot_next, serial, nblk, false);
   }
   // new-state halo + global dt (MIN over ranks into the next slot)
   if (fx_step) {

@@ -154,6 +154,16 @@ class DeviceSolver : public SolverBase {
   int fill_occ = -1;      // split fill kernels: -1 auto, 0 compiler default, 2/3/4 waves-per-SIMD register budget
   std::string sgl_why;
   int lean_state = 0;     // 1: lean arrays authoritative (A/B/F/p stale)
+  // Single-gas laminar N-S: one LDS-tiled kernel per step with the fluxes
+  // recomputed in the tile (hip/lean_ns.hpp) when eligible (lns_ok: flat,
+  // SK_SGL, adiabatic walls, no sources; one strip)
+  bool lean_ns = true;
+  bool lns_ok = false;
+  std::string lns_why;
+  int lns_state = 0;      // 1: lean N-S buffers authoritative (committed S, A/B/F, p stale)
+  int cbuf = 0;           // lean N-S: CP/mu/lam/k level ping-pong (0: the generic arrays)
+  long lns_steps = 0;
+  void lns_materialize();
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
   void lean_materialize();
@@ -186,6 +196,8 @@ class DeviceSolver : public SolverBase {
   void run_graph();
   bool persist_eligible() const;
   void run_persist();
+  void step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk, bool to_lns);
+  bool lns_step_ok(const StepParams& P) const;
   // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
   void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };

@@ -1,0 +1,243 @@
+// Lean viscous step (single-gas N-S, SK_SGL): one LDS-tiled kernel per time
+// step instead of the split predict + fill pair, with the fluxes of the
+// step recomputed inside the tile instead of stored.
+//
+// Split stepper (stepkern.hpp), step n:
+//   predict_n   S^n (committed), A^n, B^n (stored by the last fill), dt_n
+//               -> Sp^{n+1} (predicted state), beta
+//   fill_{n+1}  Sp^{n+1}, neighbours' Sp^{n+1} (rho gradient), the previous
+//               fill's primitives P^n (U, V, T gradients; CP, mu, lam, k)
+//               -> committed S^{n+1}, A/B^{n+1}, P^{n+1}, dt_{n+1}
+// The fluxes A/B of every cell are a pure function of Sp and P of that cell
+// and its four neighbours (reference FillNode2D, hyper_flow_node.hpp:373-600,
+// called per cell at deeps2d_core.cpp:1169-1244), so they need not move
+// through memory.  Kernel K_n of this path:
+//   1. F_n (fill_compute, the same function the split fill runs) for the
+//      tile's cells and its one-cell cross-shaped ring, from Sp^n and the
+//      level n-1 primitives in global memory -> committed S^n, A^n, B^n into
+//      LDS; the tile's own cells also store their level-n primitives;
+//   2. predict_n (predict_core) of the tile's cells from LDS -> Sp^{n+1};
+//   3. the own-cell part of F_{n+1} that dt_{n+1} needs (U, V, T, k of the
+//      new state; no neighbours) -> dt_{n+1}.
+// Persistent state per cell: Sp (4), beta (4), U/V/T and CP/mu/lam/k at two
+// levels (ping-pong), i.e. ~270 B of HBM traffic per cell-step instead of
+// ~460 B for the split pair; every value is produced by the same expressions
+// as the split kernels, so the two paths are bitwise equal (GPU tests).  The
+// device solver switches freely between them (DeviceSolver::lns_*).
+#pragma once
+
+#include "../core/lean_euler.hpp"
+
+namespace hf2d {
+
+// Kernel argument block.  Level m-1 = the primitives the fill F_m reads
+// (prim_old of the split fill), level m = the ones it produces.
+struct LnsArrays {
+  long N = 0;
+  const real* Sp = nullptr;   // Sp^m [k * N + idx] (live equations 0..3)
+  real* Sp_out = nullptr;     // Sp^{m+1}
+  real* beta = nullptr;       // in place
+  const real *Ui = nullptr, *Vi = nullptr, *Ti = nullptr;
+  real *Uo = nullptr, *Vo = nullptr, *To = nullptr;
+  const real *CPi = nullptr, *mui = nullptr, *lami = nullptr, *kki = nullptr, *pi = nullptr;
+  real *CPo = nullptr, *muo = nullptr, *lamo = nullptr, *kko = nullptr, *po = nullptr;
+  const real *R = nullptr, *BGX = nullptr, *BGY = nullptr, *grad = nullptr;
+  real* SrcAdd = nullptr;     // in place (only the owner's value is used)
+  const real* dSdx_in = nullptr;
+  const real* dSdy_in = nullptr;
+  real* dSdx_out = nullptr;
+  real* dSdy_out = nullptr;
+  const u64* CT = nullptr;
+  const u64* TT = nullptr;
+  const uint8_t* nb = nullptr;
+  const uint8_t* gf = nullptr;
+};
+
+constexpr int LNS_NL = 4;                 // live equations (SGL)
+constexpr int LNS_PLANES = 3 * LNS_NL;    // committed S, A, B per LDS cell
+
+// fill_compute() input accessor over the lean buffers (F_m of any cell of
+// the tile or its ring).  Fields the laminar single-gas fill never reads
+// (species, turbulence, stored fluxes of skipped nodes) return +0.
+struct LnsFillIO {
+  const LnsArrays& a;
+  long N, idx, nbi[4];
+  HF_HD LnsFillIO(const LnsArrays& aa, long i) : a(aa), N(aa.N), idx(i), nbi{i, i, i, i} {}
+  HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
+    nbi[ND_L] = (long)(i - n1) * ny + j;
+    nbi[ND_R] = (long)(i + n2) * ny + j;
+    nbi[ND_U] = idx + n3;
+    nbi[ND_D] = idx - n4;
+  }
+  HF_HD u64 CT() const { return a.CT[idx]; }
+  HF_HD u64 TT() const { return a.TT[idx]; }
+  HF_HD uint8_t gf() const { return a.gf[idx]; }
+  HF_HD uint8_t nb() const { return a.nb[idx]; }
+  HF_HD real S(int k) const { return a.Sp[k * N + idx]; }
+  HF_HD real Sn(int k, int d) const { return a.Sp[k * N + nbi[d]]; }
+  HF_HD real A(int) const { return 0.0; }
+  HF_HD real B(int) const { return 0.0; }
+  HF_HD real F(int) const { return 0.0; }
+  HF_HD real Src(int) const { return 0.0; }
+  HF_HD real SrcAdd(int k) const { return a.SrcAdd[k * N + idx]; }
+  HF_HD real Uo() const { return a.Ui[idx]; }
+  HF_HD real Vo() const { return a.Vi[idx]; }
+  HF_HD real To() const { return a.Ti[idx]; }
+  HF_HD real Uon(int d) const { return a.Ui[nbi[d]]; }
+  HF_HD real Von(int d) const { return a.Vi[nbi[d]]; }
+  HF_HD real Ton(int d) const { return a.Ti[nbi[d]]; }
+  HF_HD real p() const { return a.pi[idx]; }
+  HF_HD real kk() const { return a.kki[idx]; }
+  HF_HD real R() const { return a.R[idx]; }
+  HF_HD real CP() const { return a.CPi[idx]; }
+  HF_HD real lam() const { return a.lami[idx]; }
+  HF_HD real mu() const { return a.mui[idx]; }
+  HF_HD real Diff() const { return 0.0; }
+  HF_HD real mu_t() const { return 0.0; }
+  HF_HD real lam_t() const { return 0.0; }
+  HF_HD real l_min() const { return 0.0; }
+  HF_HD real y_plus() const { return 0.0; }
+  HF_HD real Re_local() const { return 0.0; }
+  HF_HD real BGX() const { return a.BGX[idx]; }
+  HF_HD real BGY() const { return a.BGY[idx]; }
+  HF_HD real Tf() const { return 0.0; }
+  HF_HD real Y(int) const { return 0.0; }
+  HF_HD real grad(int g) const { return a.grad[g * N + idx]; }
+  HF_HD real Ys(int) const { return 0.0; }
+  HF_HD real Ysn(int, int) const { return 0.0; }
+};
+
+// The node's level-m values kept in registers between F_m and the partial
+// F_{m+1} (the split fill's prim_old / per-cell inputs of the next fill).
+struct LnsLevel {
+  real U, V, Tg, p, k, R, CP, lam, mu, BGX, BGY;
+  real SrcAdd[LNS_NL];
+};
+
+// Input accessor of the own-cell part of F_{m+1}: the new predicted state
+// (registers) and the level-m values of the node (no neighbours: they only
+// enter the fluxes and gradients, which this part does not produce).
+struct LnsOwnIO {
+  const real* sn;   // Sp^{m+1}, live equations
+  const LnsLevel& v;
+  u64 ct, tt;
+  uint8_t g, b;
+  HF_HD LnsOwnIO(const real* s, const LnsLevel& lv, u64 c, u64 t, uint8_t gg, uint8_t bb)
+      : sn(s), v(lv), ct(c), tt(t), g(gg), b(bb) {}
+  HF_HD void set_nb(int, int, int, int, int, int, int) {}
+  HF_HD u64 CT() const { return ct; }
+  HF_HD u64 TT() const { return tt; }
+  HF_HD uint8_t gf() const { return g; }
+  HF_HD uint8_t nb() const { return b; }
+  HF_HD real S(int k) const { return k < LNS_NL ? sn[k] : 0.0; }
+  HF_HD real Sn(int k, int) const { return k < LNS_NL ? sn[k] : 0.0; }
+  HF_HD real A(int) const { return 0.0; }
+  HF_HD real B(int) const { return 0.0; }
+  HF_HD real F(int) const { return 0.0; }
+  HF_HD real Src(int) const { return 0.0; }
+  HF_HD real SrcAdd(int k) const { return k < LNS_NL ? v.SrcAdd[k] : 0.0; }
+  HF_HD real Uo() const { return v.U; }
+  HF_HD real Vo() const { return v.V; }
+  HF_HD real To() const { return v.Tg; }
+  HF_HD real Uon(int) const { return v.U; }
+  HF_HD real Von(int) const { return v.V; }
+  HF_HD real Ton(int) const { return v.Tg; }
+  HF_HD real p() const { return v.p; }
+  HF_HD real kk() const { return v.k; }
+  HF_HD real R() const { return v.R; }
+  HF_HD real CP() const { return v.CP; }
+  HF_HD real lam() const { return v.lam; }
+  HF_HD real mu() const { return v.mu; }
+  HF_HD real Diff() const { return 0.0; }
+  HF_HD real mu_t() const { return 0.0; }
+  HF_HD real lam_t() const { return 0.0; }
+  HF_HD real l_min() const { return 0.0; }
+  HF_HD real y_plus() const { return 0.0; }
+  HF_HD real Re_local() const { return 0.0; }
+  HF_HD real BGX() const { return v.BGX; }
+  HF_HD real BGY() const { return v.BGY; }
+  HF_HD real Tf() const { return 0.0; }
+  HF_HD real Y(int) const { return 0.0; }
+  HF_HD real grad(int) const { return 0.0; }
+  HF_HD real Ys(int) const { return 0.0; }
+  HF_HD real Ysn(int, int) const { return 0.0; }
+};
+
+// predict_core() accessor: committed S and the fluxes of the cell and its
+// neighbours from LDS, the node's own F/Src/SrcAdd from registers (its F_m),
+// beta and the Cauchy dS/dx, dS/dy in global memory.
+struct LnsPredictIO {
+  static constexpr int NE = LNS_NL;
+  static constexpr bool skip(int) { return false; }
+  HF_HD static constexpr int eq(int k) { return k; }
+  const LnsArrays& a;
+  const real* lds;
+  const real* srcadd;
+  long N, idx, iL, iR, iU, iD;
+  int NC, c, cL, cR, cU, cD;
+  uint8_t gf;
+  real sn[LNS_NL];
+  HF_HD real at(int f, int cc) const { return lds[f * NC + cc]; }
+  HF_HD real S(int k) const { return at(k, c); }
+  HF_HD real SL(int k) const { return at(k, cL); }
+  HF_HD real SR(int k) const { return at(k, cR); }
+  HF_HD real SU(int k) const { return at(k, cU); }
+  HF_HD real SD(int k) const { return at(k, cD); }
+  HF_HD real AL(int k) const { return at(LNS_NL + k, cL); }
+  HF_HD real AR(int k) const { return at(LNS_NL + k, cR); }
+  HF_HD real BU(int k) const { return at(2 * LNS_NL + k, cU); }
+  HF_HD real BD(int k) const { return at(2 * LNS_NL + k, cD); }
+  HF_HD real dxL(int k) const { return a.dSdx_in[k * N + iL]; }
+  HF_HD real dxR(int k) const { return a.dSdx_in[k * N + iR]; }
+  HF_HD real dyU(int k) const { return a.dSdy_in[k * N + iU]; }
+  HF_HD real dyD(int k) const { return a.dSdy_in[k * N + iD]; }
+  HF_HD real beta(int k) const { return a.beta[k * N + idx]; }
+  HF_HD real F(int) const { return 0.0; }   // flat problems only (lns_eligible)
+  HF_HD real Src(int) const { return 0.0; }
+  HF_HD real SrcAdd(int k) const { return (gf & GF_SRCADD) ? srcadd[k] : 0.0; }
+  HF_HD void put_S(int k, real v) { sn[k] = v; }
+  HF_HD void put_beta(int k, real v) const { a.beta[k * N + idx] = v; }
+  HF_HD void put_dS(int k, real x, real y) const {
+    if (gf & GF_DX_OUT) a.dSdx_out[k * N + idx] = x;
+    if (gf & GF_DY_OUT) a.dSdy_out[k * N + idx] = y;
+  }
+  HF_HD void keep_dS(int k) const {
+    if (gf & GF_DX_OUT) a.dSdx_out[k * N + idx] = a.dSdx_in[k * N + idx];
+    if (gf & GF_DY_OUT) a.dSdy_out[k * N + idx] = a.dSdy_in[k * N + idx];
+  }
+};
+
+// Ring cell r of a TI x TJ tile -> tile coordinates (ii, jj), ii or jj just
+// outside the tile (cross-shaped one-cell halo, no corners).
+HF_HD inline void lns_ring_cell(const LeanTile& T, int r, int* ii, int* jj) {
+  if (r < T.TJ) {
+    *ii = -1;
+    *jj = r;
+  } else if (r < 2 * T.TJ) {
+    *ii = T.TI;
+    *jj = r - T.TJ;
+  } else if (r < 2 * T.TJ + T.TI) {
+    *ii = r - 2 * T.TJ;
+    *jj = -1;
+  } else {
+    *ii = r - 2 * T.TJ - T.TI;
+    *jj = T.TJ;
+  }
+}
+
+// F_m of global cell (gi, gj) into LDS cell cc (committed S, A, B).
+// Returns fill_compute's node; *early / *filled as there.
+HF_HD inline void lns_fill_to_lds(const StepParams& P, const LnsArrays& a, int gi, int gj, real* lds, int NC, int cc,
+                                  CellLocal& c, bool* early, bool* filled, int* neg_dummy) {
+  LnsFillIO io(a, (long)gi * P.ny + gj);
+  real mY[1], mgx[1], mgy[1];
+  (void)fill_compute<SK_SGL, 1>(P, io, c, mY, mgx, mgy, nullptr, 0, gi, gj, true, neg_dummy, early, filled);
+#pragma unroll
+  for (int k = 0; k < LNS_NL; k++) {
+    lds[k * NC + cc] = c.S[k];
+    lds[(LNS_NL + k) * NC + cc] = (*early || !*filled) ? 0.0 : c.A[k];
+    lds[(2 * LNS_NL + k) * NC + cc] = (*early || !*filled) ? 0.0 : c.B[k];
+  }
+}
+
+}  // namespace hf2d

@@ -427,6 +427,40 @@ def test_march_kernel_bitwise_equals_tile(gpu, deck, march, sg):
     assert a.records() == b.records()
 
 
+@pytest.mark.parametrize("deck", ["step", "step_ref_ns", "step_graphs"])
+def test_lean_ns_equals_split(gpu, deck):
+    """Lean laminar N-S kernel (hip/lean_ns.hpp: fluxes recomputed in the LDS
+    tile, one kernel per step) == the split predict + fill kernels on every
+    field, dt and time, across entry / materialize / re-entry transitions
+    (residual steps, downloads between windows, graph windows)."""
+    from tests.conftest import read_deck
+
+    if deck in ("step", "step_graphs"):
+        text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5)
+    elif deck == "step_ref_ns":
+        text = decks.set_key(read_deck("Step.dat"), "ProblemType", 1)   # reference deck, laminar N-S
+    else:
+        text = decks.wedge15(200, 60, navier_stokes=True, turbulence=0, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    b.solver.lean_ns = False
+    if deck != "step_graphs":
+        a.solver.use_graph = b.solver.use_graph = False
+    assert a.solver.lns_ok, a.solver.lns_why
+    sched = [(4, True), (30, False), (6, True), (19, False)] if deck != "step_graphs" else [(40, False), (13, True), (61, False)]
+    for n, res in sched:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+        assert a.summary()["dt"] == b.summary()["dt"]
+    assert a.solver.lns_steps > 0
+    assert b.solver.lns_steps == 0
+    assert a.summary()["time"] == b.summary()["time"]
+    # residual sums are accumulated per tile instead of per 256-cell block
+    np.testing.assert_allclose(a.summary()["rms"], b.summary()["rms"], rtol=1e-12, atol=0)
+    for f in FIELDS + ["k", "R", "CP", "mu", "lam", "dUdx", "dTdy", "Diff"]:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
 @pytest.mark.parametrize("deck,mode", [("step", 1), ("step_ref_ns", 1), ("resonator", 2), ("wedge_keps", 2)])
 def test_single_gas_ns_specialisation_equals_generic(gpu, deck, mode):
     """Single-gas N-S split kernels (fill_cell/predict_cell_t <SK_SGL> laminar:
@@ -446,6 +480,7 @@ def test_single_gas_ns_specialisation_equals_generic(gpu, deck, mode):
     a = gpu.Simulation(text, "gpu")
     b = gpu.Simulation(text, "gpu")
     b.solver.sgl = False
+    a.solver.lean_ns = False   # the split SGL/SGT kernels themselves (lean N-S: test_lean_ns_equals_split)
     assert a.solver.sk_mode == mode, a.solver.sgl_why
     for n, res in [(4, True), (30, False), (6, True), (19, False)]:
         a.step(n, residual=res)

@@ -10,7 +10,7 @@ def main():
     pat = sys.argv[1]
     cells = float(sys.argv[2]) if len(sys.argv) > 2 else 400000.0
     out = {}
-    for f in sorted(glob.glob("gpurun_out/pmc*/run_counter_collection.csv")):
+    for f in sorted(glob.glob(sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/pmc*/run_counter_collection.csv")):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             if pat in r["Kernel_Name"]:
