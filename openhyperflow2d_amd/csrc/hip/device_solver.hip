@@ -1117,8 +1117,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
 constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
 
 template <bool RES>
-__global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
-                                                        int slot, int slot_next, int serial, ResidualPack* partials) {
+__device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
+                                              int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   apply_dt(P, sc, slot);
@@ -1150,7 +1150,10 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
   bool early = true, filled = false;
   const long N = a.N;
   const long idx = (long)i * P.ny + j;
+  real bpre[LNS_NL];
   if (mine) {
+#pragma unroll
+    for (int k = 0; k < LNS_NL; k++) bpre[k] = a.beta[k * N + idx];
     CellLocal oc;
     lns_fill_to_lds(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
     CT = oc.CT;
@@ -1195,7 +1198,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
   double dtl = 1.0;
   int neg = 0;
   if (mine) {
-    LnsPredictIO io{a, lds, lv.SrcAdd, N, idx, idx, idx, idx, idx, NC, c, c, c, c, c, gf, {0, 0, 0, 0}};
+    LnsPredictIO io{a, lds, lv.SrcAdd, bpre, N, idx, idx, idx, idx, idx, NC, c, c, c, c, c, gf, {0, 0, 0, 0}};
     if (!is_active(CT)) {
 #pragma unroll
       for (int k = 0; k < LNS_NL; k++) {
@@ -1243,6 +1246,19 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
     if (serial) m = fmin(m, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
   }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
+                                                        int slot, int slot_next, int serial, ResidualPack* partials) {
+  lns_step_body<RES>(P, a, T, sc, slot, slot_next, serial, partials);
+}
+// register budget of OCC waves per SIMD (DeviceSolver::lns_occ, measured)
+template <bool RES, int OCC>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_lns_step_occ(
+    StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
+    ResidualPack* partials) {
+  lns_step_body<RES>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 
 __global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
@@ -3382,6 +3398,12 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       if (want_res)
         hipLaunchKernelGGL(hf2d_lns_step<true>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
                            serial, m.partials);
+      else if (lns_occ == 5)
+        hipLaunchKernelGGL((hf2d_lns_step_occ<false, 5>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
+                           slot_next, serial, m.partials);
+      else if (lns_occ == 6)
+        hipLaunchKernelGGL((hf2d_lns_step_occ<false, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
+                           slot_next, serial, m.partials);
       else
         hipLaunchKernelGGL(hf2d_lns_step<false>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
                            serial, m.partials);

@@ -163,6 +163,7 @@ class DeviceSolver : public SolverBase {
   int lns_state = 0;      // 1: lean N-S buffers authoritative (committed S, A/B/F, p stale)
   int cbuf = 0;           // lean N-S: CP/mu/lam/k level ping-pong (0: the generic arrays)
   long lns_steps = 0;
+  int lns_occ = 0;        // 0: compiler register budget; 5 / 6: waves-per-SIMD budget
   void lns_materialize();
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)

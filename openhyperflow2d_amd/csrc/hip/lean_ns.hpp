@@ -57,41 +57,76 @@ constexpr int LNS_NL = 4;                 // live equations (SGL)
 constexpr int LNS_PLANES = 3 * LNS_NL;    // committed S, A, B per LDS cell
 
 // fill_compute() input accessor over the lean buffers (F_m of any cell of
-// the tile or its ring).  Fields the laminar single-gas fill never reads
-// (species, turbulence, stored fluxes of skipped nodes) return +0.
+// the tile or its ring).  Every input the laminar fill reads is loaded up
+// front in one batch -- the four neighbours' rho, U, V, T too, at clamped
+// indices, selected by the neighbour bits later (a missing neighbour
+// resolves to the cell itself, as in FillSoAIO) -- so a fill costs one
+// memory latency instead of a chain of dependent ones.  Fields the laminar
+// single-gas fill never reads return +0; wall / inactive-only fields load
+// on demand.
 struct LnsFillIO {
   const LnsArrays& a;
-  long N, idx, nbi[4];
-  HF_HD LnsFillIO(const LnsArrays& aa, long i) : a(aa), N(aa.N), idx(i), nbi{i, i, i, i} {}
-  HF_HD void set_nb(int i, int j, int ny, int n1, int n2, int n3, int n4) {
-    nbi[ND_L] = (long)(i - n1) * ny + j;
-    nbi[ND_R] = (long)(i + n2) * ny + j;
-    nbi[ND_U] = idx + n3;
-    nbi[ND_D] = idx - n4;
+  long N, idx;
+  u64 ct, tt;
+  uint8_t g, b;
+  real s[LNS_NL], u, v, t, cp, mu_, lam_, kk_, r_;
+  real rn[4], un[4], vn[4], tn[4];
+  int nbit[4];
+  HF_HD LnsFillIO(const LnsArrays& aa, int i, int j, int nx, int ny) : a(aa), N(aa.N), idx((long)i * ny + j) {
+    const long nbi[4] = {i > 0 ? idx - ny : idx, i < nx - 1 ? idx + ny : idx, j < ny - 1 ? idx + 1 : idx,
+                         j > 0 ? idx - 1 : idx};
+    ct = a.CT[idx];
+    tt = a.TT[idx];
+    g = a.gf[idx];
+    b = a.nb[idx];
+#pragma unroll
+    for (int k = 0; k < LNS_NL; k++) s[k] = a.Sp[k * N + idx];
+    u = a.Ui[idx];
+    v = a.Vi[idx];
+    t = a.Ti[idx];
+    cp = a.CPi[idx];
+    mu_ = a.mui[idx];
+    lam_ = a.lami[idx];
+    kk_ = a.kki[idx];
+    r_ = a.R[idx];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      rn[d] = a.Sp[nbi[d]];
+      un[d] = a.Ui[nbi[d]];
+      vn[d] = a.Vi[nbi[d]];
+      tn[d] = a.Ti[nbi[d]];
+      nbit[d] = 0;
+    }
   }
-  HF_HD u64 CT() const { return a.CT[idx]; }
-  HF_HD u64 TT() const { return a.TT[idx]; }
-  HF_HD uint8_t gf() const { return a.gf[idx]; }
-  HF_HD uint8_t nb() const { return a.nb[idx]; }
-  HF_HD real S(int k) const { return a.Sp[k * N + idx]; }
-  HF_HD real Sn(int k, int d) const { return a.Sp[k * N + nbi[d]]; }
+  HF_HD void set_nb(int, int, int, int n1, int n2, int n3, int n4) {
+    nbit[ND_L] = n1;
+    nbit[ND_R] = n2;
+    nbit[ND_U] = n3;
+    nbit[ND_D] = n4;
+  }
+  HF_HD u64 CT() const { return ct; }
+  HF_HD u64 TT() const { return tt; }
+  HF_HD uint8_t gf() const { return g; }
+  HF_HD uint8_t nb() const { return b; }
+  HF_HD real S(int k) const { return s[k]; }
+  HF_HD real Sn(int k, int d) const { return k == 0 ? (nbit[d] ? rn[d] : s[0]) : 0.0; }
   HF_HD real A(int) const { return 0.0; }
   HF_HD real B(int) const { return 0.0; }
   HF_HD real F(int) const { return 0.0; }
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int k) const { return a.SrcAdd[k * N + idx]; }
-  HF_HD real Uo() const { return a.Ui[idx]; }
-  HF_HD real Vo() const { return a.Vi[idx]; }
-  HF_HD real To() const { return a.Ti[idx]; }
-  HF_HD real Uon(int d) const { return a.Ui[nbi[d]]; }
-  HF_HD real Von(int d) const { return a.Vi[nbi[d]]; }
-  HF_HD real Ton(int d) const { return a.Ti[nbi[d]]; }
-  HF_HD real p() const { return a.pi[idx]; }
-  HF_HD real kk() const { return a.kki[idx]; }
-  HF_HD real R() const { return a.R[idx]; }
-  HF_HD real CP() const { return a.CPi[idx]; }
-  HF_HD real lam() const { return a.lami[idx]; }
-  HF_HD real mu() const { return a.mui[idx]; }
+  HF_HD real Uo() const { return u; }
+  HF_HD real Vo() const { return v; }
+  HF_HD real To() const { return t; }
+  HF_HD real Uon(int d) const { return nbit[d] ? un[d] : u; }
+  HF_HD real Von(int d) const { return nbit[d] ? vn[d] : v; }
+  HF_HD real Ton(int d) const { return nbit[d] ? tn[d] : t; }
+  HF_HD real p() const { return 0.0; }   // rewritten by fill_node before any use (SGL)
+  HF_HD real kk() const { return kk_; }
+  HF_HD real R() const { return r_; }
+  HF_HD real CP() const { return cp; }
+  HF_HD real lam() const { return lam_; }
+  HF_HD real mu() const { return mu_; }
   HF_HD real Diff() const { return 0.0; }
   HF_HD real mu_t() const { return 0.0; }
   HF_HD real lam_t() const { return 0.0; }
@@ -102,7 +137,7 @@ struct LnsFillIO {
   HF_HD real BGY() const { return a.BGY[idx]; }
   HF_HD real Tf() const { return 0.0; }
   HF_HD real Y(int) const { return 0.0; }
-  HF_HD real grad(int g) const { return a.grad[g * N + idx]; }
+  HF_HD real grad(int gg) const { return a.grad[gg * N + idx]; }
   HF_HD real Ys(int) const { return 0.0; }
   HF_HD real Ysn(int, int) const { return 0.0; }
 };
@@ -173,6 +208,7 @@ struct LnsPredictIO {
   const LnsArrays& a;
   const real* lds;
   const real* srcadd;
+  const real* bpre;   // the node's beta, loaded before the tile barrier
   long N, idx, iL, iR, iU, iD;
   int NC, c, cL, cR, cU, cD;
   uint8_t gf;
@@ -191,7 +227,7 @@ struct LnsPredictIO {
   HF_HD real dxR(int k) const { return a.dSdx_in[k * N + iR]; }
   HF_HD real dyU(int k) const { return a.dSdy_in[k * N + iU]; }
   HF_HD real dyD(int k) const { return a.dSdy_in[k * N + iD]; }
-  HF_HD real beta(int k) const { return a.beta[k * N + idx]; }
+  HF_HD real beta(int k) const { return bpre[k]; }
   HF_HD real F(int) const { return 0.0; }   // flat problems only (lns_eligible)
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int k) const { return (gf & GF_SRCADD) ? srcadd[k] : 0.0; }
@@ -229,7 +265,7 @@ HF_HD inline void lns_ring_cell(const LeanTile& T, int r, int* ii, int* jj) {
 // Returns fill_compute's node; *early / *filled as there.
 HF_HD inline void lns_fill_to_lds(const StepParams& P, const LnsArrays& a, int gi, int gj, real* lds, int NC, int cc,
                                   CellLocal& c, bool* early, bool* filled, int* neg_dummy) {
-  LnsFillIO io(a, (long)gi * P.ny + gj);
+  LnsFillIO io(a, gi, gj, P.nx, P.ny);
   real mY[1], mgx[1], mgy[1];
   (void)fill_compute<SK_SGL, 1>(P, io, c, mY, mgx, mgy, nullptr, 0, gi, gj, true, neg_dummy, early, filled);
 #pragma unroll
