@@ -185,12 +185,14 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
 // ---------------------------------------------------------------------------
 // Turbulence closures.
 // ---------------------------------------------------------------------------
-template <class N>
+// KEPS_ONLY: the caller guarantees that no node carries a model bit other
+// than k-eps (lean N-S kernel), so only that branch is compiled in.
+template <class N, bool KEPS_ONLY = false>
 HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init) {
   const real dx = P.dx, dy = P.dy;
   real l = hf_max(n.l_min, hf_min(dy, dx)) * 0.41;
   const u64 TT = n.TurbType;
-  if (has_all(TT, TCT_Prandtl_Model)) {
+  if (!KEPS_ONLY && has_all(TT, TCT_Prandtl_Model)) {
     const real A_p = 26.0;
     const real n_0 = n.l_min * 0.41;
     if (P.tem == TEM_Prandtl) {
@@ -282,7 +284,7 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
       }
       turb_axisym_addon(n, P, is_init);
     }
-  } else if (has_all(TT, TCT_Spalart_Allmaras_Model)) {
+  } else if (!KEPS_ONLY && has_all(TT, TCT_Spalart_Allmaras_Model)) {
     real fv1 = 1.0;
     if (is_init) {
       n.S[I_NUT] = n.mu / n.S[I_RHO] / 100.0;
@@ -326,12 +328,12 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
       n.mu_t = hf_max(0.0, (n.S[I_RHO] * n.S[I_NUT] * fv1));
       n.lam_t = n.mu_t * n.CP;
     }
-  } else if (has_all(TT, TCT_k_omega_SST_Model)) {
+  } else if (!KEPS_ONLY && has_all(TT, TCT_k_omega_SST_Model)) {
     turb_sst(n, P, is_mu_t, is_init);
-  } else if (has_all(TT, TCT_Integral_Model) && n.mu != 0.0) {
+  } else if (!KEPS_ONLY && has_all(TT, TCT_Integral_Model) && n.mu != 0.0) {
     n.Re_local = n.l_min *
                  std::sqrt(n.S[I_RHOU] * n.S[I_RHOU] + n.S[I_RHOV] * n.S[I_RHOV] + 1.e-30) / n.mu;
-  } else if (has_all(TT, TCT_Smagorinsky_Model)) {
+  } else if (!KEPS_ONLY && has_all(TT, TCT_Smagorinsky_Model)) {
     const real Cs = 0.1;
     const real _delta = std::sqrt(dx * dy);
     const real Wxy = 0.5 * (n.dVdx - n.dUdy);
@@ -358,10 +360,11 @@ struct RefMix {
   HF_HD void heat_flux(const N&, real&, real&) const {}
 };
 
-// TURB = false: the caller guarantees that no node carries a turbulence-model
+// TURB = 0: the caller guarantees that no node carries a turbulence-model
 // bit (SK_SGL, lean.cpp sk_eligible), so turb_model() is a no-op and is not
-// compiled in (its Spalart-Allmaras branch alone put the node in scratch).
-template <class N, class MX = RefMix, bool TURB = true>
+// compiled in (its Spalart-Allmaras branch alone put the node in scratch);
+// TURB = 2: k-eps is the only model bit present (lean N-S kernel).
+template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every model, 2 k-eps only
 HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (has_all(n.CT, CT_SOLID)) return false;
   if (n.S[I_RHO] == 0) return false;
@@ -388,7 +391,7 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
     } else if (P.is_init) {
       n.mu_t = n.lam_t = 0.;
     }
-    if (TURB && n.TurbType > 0) turb_model(n, P, P.is_mu_t, P.is_init);
+    if (TURB != 0 && n.TurbType > 0) turb_model<N, TURB == 2>(n, P, P.is_mu_t, P.is_init);
   }
 
   if (!MX::MECH) {

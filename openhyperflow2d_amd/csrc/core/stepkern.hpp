@@ -599,7 +599,7 @@ struct FillSoAIO {
 // did not skip the node.  `inplace`: the fluxes are updated in place, so
 // those of the flow and species equations need not be loaded (fill_node
 // rewrites them on every node it does not skip).
-template <int MODE, int NSB, class IO>
+template <int MODE, int NSB, class IO, bool KEPS_ONLY = false>
 HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* mY, real* mgx, real* mgy,
                                const MechData* mech, int nsp, int i, int j, bool inplace, int* neg_T,
                                bool* early, bool* filled_out) {
@@ -772,7 +772,7 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     MechMix<NSB> mx{mech, mY, mgx, mgy};
     filled = fill_node(c, fp, mx);
   } else {
-    filled = fill_node<CellLocal, RefMix, MODE != SK_SGL>(c, fp);
+    filled = fill_node<CellLocal, RefMix, MODE == SK_SGL ? 0 : (KEPS_ONLY ? 2 : 1)>(c, fp);
   }
   *filled_out = filled;
 

@@ -1116,10 +1116,11 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
 // ---------------------------------------------------------------------------
 constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
 
-template <bool RES>
+template <bool RES, int MODE>
 __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
+  constexpr int NL = Lns<MODE>::NL;
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
@@ -1140,22 +1141,22 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
       CellLocal rc;
       bool early, filled;
-      lns_fill_to_lds(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
+      lns_fill_to_lds<MODE>(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
     }
   }
   // 1b. own cell: F_m, its level-m outputs, kept values for 2./3.
-  LnsLevel lv;
+  LnsLevel<MODE> lv;
   u64 CT = 0, TT = 0;
   uint8_t gf = 0, nbm = 0;
   bool early = true, filled = false;
   const long N = a.N;
   const long idx = (long)i * P.ny + j;
-  real bpre[LNS_NL];
+  real bpre[NL];
   if (mine) {
 #pragma unroll
-    for (int k = 0; k < LNS_NL; k++) bpre[k] = a.beta[k * N + idx];
+    for (int q = 0; q < NL; q++) bpre[q] = a.beta[Lns<MODE>::eqk(q) * N + idx];
     CellLocal oc;
-    lns_fill_to_lds(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
+    lns_fill_to_lds<MODE>(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
     CT = oc.CT;
     gf = a.gf[idx];
     nbm = a.nb[idx];
@@ -1169,9 +1170,17 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       a.CPo[idx] = oc.CP;
       a.lamo[idx] = oc.lam;
       a.muo[idx] = oc.mu;
+      if (MODE == SK_SGT) {
+        a.mu_to[idx] = oc.mu_t;
+        a.Src[(long)I_K * N + idx] = oc.Src[I_K];
+        a.Src[(long)I_EPS * N + idx] = oc.Src[I_EPS];
+      }
       if (gf & GF_SRCADD)
 #pragma unroll
-        for (int k = 0; k < LNS_NL; k++) a.SrcAdd[k * N + idx] = oc.SrcAdd[k];
+        for (int q = 0; q < NL; q++) {
+          const int k = Lns<MODE>::eqk(q);
+          a.SrcAdd[k * N + idx] = oc.SrcAdd[k];
+        }
       lv.U = oc.U;
       lv.V = oc.V;
       lv.Tg = oc.Tg;
@@ -1181,10 +1190,18 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       lv.CP = oc.CP;
       lv.lam = oc.lam;
       lv.mu = oc.mu;
+      lv.mu_t = oc.mu_t;
+      lv.l_min = oc.l_min;
+      lv.y_plus = oc.y_plus;
       lv.BGX = oc.BGX;
       lv.BGY = oc.BGY;
 #pragma unroll
-      for (int k = 0; k < LNS_NL; k++) lv.SrcAdd[k] = oc.SrcAdd[k];
+      for (int q = 0; q < NL; q++) {
+        const int k = Lns<MODE>::eqk(q);
+        lv.SrcAdd[q] = oc.SrcAdd[k];
+        lv.F[q] = oc.F[k];
+        lv.Src[q] = oc.Src[k];
+      }
     }
   }
   __syncthreads();
@@ -1198,10 +1215,11 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   double dtl = 1.0;
   int neg = 0;
   if (mine) {
-    LnsPredictIO io{a, lds, lv.SrcAdd, bpre, N, idx, idx, idx, idx, idx, NC, c, c, c, c, c, gf, {0, 0, 0, 0}};
+    LnsPredictIO<MODE> io{a, lds, lv, bpre, N, idx, idx, idx, idx, idx, NC, c, c, c, c, c, gf, {}};
     if (!is_active(CT)) {
 #pragma unroll
-      for (int k = 0; k < LNS_NL; k++) {
+      for (int q = 0; q < NL; q++) {
+        const int k = Lns<MODE>::eqk(q);
         io.sn[k] = io.S(k);
         io.keep_dS(k);
       }
@@ -1219,14 +1237,18 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, r);
     }
 #pragma unroll
-    for (int k = 0; k < LNS_NL; k++) a.Sp_out[k * N + idx] = io.sn[k];
+    for (int q = 0; q < NL; q++) {
+      const int k = Lns<MODE>::eqk(q);
+      a.Sp_out[k * N + idx] = io.sn[k];
+    }
     // 3. own-cell part of F_{m+1}: dt_{m+1}
     if (!early) {
-      LnsOwnIO oio(io.sn, lv, CT, TT, gf, nbm);
+      LnsOwnIO<MODE> oio(io.sn, lv, CT, TT, gf, nbm);
       CellLocal nc;
       real mY[1], mgx[1], mgy[1];
       bool e2, f2;
-      dtl = fill_compute<SK_SGL, 1>(P, oio, nc, mY, mgx, mgy, nullptr, 0, i, j, true, &neg, &e2, &f2);
+      dtl = fill_compute<MODE, 1, LnsOwnIO<MODE>, true>(P, oio, nc, mY, mgx, mgy, nullptr, 0, i, j, true, &neg, &e2,
+                                                         &f2);
     }
   }
   if (RES) {
@@ -1248,17 +1270,17 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   }
 }
 
-template <bool RES>
+template <bool RES, int MODE>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
                                                         int slot, int slot_next, int serial, ResidualPack* partials) {
-  lns_step_body<RES>(P, a, T, sc, slot, slot_next, serial, partials);
+  lns_step_body<RES, MODE>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 // register budget of OCC waves per SIMD (DeviceSolver::lns_occ, measured)
-template <bool RES, int OCC>
+template <bool RES, int MODE, int OCC>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_lns_step_occ(
     StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
     ResidualPack* partials) {
-  lns_step_body<RES>(P, a, T, sc, slot, slot_next, serial, partials);
+  lns_step_body<RES, MODE>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 
 __global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
@@ -1539,7 +1561,7 @@ struct DeviceSolver::Impl {
   // U/V on pbuf), per-cell neighbour/publish byte
   real *Spre[2], *P2[2];
   // lean N-S: second level of CP / mu / lam / k (the first is the generic array)
-  real *CP2 = nullptr, *mu2 = nullptr, *lam2 = nullptr, *kk2 = nullptr;
+  real *CP2 = nullptr, *mu2 = nullptr, *lam2 = nullptr, *kk2 = nullptr, *mu_t2 = nullptr;
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   unsigned long long* persist_bar = nullptr;   // grid-barrier counter of hf2d_lean_persist
@@ -1629,7 +1651,7 @@ struct DeviceSolver::Impl {
   // lean N-S kernel arguments: Sp^m in S[1-sb], level m-1 primitives in
   // U/V/Tg[1-pb] and CPx[1-cb]; K_m writes Sp^{m+1} into S[sb], level m into
   // U/V/Tg[pb] and CPx[cb] (CPx[0] = the generic arrays)
-  LnsArrays lns_arrays(const HostArrays& h, int sb, int pb, int cb, int db) const {
+  LnsArrays lns_arrays(const HostArrays& h, int sb, int pb, int cb, int db, int ab) const {
     LnsArrays a;
     a.N = h.N;
     a.Sp = S[1 - sb];
@@ -1653,7 +1675,15 @@ struct DeviceSolver::Impl {
     a.muo = mux[cb];
     a.lamo = lamx[cb];
     a.kko = kkx[cb];
-    a.pi = p;
+    real* const mutx[2] = {mu_t, mu_t2};
+    a.mu_ti = mutx[1 - cb];
+    a.mu_to = mutx[cb];
+    a.l_min = l_min;
+    a.y_plus = y_plus;
+    a.Src = Src;
+    a.gA = A[ab];
+    a.gB = B[ab];
+    a.gF = F;
     a.R = R;
     a.BGX = BGX;
     a.BGY = BGY;
@@ -1932,27 +1962,38 @@ void DeviceSolver::upload() {
     };
     lns_ok = true;
     lns_why.clear();
-    if (sk_mode != SK_SGL) no("not single-gas laminar N-S");
-    else if (cs.cfg.FT != FT_FLAT) no("axisymmetric");
+    // turbulence: the k-eps family without Chien's model (it reads the
+    // previous p) and no eddy-viscosity term in the dt (the own-cell part of
+    // the next fill has no gradients)
+    const u64 other_models = TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
+                             TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model |
+                             TCT_nut_92_Model | TCT_Smagorinsky_Model;
+    if (sk_mode != SK_SGL && sk_mode != SK_SGT) no("not single-gas N-S");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
     else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
+    else if (sk_mode == SK_SGT && cs.cfg.TurbExtModel == TEM_k_eps_Chien) no("Chien k-eps");
+    else if (sk_mode == SK_SGT && cs.cfg.ViscousCFL > 0) no("viscous CFL with eddy viscosity");
     else
       for (long q = 0; q < N && lns_ok; q++) {
         if (h.gf[q] & GF_SRC) no("volume sources");
         else if (!has_all(h.CT[q], CT_SOLID) && !has_all(h.CT[q], CT_NODE_IS_SET)) no("unset non-solid node");
+        else if (h.TT[q] & other_models) no("turbulence model other than k-eps");
       }
     if (lns_ok && !m.CP2) {
       m.CP2 = m.mem.alloc<real>(N);
       m.mu2 = m.mem.alloc<real>(N);
       m.lam2 = m.mem.alloc<real>(N);
       m.kk2 = m.mem.alloc<real>(N);
+      m.mu_t2 = m.mem.alloc<real>(N);
     }
     if (m.CP2) {
       cp(m.CP2, h.CP.data(), SB);
       cp(m.mu2, h.mu.data(), SB);
       cp(m.lam2, h.lam.data(), SB);
       cp(m.kk2, h.kk.data(), SB);
+      cp(m.mu_t2, h.mu_t.data(), SB);
     }
+    lns_prev_mu_t = -1;
     lns_state = 0;
     cbuf = 0;
   }
@@ -2059,15 +2100,21 @@ void DeviceSolver::lns_materialize() {
   real* const mux[2] = {m.mu, m.mu2};
   real* const lamx[2] = {m.lam, m.lam2};
   real* const kkx[2] = {m.kk, m.kk2};
+  real* const mutx[2] = {m.mu_t, m.mu_t2};
   sin.CP = cpx[1 - cbuf];
   sin.mu = mux[1 - cbuf];
   sin.lam = lamx[1 - cbuf];
   sin.kk = kkx[1 - cbuf];
+  sin.mu_t = mutx[1 - cbuf];
   SoA out = m.view(h, sbuf, abuf, dsbuf, pbuf);
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
   const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
-  hipLaunchKernelGGL((hf2d_fill<SK_SGL, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
-                     (int)(nstep % 3), -1, 0, 1);
+  if (sk_mode == SK_SGT)
+    hipLaunchKernelGGL((hf2d_fill<SK_SGT, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
+                       (int)(nstep % 3), -1, 0, 1);
+  else
+    hipLaunchKernelGGL((hf2d_fill<SK_SGL, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
+                       (int)(nstep % 3), -1, 0, 1);
   HIP_CHECK(hipGetLastError());
   lns_state = 0;
   cbuf = 0;
@@ -2962,7 +3009,7 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   // (the in-process host transport synchronises on the host: eager only)
   const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
                      !(lean && lean_ok && lean_state == 0) &&
-                     !(lean_ns && lns_ok && lns_state == 0 && P0.sm == SM_NS);   // lean N-S entry step: eager
+                     !(lns_state == 0 && lns_entry(P0));   // lean N-S entry step: eager
   if (plain && persist_eligible()) {
     if (!pending.empty() && !pending_persist) flush_pending();
     pending_persist = true;
@@ -3083,6 +3130,7 @@ void DeviceSolver::step_split(const StepParams& P, bool want_res, int slot, int 
       out.mu = m.mu2;
       out.lam = m.lam2;
       out.kk = m.kk2;
+      out.mu_t = m.mu_t2;
     }
     if (mode == SK_MECH) {
       // operator-split kinetics: Ys[1-sbuf] -> Ys[sbuf]; N-S strips also react
@@ -3133,11 +3181,21 @@ void DeviceSolver::step_split(const StepParams& P, bool want_res, int slot, int 
     pbuf = 1 - pbuf;
 }
 
+bool DeviceSolver::lns_entry(const StepParams& P0) const {
+  if (!lean_ns || !lns_ok) return false;
+  StepParams P = P0;
+  P.ny = h.ny;
+  return lns_step_ok(P);
+}
+
 // The lean N-S kernel applies to this step (lean_ns.hpp; eligibility lns_ok)
 bool DeviceSolver::lns_step_ok(const StepParams& P) const {
   const Impl& m = *impl;
-  return lean_ns && lns_ok && P.sm == SM_NS && sgl && sgl_ok && sk_mode == SK_SGL && !m.mech && m.nranks == 1 &&
-         !m.p2p.on && !P.fpa.is_init && !P.ffc.is_init && P.ny >= LEAN_TILE_MIN_TJ;
+  // (the fill F_m runs in step m here but in step m-1 in the split stepper:
+  // the step parameters it reads must agree, i.e. is_mu_t must not change)
+  return lean_ns && lns_ok && P.sm == SM_NS && sgl && sgl_ok && (sk_mode == SK_SGL || sk_mode == SK_SGT) &&
+         !m.mech && m.nranks == 1 && !m.p2p.on && !P.fpa.is_init && !P.ffc.is_init &&
+         P.fpa.is_mu_t == lns_prev_mu_t && P.ny >= LEAN_TILE_MIN_TJ;
 }
 
 StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
@@ -3391,22 +3449,35 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       lns_state = 1;
       cbuf = 1;
     } else {
-      const LnsArrays a = m.lns_arrays(h, sbuf, pbuf, cbuf, dsbuf);
-      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 1);
+      const LnsArrays a = m.lns_arrays(h, sbuf, pbuf, cbuf, dsbuf, abuf);
+      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj > 0 ? lean_tj : lns_tile_height(P.ny, BLOCK), 1);
       const int ntile = T.nbi * T.nbj;
-      const size_t shmem = (size_t)LNS_PLANES * T.NC * sizeof(real);
-      if (want_res)
-        hipLaunchKernelGGL(hf2d_lns_step<true>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
-                           serial, m.partials);
-      else if (lns_occ == 5)
-        hipLaunchKernelGGL((hf2d_lns_step_occ<false, 5>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else if (lns_occ == 6)
-        hipLaunchKernelGGL((hf2d_lns_step_occ<false, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else
-        hipLaunchKernelGGL(hf2d_lns_step<false>, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
-                           serial, m.partials);
+      const bool t2 = sk_mode == SK_SGT;
+      const size_t shmem = (size_t)(t2 ? Lns<SK_SGT>::PLANES : Lns<SK_SGL>::PLANES) * T.NC * sizeof(real);
+      // register budget (measured, 1x MI355X): the k-eps kernel compiles to
+      // ~173 VGPRs (2 waves/SIMD); a 3-wave budget is 11 % faster (resonator
+      // 2000x200: 110.7 -> 98.8 us/step); the laminar one is best unbounded
+      const int occ = lns_occ > 0 ? lns_occ : (t2 ? 3 : 0);
+#define HF2D_LNS(R, MD)                                                                                           \
+  do {                                                                                                            \
+    if (!R && occ == 5)                                                                                           \
+      hipLaunchKernelGGL((hf2d_lns_step_occ<R, MD, 5>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, \
+                         slot_next, serial, m.partials);                                                          \
+    else if (!R && occ == 3)                                                                                      \
+      hipLaunchKernelGGL((hf2d_lns_step_occ<R, MD, 3>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, \
+                         slot_next, serial, m.partials);                                                          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((hf2d_lns_step<R, MD>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,        \
+                         slot_next, serial, m.partials);                                                          \
+  } while (0)
+      if (t2) {
+        if (want_res) HF2D_LNS(true, SK_SGT);
+        else HF2D_LNS(false, SK_SGT);
+      } else {
+        if (want_res) HF2D_LNS(true, SK_SGL);
+        else HF2D_LNS(false, SK_SGL);
+      }
+#undef HF2D_LNS
       HIP_CHECK(hipGetLastError());
       nres = (unsigned)ntile;
       sbuf = 1 - sbuf;
@@ -3434,6 +3505,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     HIP_CHECK(hipGetLastError());
   }
   nstep++;
+  lns_prev_mu_t = P.fpa.is_mu_t;
   StepResult r;
   r.async = true;
   if (want_res) {

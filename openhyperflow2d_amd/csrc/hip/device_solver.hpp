@@ -163,7 +163,8 @@ class DeviceSolver : public SolverBase {
   int lns_state = 0;      // 1: lean N-S buffers authoritative (committed S, A/B/F, p stale)
   int cbuf = 0;           // lean N-S: CP/mu/lam/k level ping-pong (0: the generic arrays)
   long lns_steps = 0;
-  int lns_occ = 0;        // 0: compiler register budget; 5 / 6: waves-per-SIMD budget
+  int lns_occ = 0;
+  int lns_prev_mu_t = -1;  // is_mu_t of the previous step (the split fill F_m ran with it)        // 0: compiler register budget; 5 / 6: waves-per-SIMD budget
   void lns_materialize();
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
@@ -199,6 +200,7 @@ class DeviceSolver : public SolverBase {
   void run_persist();
   void step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk, bool to_lns);
   bool lns_step_ok(const StepParams& P) const;
+  bool lns_entry(const StepParams& P0) const;
   // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
   void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };
