@@ -167,6 +167,61 @@ def flat_plate(nx: int = 250, ny: int = 100, *, dx: float = 1.0e-3, dy: float = 
     return t
 
 
+def mixing_layer(nx: int = 600, ny: int = 300, *, dx: float = 5.0e-4, dy: float = 1.0e-4, mach1: float = 2.0,
+                 mach2: float = 1.2, p: float = 5.0e4, T: float = 300.0, turbulence: int = 6, nmax: int = 200,
+                 nout: int = 100, project: Optional[str] = None, cfl: Optional[float] = None) -> str:
+    """Compressible plane mixing layer (validation of the turbulence models):
+    the Wedge template's five-bound contour re-shaped so the inflow edge is
+    split at mid height -- the fast stream (Flow2D-1, ``mach1``) above, the
+    slow one (Flow2D-2, ``mach2``) below, both at ``p``, ``T`` -- with
+    far-field top (stream 1) and bottom (stream 2) edges and a
+    non-reflecting outlet.  ``turbulence``: TurbulenceModel code (6 SST)."""
+    t = remove_commented_directives(template_text("Wedge.dat"))
+    project = project or "MixingLayer_%dx%d" % (nx, ny)
+    t = _rename(t, project)
+    L, H = nx * dx, ny * dy
+    eps = 1e-9
+    t = set_key(t, "MaxX", nx)
+    t = set_key(t, "MaxY", ny)
+    t = set_key(t, "dx", dx)
+    t = set_key(t, "dy", dy)
+    t = set_key(t, "ProblemType", 1)
+    t = set_key(t, "TurbulenceModel", turbulence)
+    t = set_key(t, "TurbExtModel", 4)
+    t = set_key(t, "isTurbulenceReset", 1 if turbulence else 0)
+    t = set_key(t, "Nmax", nmax)
+    t = set_key(t, "NOutStep", nout)
+    t = set_key(t, "MonitorIndex", 5)
+    t = set_key(t, "ExitMonitorValue", 1.0e-30)
+    t = set_key(t, "isAdiabaticWall", 1)
+    t = set_key(t, "Ts0", T)
+    t = set_key(t, "Flow2D-1.Mode", 2)
+    t = set_key(t, "Flow2D-2.Mode", 2)
+    t = set_key(t, "Flow2D-1.Mach", mach1)
+    t = set_key(t, "Flow2D-2.Mach", mach2)
+    t = set_key(t, "Flow2D-2.Angle", 0.0)
+    for f in (1, 2):
+        t = set_key(t, "Flow2D-%d.p" % f, p)
+        t = set_key(t, "Flow2D-%d.T" % f, T)
+    if cfl is not None:
+        t = set_key(t, "CFL", cfl)
+        t = set_table(t, "CFL_Scenario", [(0.0, cfl), (1.0e9, cfl)])
+    # top (stream 1), outlet, bottom (stream 2), lower inflow (2), upper inflow (1)
+    t = set_table(t, "Contour1", [(0.0, H), (L - eps, H), (L - eps, 0.0), (0.0, 0.0), (0.0, 0.5 * H)])
+    far = "NT_FARFIELD_2D, TCT_k_CONST_2D, TCT_eps_CONST_2D"
+    conds = [far, "NT_D0X_2D, TCT_dkdx_NULL_2D, TCT_depsdx_NULL_2D,  CT_NONREFLECTED_2D", far, far, far]
+    flows = [1, 1, 2, 2, 1]
+    for b in range(1, 6):
+        t = set_key(t, "Contour1.Bound%d.Cond" % b, conds[b - 1])
+        t = set_key(t, "Contour1.Bound%d.Flow2D" % b, flows[b - 1])
+        t = set_key(t, "Contour1.Bound%d.TurbulenceModel" % b, turbulence)
+    t = set_table(t, "Area1", [(3, 3)])
+    t = set_key(t, "Area1.Flow2D", 2)
+    t = set_key(t, "Area1.TurbulenceModel", turbulence)
+    t = set_key(t, "NumArea", 1)
+    return t
+
+
 def step(nx: int = 1200, ny: int = 400, *, navier_stokes: bool = True, nmax: int = 200, nout: int = 100,
          project: Optional[str] = None, exit_time: float = 1.0e-30) -> str:
     """Mach-3 forward-facing step (TestCases/Step.dat rescaled)."""

@@ -51,3 +51,39 @@ def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
     turb = 0.0592 * (rhos / rhoe) * (rhos * Ue * x / mus) ** -0.2
     return {"x": x, "Re_x": rex, "Cf": cf, "Cf_lam": lam, "Cf_turb": turb, "Mach": np.full_like(x, Me),
             "Tw": Tw}
+
+
+def langley_phi(mc: float) -> float:
+    """Compressibility reduction of the mixing-layer growth rate, the usual
+    fit to the Langley experimental curve: 0.23 + 0.77 exp(-3.5 Mc^2)."""
+    return 0.23 + 0.77 * math.exp(-3.5 * mc * mc)
+
+
+def mixing_layer_growth(sim, x0_frac: float = 0.3, x1_frac: float = 0.9) -> Dict[str, object]:
+    """Vorticity thickness delta_w(x) = (U1 - U2) / max_y |dU/dy| of a
+    ``decks.mixing_layer`` run, its linear growth rate over [x0, x1] of the
+    domain and the reference rates: incompressible
+    d(delta_w)/dx = 0.18 lambda (lambda = (U1 - U2)/(U1 + U2), equal
+    densities; Brown & Roshko) and the compressible one scaled by the
+    convective-Mach fit langley_phi(Mc), Mc = (U1 - U2)/(a1 + a2)."""
+    case = sim.case
+    dx, dy = case.dx, case.dy
+    U, rho, p = (np.asarray(sim.field(f)) for f in ("U", "rho", "p"))
+    nx, ny = U.shape
+    U1, U2 = U[0, ny - 3], U[0, 2]
+    a1 = math.sqrt(1.4 * p[0, ny - 3] / rho[0, ny - 3])
+    a2 = math.sqrt(1.4 * p[0, 2] / rho[0, 2])
+    dU = U1 - U2
+    i = np.arange(int(x0_frac * nx), int(x1_frac * nx))
+    grad = np.abs(np.diff(U[i, 2:ny - 2], axis=1)) / dy
+    dw = dU / grad.max(axis=1)
+    x = (i + 0.5) * dx
+    A = np.vstack([x, np.ones_like(x)]).T
+    coef, res, _, _ = np.linalg.lstsq(A, dw, rcond=None)
+    pred = A @ coef
+    r2 = 1.0 - float(((dw - pred) ** 2).sum()) / float(((dw - dw.mean()) ** 2).sum() + 1e-300)
+    lam = dU / (U1 + U2)
+    mc = dU / (a1 + a2)
+    inc = 0.18 * lam
+    return {"x": x, "delta_w": dw, "rate": float(coef[0]), "r2": r2, "lambda": lam, "Mc": mc,
+            "rate_incompressible": inc, "rate_compressible": inc * langley_phi(mc), "U1": U1, "U2": U2}
