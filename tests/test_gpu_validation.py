@@ -61,3 +61,23 @@ def test_keps_plate_keeps_the_reference_eddy_viscosity_cap(turbulent_runs):
     r = turbulent_runs[4]
     hi = r["Re_x"] > 1.4e6
     assert (r["Cf"][hi] / r["Cf_lam"][hi]).max() < 1.0
+
+
+def test_sst_mixing_layer_grows_linearly_at_the_incompressible_rate(gpu):
+    """Compressible plane mixing layer (decks.mixing_layer: Mach 2.0 over
+    Mach 1.2 air, Mc = 0.40, lambda = 0.25) with k-omega SST: the vorticity
+    thickness grows linearly (measured R^2 = 1.000 over 30-90 % of the
+    domain) at 0.98 x the incompressible Brown-Roshko rate 0.18 lambda and
+    1.47 x the Langley-corrected compressible rate: SST without a
+    compressibility correction reproduces the incompressible spreading, the
+    known behaviour of the model (profiles/mixing_layer_validation.md)."""
+    text = decks.mixing_layer(600, 300, turbulence=6, nmax=10 ** 9, nout=10 ** 8)
+    sim = gpu.Simulation(text, "gpu")
+    t_end = 2.5 * 600 * 5e-4 / (1.2 * 347.0)
+    while sim.summary()["time"] < t_end:
+        sim.step(2000)
+    g = validation.mixing_layer_growth(sim)
+    assert abs(g["Mc"] - 0.40) < 0.02, g["Mc"]
+    assert g["r2"] > 0.98, g["r2"]
+    assert 0.7 < g["rate"] / g["rate_incompressible"] < 1.3, g["rate"] / g["rate_incompressible"]
+    assert g["rate"] > g["rate_compressible"]

@@ -26,11 +26,14 @@ ap.add_argument("--p", type=float, default=5e4)
 ap.add_argument("--flow-throughs", type=float, default=2.5)
 ap.add_argument("--backend", default="gpu")
 ap.add_argument("--out", default="")
+ap.add_argument("--no-lean-ns", action="store_true")
 a = ap.parse_args()
 
 text = decks.mixing_layer(a.nx, a.ny, dx=a.dx, dy=a.dy, mach1=a.m1, mach2=a.m2, p=a.p, turbulence=a.model,
                           nmax=10 ** 9, nout=10 ** 8)
 sim = hf.Simulation(text, a.backend)
+if a.no_lean_ns:
+    sim.solver.lean_ns = False
 L = a.nx * a.dx
 t_end = a.flow_throughs * L / (a.m2 * 347.0)
 t0 = time.time()
