@@ -121,6 +121,7 @@ struct StepParams {
   FillParams ffc;    // for NT_FC cells: FillNode2D(1, 0, ...)
   const SpeciesProps* species;  // host or device pointer
   const ScenarioTables* scen = nullptr;   // device: evaluate beta_min / CFL_min per step
+  int xcd = 0;       // device split kernels: XCD-aware workgroup order (speed only; host ignores it)
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

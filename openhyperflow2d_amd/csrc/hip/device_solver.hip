@@ -91,12 +91,30 @@ __device__ inline void shfl_merge(ResidualPack& r, int off) {
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2).  Remap so XCD x owns a contiguous run of tiles: the i+-1 neighbour
+// columns a tile reads then sit in the same L2.  Bijective on [0, n).
+constexpr unsigned NUM_XCD = 8;
+__device__ inline unsigned xcd_remap(unsigned b, unsigned n) {
+  const unsigned q = n / NUM_XCD;
+  if (b >= q * NUM_XCD) return b;
+  return (b % NUM_XCD) * q + b / NUM_XCD;
+}
+// Split kernels (one cell per thread, x-major): logical block of this
+// workgroup.  A column of a tall grid spans a few blocks, so the left/right
+// neighbour reads of the round-robin order land on another XCD's L2; with
+// StepParams::xcd the blocks of an XCD form one contiguous column range.
+__device__ inline unsigned split_block(const StepParams& P) {
+  return P.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+}
+
 template <bool RES, int MODE = SK_GENERIC>
 __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA out, long c0, long c1,
                                                        DevScalars* sc, int slot, int slot_next, int serial,
                                                        ResidualPack* partials) {
   apply_dt(P, sc, slot);
-  const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
+  const unsigned blk = split_block(P);
+  const long g = (long)blk * BLOCK + threadIdx.x;
   if (g == 0) {
     // Reset the slot the NEXT step will accumulate into (never the one this
     // step's fill is min-reducing, which other blocks may already be
@@ -119,7 +137,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
-    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blockIdx.x * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)blk * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
   }
 }
 
@@ -167,7 +185,7 @@ __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const S
                                           long c1, DevScalars* sc, int slot, int slot_next, int serial,
                                           int store_grad) {
   apply_dt(P, sc, slot);
-  const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
+  const long c = c0 + (long)split_block(P) * BLOCK + threadIdx.x;
   double dtl = 1.0;
   int neg = 0;
   if (c < c1) {
@@ -245,16 +263,6 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
     if (slot_next >= 0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));   // < 0: lean N-S materialize
   }
-}
-
-// Workgroups are dispatched round-robin over the 8 XCDs (each with its own
-// L2).  Remap so XCD x owns a contiguous run of tiles: the i+-1 neighbour
-// columns a tile reads then sit in the same L2.  Bijective on [0, n).
-constexpr unsigned NUM_XCD = 8;
-__device__ inline unsigned xcd_remap(unsigned b, unsigned n) {
-  const unsigned q = n / NUM_XCD;
-  if (b >= q * NUM_XCD) return b;
-  return (b % NUM_XCD) * q + b / NUM_XCD;
 }
 
 template <bool RES, bool FROMG>
@@ -1778,6 +1786,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     HIP_CHECK(hipGetDeviceProperties(&prop, dev));
     cu_count = prop.multiProcessorCount;
   }
+  if (const char* e = std::getenv("HF2D_SPLIT_XCD")) split_xcd = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
@@ -3095,8 +3104,9 @@ void DeviceSolver::run_graph() {
 }
 
 // Split predict + fill step (every N-S / mechanism / generic case).
-void DeviceSolver::step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk,
+void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int slot_next, int serial, unsigned nblk,
                               bool to_lns) {
+  StepParams P = P0;
   Impl& m = *impl;
   hipStream_t st = m.stream;
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
@@ -3105,6 +3115,9 @@ void DeviceSolver::step_split(const StepParams& P, bool want_res, int slot, int 
     // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
     // mechanism mode: SK_MECH (Euler and N-S)
     const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+    // XCD-aware order: split Step 63.8 -> 59.2 us, resonator 117.7 -> 107.8 us
+    // on 1x MI355X; the mechanism pair is 2 % slower with it (1.767 vs 1.800 ms)
+    P.xcd = (split_xcd && mode != SK_MECH) ? 1 : 0;
 #define HF2D_PRED(R, M)                                                                                     \
   hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
                      serial, m.partials)
