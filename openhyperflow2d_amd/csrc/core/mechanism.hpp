@@ -74,6 +74,27 @@ struct MechData {
 // Thermodynamics (per unit R: cp/R, h/(RT), s/R) and mixture relations
 // ---------------------------------------------------------------------------
 HF_HD inline const real* mech_coef(const MechData& m, int s, real T) { return m.a[s][T < m.Tmid[s] ? 0 : 1]; }
+// The same coefficients as mech_coef() by value: both ranges are read at
+// addresses that do not depend on T (on the GPU: scalar loads, issued ahead
+// of the T-dependent arithmetic) and the range is picked per lane by a
+// select.  Indexing with the T-dependent range made every species of every
+// Newton iteration of mech_T_from_e a per-lane gather and a full memory round
+// trip (the mechanism fill's T recovery was latency-bound on them).
+struct Nasa7 {
+  real a[7];
+};
+HF_HD inline Nasa7 mech_coef_v(const MechData& m, int s, real T) {
+  const real* lo = m.a[s][0];
+  const real* hi = m.a[s][1];
+  const bool low = T < m.Tmid[s];
+  Nasa7 c;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const real l = lo[k], h = hi[k];
+    c.a[k] = low ? l : h;
+  }
+  return c;
+}
 HF_HD inline real nasa_cp(const real* a, real T) { return a[0] + T * (a[1] + T * (a[2] + T * (a[3] + T * a[4]))); }
 HF_HD inline real nasa_h(const real* a, real T) {
   return a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) + a[5] / T;
@@ -89,7 +110,8 @@ HF_HD inline void mech_mix_thermo(const MechData& m, const real* Y, real T, real
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
     if (s >= m.ns) break;
-    const real* a = mech_coef(m, s, T);
+    const Nasa7 c = mech_coef_v(m, s, T);
+    const real* a = c.a;
     const real R = m.Rs[s];
     se += Y[s] * R * T * (nasa_h(a, T) - 1.0);
     scv += Y[s] * R * (nasa_cp(a, T) - 1.0);
@@ -129,13 +151,23 @@ HF_HD inline void mech_transport(const MechData& m, const real* Y, real T, real*
   if (i > MECH_NT - 2) i = MECH_NT - 2;
   const real w = x - (real)i;   // linear inter/extrapolation from the end segments
   real smu = 0, slam = 0;
+  // the per-lane table reads of every species first (s < NSB <= MECH_MAXSP
+  // rows always exist), then the sums of the mechanism's species in order:
+  // one memory round trip instead of one per species
+  static_assert(NSB <= MECH_MAXSP, "species block larger than the tables");
+  real m0[NSB], m1[NSB], l0[NSB], l1[NSB];
+#pragma unroll
+  for (int s = 0; s < NSB; s++) {
+    m0[s] = m.mu_tab[s][i];
+    m1[s] = m.mu_tab[s][i + 1];
+    l0[s] = m.lam_tab[s][i];
+    l1[s] = m.lam_tab[s][i + 1];
+  }
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
     if (s >= m.ns) break;
-    const real* tm = m.mu_tab[s];
-    const real* tl = m.lam_tab[s];
-    smu += Y[s] * (tm[i] + (tm[i + 1] - tm[i]) * w);
-    slam += Y[s] * (tl[i] + (tl[i + 1] - tl[i]) * w);
+    smu += Y[s] * (m0[s] + (m1[s] - m0[s]) * w);
+    slam += Y[s] * (l0[s] + (l1[s] - l0[s]) * w);
   }
   *mu = smu;
   *lam = slam;
@@ -143,7 +175,8 @@ HF_HD inline void mech_transport(const MechData& m, const real* Y, real T, real*
 
 // Species absolute enthalpy h_s(T) (J/kg) for the enthalpy-diffusion heat flux.
 HF_HD inline real mech_h_species(const MechData& m, int s, real T) {
-  return m.Rs[s] * T * nasa_h(mech_coef(m, s, T), T);
+  const Nasa7 c = mech_coef_v(m, s, T);
+  return m.Rs[s] * T * nasa_h(c.a, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -162,8 +195,8 @@ HF_HD inline void mech_gibbs(const MechData& m, real T, real lnT, real* g) {
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
     if (s >= m.ns) break;
-    const real* a = mech_coef(m, s, T);
-    g[s] = nasa_h(a, T) - nasa_s(a, T, lnT);
+    const Nasa7 c = mech_coef_v(m, s, T);
+    g[s] = nasa_h(c.a, T) - nasa_s(c.a, T, lnT);
   }
 }
 

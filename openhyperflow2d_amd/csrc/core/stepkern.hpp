@@ -668,9 +668,13 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
   // mechanism species: mass fractions and d(rho Y_s)/dx,y (active viscous nodes)
   if (MECH) {
     const real rho = c.S[I_RHO];
+    // species loads at a clamped index, unconditionally: no branch between
+    // them, so all NSB loads are in flight together (a guarded load per
+    // species was one memory round trip each)
 #pragma unroll
     for (int s = 0; s < (MECH ? NSB : 1); s++) {
-      mY[s] = (s < nsp && rho != 0) ? io.Ys(s) / rho : 0.0;
+      const real ys = io.Ys(s < nsp ? s : nsp - 1);
+      mY[s] = (s < nsp && rho != 0) ? ys / rho : 0.0;
       mgx[s] = mgy[s] = 0.0;
     }
   }
@@ -719,10 +723,13 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     if (!ny0) c.droYdy[NCOMP] = (aU - aD) * dy_1_m;
     if (MECH) {
 #pragma unroll
-      for (int s = 0; s < (MECH ? NSB : 1); s++) {
-        if (s >= nsp) break;
-        if (!nx0) mgx[s] = (io.Ysn(s, ND_R) - io.Ysn(s, ND_L)) * dx_1_n;
-        if (!ny0) mgy[s] = (io.Ysn(s, ND_U) - io.Ysn(s, ND_D)) * dy_1_m;
+      for (int s = 0; s < (MECH ? NSB : 1); s++) {   // (clamped loads, as above)
+        const int sl = s < nsp ? s : nsp - 1;
+        const real yR = io.Ysn(sl, ND_R), yL = io.Ysn(sl, ND_L), yU = io.Ysn(sl, ND_U), yD = io.Ysn(sl, ND_D);
+        if (s < nsp) {
+          if (!nx0) mgx[s] = (yR - yL) * dx_1_n;
+          if (!ny0) mgy[s] = (yU - yD) * dy_1_m;
+        }
       }
     }
     const real rho = c.S[I_RHO];
@@ -845,13 +852,16 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     // species fluxes: inviscid, Le = 1 diffusion with Diff (the reference's
     // slot fluxes), axisymmetric F (N-S flat: F = 0)
     const bool nsv = P.sm == SM_NS;
-    const int bath = sin.mech->bath;
+    const int bath = sin.mech->bath, nsp = sin.nsp;
+    real ysv[MECH ? NSB : 1];   // loaded together (clamped index), then used
+#pragma unroll
+    for (int s = 0; s < (MECH ? NSB : 1); s++) ysv[s] = sin.Ys[(long)(s < nsp ? s : nsp - 1) * N + idx];
 #pragma unroll
     for (int s = 0; s < (MECH ? NSB : 1); s++) {
-      if (s >= sin.nsp) break;
+      if (s >= nsp) break;
       if (s == bath) continue;
       const long o = (long)s * N + idx;
-      const real rys = sin.Ys[o];
+      const real rys = ysv[s];
       real a = rys * c.U, b = rys * c.V;
       real f = axi ? (real)P.fpa.FT * b : 0.0;
       if (nsv) {
