@@ -587,6 +587,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_persist", &DeviceSolver::lean_persist)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("split_xcd", &DeviceSolver::split_xcd)
+      .def_readwrite("grad_every", &DeviceSolver::grad_every)
       .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
       .def_readwrite("comm_overlap", &DeviceSolver::comm_overlap)
       .def_readwrite("lean_ns", &DeviceSolver::lean_ns)

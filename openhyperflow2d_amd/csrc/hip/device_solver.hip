@@ -1787,6 +1787,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     cu_count = prop.multiProcessorCount;
   }
   if (const char* e = std::getenv("HF2D_SPLIT_XCD")) split_xcd = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
@@ -3156,6 +3157,11 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     }
     // SGL: gradients / Diff only when the host reads the record (or y+ follows)
     const int sg_out = (step_outputs || want_res) ? 1 : 0;
+    // SGT / mechanism: the gradients an active N-S cell stores are recomputed
+    // by its next fill before any use (fill_compute), so between outputs
+    // (and the wall friction velocities of the cycle end, an output step) they
+    // are dead stores: 80 B/cell (HF2D_GRAD_EVERY=1 stores them every step)
+    const int tg_out = grad_every ? 1 : sg_out;
     // register budget: measured on 1x MI355X (tools/fill_occ_sweep.sh): the
     // mechanism fill is 10 % faster at 2 waves/SIMD (256 VGPRs, a few spills)
     // than at the compiler's 1; SGL / SGT are fastest at the default
@@ -3177,14 +3183,14 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
   } while (0)
     if (mode == SK_MECH) {
       if (m.nsp <= 9)
-        HF2D_FILL(SK_MECH, 9, 1);
+        HF2D_FILL(SK_MECH, 9, tg_out);
       else
         hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
-                           m.sc, slot, slot_next, serial, 1);
+                           m.sc, slot, slot_next, serial, tg_out);
     } else if (mode == SK_SGL)
       HF2D_FILL(SK_SGL, 1, sg_out);
     else if (mode == SK_SGT)
-      HF2D_FILL(SK_SGT, 1, 1);
+      HF2D_FILL(SK_SGT, 1, tg_out);
     else
       hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
                          slot_next, serial, 1);
