@@ -890,7 +890,10 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     out.lam_t[idx] = c.lam_t;
     out.Re_local[idx] = c.Re_local;
   }
-  if (!SG)
+  // (mechanism mode: the slot fractions are Tecplot output only -- a fill reads
+  // them for the slot equations' wall sources, which are not live -- so they
+  // are stored on output steps, like the gradients)
+  if (!SG && (!MECH || store_grad))
     for (int s = 0; s < NSPEC; s++) out.Y[s * N + idx] = c.Y[s];
   if (store_grad && active && P.sm == SM_NS) {
     out.grad[G_DUDX * N + idx] = c.dUdx;
