@@ -594,6 +594,66 @@ struct FillSoAIO {
   HF_HD real Ysn(int s, int d) const { return sin.Ys[(long)s * N + nbi[d]]; }
 };
 
+// MechMix whose species gradients are formed inside heat_flux() (after the
+// Newton recovery of T) instead of before fill_node(), and which stores the
+// species fluxes right there (the split mechanism fill, N-S): the gradient
+// and flux registers are not live across the Newton iteration.  Same loads,
+// same expressions, same order as fill_compute's gradient loop, MechMix's
+// heat flux and fill_cell's species-flux loop: bitwise equal.
+template <int NSB, class IO>
+struct MechMixLazy {
+  static constexpr bool MECH = true;
+  const MechData* m;
+  const real* Y;
+  IO* io;
+  const SoA* out;
+  long N, idx;
+  real dx_1_n, dy_1_m, FT;
+  int nsp, bath;
+  bool grad_on, nx0, ny0, axi;
+  template <class Nd>
+  HF_HD void state(Nd& n) const {
+    MechMix<NSB>{m, Y, nullptr, nullptr}.state(n);
+  }
+  template <class Nd>
+  HF_HD void heat_flux(const Nd& n, real& qx, real& qy) const {
+    real ys[NSB], yR[NSB], yL[NSB], yU[NSB], yD[NSB];
+#pragma unroll
+    for (int s = 0; s < NSB; s++) {
+      const int sl = s < nsp ? s : nsp - 1;
+      ys[s] = io->Ys(sl);
+      yR[s] = io->Ysn(sl, ND_R);
+      yL[s] = io->Ysn(sl, ND_L);
+      yU[s] = io->Ysn(sl, ND_U);
+      yD[s] = io->Ysn(sl, ND_D);
+    }
+#pragma unroll
+    for (int s = 0; s < NSB; s++) {
+      if (s >= m->ns) break;
+      real gx = 0.0, gy = 0.0;
+      if (grad_on && s < nsp) {
+        if (!nx0) gx = (yR[s] - yL[s]) * dx_1_n;
+        if (!ny0) gy = (yU[s] - yD[s]) * dy_1_m;
+      }
+      const real h = mech_h_species(*m, s, n.Tg);
+      qx += n.Diff * h * gx;
+      qy += n.Diff * h * gy;
+      if (s < nsp && s != bath) {
+        const long o = (long)s * N + idx;
+        real a = ys[s] * n.U, b = ys[s] * n.V;
+        real f = axi ? FT * b : 0.0;
+        const real rx = n.Diff * gx, ry = n.Diff * gy;
+        a -= rx;
+        b -= ry;
+        f = axi ? f - ry : 0.0;
+        out->As[o] = a;
+        out->Bs[o] = b;
+        if (axi) out->Fs[o] = f;
+      }
+    }
+  }
+};
+
 // Gradients + FillNode2D + dt + chemistry of one cell into the register node
 // `c` (no stores).  Returns the local dt (1.0 when the cell does not limit
 // dt); *early: solid / unset node (only S is carried); *filled: fill_node()
@@ -603,7 +663,7 @@ struct FillSoAIO {
 template <int MODE, int NSB, class IO, bool KEPS_ONLY = false>
 HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* mY, real* mgx, real* mgy,
                                const MechData* mech, int nsp, int i, int j, bool inplace, int* neg_T,
-                               bool* early, bool* filled_out) {
+                               bool* early, bool* filled_out, const SoA* sout = nullptr) {
   const u64 CT = io.CT();
   constexpr bool MECH = MODE == SK_MECH;
   constexpr bool SGL = MODE == SK_SGL, SG = MODE == SK_SGL || MODE == SK_SGT;
@@ -695,6 +755,10 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     c.depsdy = io.grad(G_DEDY);
   }
 
+  // lazy mechanism gradients (sout): formed in MechMixLazy::heat_flux
+  real lz_dx = 0, lz_dy = 0;
+  bool lz_nx0 = false, lz_ny0 = false;
+  const bool lazy = MECH && sout != nullptr && P.sm == SM_NS;
   if (active && P.sm == SM_NS) {
     const uint8_t nbm = io.nb();
     const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
@@ -702,6 +766,8 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     io.set_nb(i, j, P.ny, n1, n2, n3, n4);
     const real dx_1_n = (1.0 / P.dx) / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
     const real dy_1_m = (1.0 / P.dy) / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+    lz_dx = dx_1_n;
+    lz_dy = dy_1_m;
     real aR = io.Sn(0, ND_R), aL = io.Sn(0, ND_L), aU = io.Sn(0, ND_U), aD = io.Sn(0, ND_D);
     c.droYdx[NCOMP] = c.droYdy[NCOMP] = 0.;
     const bool nx0 = has_all(CT, CT_dYdx_NULL), ny0 = has_all(CT, CT_dYdy_NULL);
@@ -721,7 +787,9 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     }
     if (!nx0) c.droYdx[NCOMP] = (aR - aL) * dx_1_n;
     if (!ny0) c.droYdy[NCOMP] = (aU - aD) * dy_1_m;
-    if (MECH) {
+    lz_nx0 = nx0;
+    lz_ny0 = ny0;
+    if (MECH && !lazy) {
 #pragma unroll
       for (int s = 0; s < (MECH ? NSB : 1); s++) {   // (clamped loads, as above)
         const int sl = s < nsp ? s : nsp - 1;
@@ -776,9 +844,15 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     fp.is_init = P.ffc.is_init;
   }
   bool filled;
-  if (MECH) {
-    MechMix<NSB> mx{mech, mY, mgx, mgy};
-    filled = fill_node(c, fp, mx);
+  if constexpr (MECH) {
+    if (lazy) {
+      MechMixLazy<NSB, IO> mx{mech, mY, &io, sout, io.N, io.idx, lz_dx, lz_dy, (real)P.fpa.FT, nsp, mech->bath,
+                              active, lz_nx0, lz_ny0, P.fpa.FT != 0};
+      filled = fill_node(c, fp, mx);
+    } else {
+      MechMix<NSB> mx{mech, mY, mgx, mgy};
+      filled = fill_node(c, fp, mx);
+    }
   } else {
     filled = fill_node<CellLocal, RefMix, MODE == SK_SGL ? 0 : (KEPS_ONLY ? 2 : 1)>(c, fp);
   }
@@ -813,7 +887,7 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
   return dt_local;
 }
 
-template <int MODE = SK_GENERIC, int NSB = 1>
+template <int MODE = SK_GENERIC, int NSB = 1, bool LAZY = false>
 HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim_old, const SoA& out, int i, int j,
                             int* neg_T, bool store_grad) {
   const long N = sin.N;
@@ -825,8 +899,9 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
   FillSoAIO io(sin, prim_old, idx);
   const bool inplace = io.inplace(out);
   bool early, filled;
-  const real dt_local =
-      fill_compute<MODE, NSB>(P, io, c, mY, mgx, mgy, sin.mech, sin.nsp, i, j, inplace, neg_T, &early, &filled);
+  const bool lazy = MECH && LAZY && P.sm == SM_NS;
+  const real dt_local = fill_compute<MODE, NSB>(P, io, c, mY, mgx, mgy, sin.mech, sin.nsp, i, j, inplace, neg_T,
+                                                &early, &filled, lazy ? &out : nullptr);
   if (early) {
     for (int k = 0; k < NEQ; k++)
       if (sk_live(MODE, k)) out.S[k * N + idx] = c.S[k];
@@ -848,7 +923,7 @@ HF_HD inline real fill_cell(const StepParams& P, const SoA& sin, const SoA& prim
     if ((k >= 4 + NCOMP && ns) || (gf & GF_SRC)) out.Src[k * N + idx] = c.Src[k];
     if (gf & GF_SRCADD) out.SrcAdd[k * N + idx] = c.SrcAdd[k];
   }
-  if (MECH && filled) {
+  if (MECH && filled && !lazy) {
     // species fluxes: inviscid, Le = 1 diffusion with Diff (the reference's
     // slot fluxes), axisymmetric F (N-S flat: F = 0)
     const bool nsv = P.sm == SM_NS;

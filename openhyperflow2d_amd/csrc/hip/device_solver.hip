@@ -159,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_reduce_residual(const ResidualPack
   }
 }
 
-template <int MODE, int NSB>
+template <int MODE, int NSB, bool LAZY = false>
 __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const SoA& pold, const SoA& out, long c0,
                                           long c1, DevScalars* sc, int slot, int slot_next, int serial,
                                           int store_grad);
@@ -173,14 +173,14 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fill(StepParams P, SoA sin, SoA po
 
 // The same fill with a register budget of OCC waves per SIMD (the split N-S
 // fills compile to 165-255 VGPRs, i.e. 1-3 waves; DeviceSolver::fill_occ)
-template <int MODE, int NSB, int OCC>
+template <int MODE, int NSB, int OCC, bool LAZY = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_fill_occ(
     StepParams P, SoA sin, SoA pold, SoA out, long c0, long c1, DevScalars* sc, int slot, int slot_next, int serial,
     int store_grad) {
-  fill_body<MODE, NSB>(P, sin, pold, out, c0, c1, sc, slot, slot_next, serial, store_grad);
+  fill_body<MODE, NSB, LAZY>(P, sin, pold, out, c0, c1, sc, slot, slot_next, serial, store_grad);
 }
 
-template <int MODE, int NSB>
+template <int MODE, int NSB, bool LAZY>
 __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const SoA& pold, const SoA& out, long c0,
                                           long c1, DevScalars* sc, int slot, int slot_next, int serial,
                                           int store_grad) {
@@ -190,7 +190,7 @@ __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const S
   int neg = 0;
   if (c < c1) {
     const int i = (int)(c / P.ny), j = (int)(c - (long)i * P.ny);
-    dtl = fill_cell<MODE, NSB>(P, sin, pold, out, i, j, &neg, store_grad != 0);
+    dtl = fill_cell<MODE, NSB, LAZY>(P, sin, pold, out, i, j, &neg, store_grad != 0);
   }
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
   __shared__ double sdt[BLOCK / WAVE];
@@ -1787,6 +1787,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     cu_count = prop.multiProcessorCount;
   }
   if (const char* e = std::getenv("HF2D_SPLIT_XCD")) split_xcd = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_MECH_LAZY")) mech_lazy = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
@@ -3182,7 +3183,10 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
                          slot, slot_next, serial, SGO);                                                        \
   } while (0)
     if (mode == SK_MECH) {
-      if (m.nsp <= 9)
+      if (m.nsp <= 9 && mech_lazy && focc == 2)
+        hipLaunchKernelGGL((hf2d_fill_occ<SK_MECH, 9, 2, true>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0,
+                           c1, m.sc, slot, slot_next, serial, tg_out);
+      else if (m.nsp <= 9)
         HF2D_FILL(SK_MECH, 9, tg_out);
       else
         hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
