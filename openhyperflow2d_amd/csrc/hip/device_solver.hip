@@ -1787,6 +1787,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     cu_count = prop.multiProcessorCount;
   }
   if (const char* e = std::getenv("HF2D_SPLIT_XCD")) split_xcd = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_SPLIT_XCD_MECH")) split_xcd_mech = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_MECH_LAZY")) mech_lazy = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   gi0 = gi0_;
@@ -3119,7 +3120,7 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
     // XCD-aware order: split Step 63.8 -> 59.2 us, resonator 117.7 -> 107.8 us
     // on 1x MI355X; the mechanism pair is 2 % slower with it (1.767 vs 1.800 ms)
-    P.xcd = (split_xcd && mode != SK_MECH) ? 1 : 0;
+    P.xcd = (split_xcd && (mode != SK_MECH || split_xcd_mech)) ? 1 : 0;
 #define HF2D_PRED(R, M)                                                                                     \
   hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
                      serial, m.partials)

@@ -153,6 +153,7 @@ class DeviceSolver : public SolverBase {
   int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)
   int fill_occ = -1;      // split fill kernels: -1 auto, 0 compiler default, 2/3/4 waves-per-SIMD register budget
   bool split_xcd = true;  // split predict/fill: XCD-aware workgroup order (HF2D_SPLIT_XCD=0 off)
+  bool split_xcd_mech = false;   // ... also for the mechanism pair (measured 2 % slower; HF2D_SPLIT_XCD_MECH=1)
   bool mech_lazy = true;  // mechanism N-S fill: species gradients/fluxes inside the heat flux (HF2D_MECH_LAZY=0 off)
   bool grad_every = false; // SGT / mechanism split fill: store the gradients every step, not only on outputs
   std::string sgl_why;
