@@ -291,7 +291,11 @@ PYBIND11_MODULE(_hf2d, m) {
         need_whole(c);
         write_hf2d(p, c.J);
       })
-      .def("read_checkpoint", [](Case& c, const std::string& p) { return read_hf2d(p, c.J); })
+      .def("read_checkpoint",
+           [](Case& c, const std::string& p) {
+             need_whole(c);
+             return read_hf2d(p, c.J);
+           })
       .def("save_plt", [](const Case& c, const std::string& p, bool rewrite) {
         need_whole(c);
         save_field_plt(p, c, c.J, c.global_time, rewrite);
@@ -302,7 +306,11 @@ PYBIND11_MODULE(_hf2d, m) {
       })
       // libOutCFD integrals on the host records (out_cfd_param.cpp)
       .def("flow2d_count", [](const Case& c) { return (int)c.flows2d.size(); })
-      .def("area_x", [](const Case& c, double x0, double y0, double dy) { return calc_area(c, c.J, x0, y0, dy); })
+      .def("area_x",
+           [](const Case& c, double x0, double y0, double dy) {
+             need_whole(c);
+             return calc_area(c, c.J, x0, y0, dy);
+           })
       .def("x_force", [](const Case& c, double x0, double y0, double dx, double dy) {
         need_whole(c);
         need_whole(c);

@@ -41,6 +41,7 @@ bool pwrite_all(int fd, const void* buf, size_t len, off_t off) {
 }  // namespace
 
 bool read_hf2d(const std::string& path, Field& J) {
+  if (!J.whole()) throw std::runtime_error("read_hf2d: the field holds a strip only (use the per-rank slab reader)");
   struct stat st;
   if (::stat(path.c_str(), &st) != 0) return false;
   const size_t want = (size_t)J.nx * J.ny * sizeof(CellRecord);
@@ -53,6 +54,7 @@ bool read_hf2d(const std::string& path, Field& J) {
 }
 
 void write_hf2d(const std::string& path, const Field& J) {
+  if (!J.whole()) throw std::runtime_error("write_hf2d: the field holds a strip only (use write_hf2d_slab)");
   int fd = ::open(path.c_str(), O_WRONLY | O_CREAT, 0644);
   if (fd < 0) throw std::runtime_error("cannot open checkpoint " + path);
   const size_t len = (size_t)J.nx * J.ny * sizeof(CellRecord);
@@ -62,9 +64,14 @@ void write_hf2d(const std::string& path, const Field& J) {
   if (!ok) throw std::runtime_error("short write to checkpoint " + path);
 }
 
+bool checkpoint_image_present(const std::string& path, int nx, int ny) {
+  struct stat st;
+  return ::stat(path.c_str(), &st) == 0 && (size_t)st.st_size == (size_t)nx * ny * sizeof(CellRecord);
+}
+
 void create_zero_hf2d(const std::string& path, int nx, int ny) {
   const off_t len = (off_t)nx * ny * (off_t)sizeof(CellRecord);
-  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
   if (fd < 0) throw std::runtime_error("cannot create checkpoint " + path);
   const int rc = ::ftruncate(fd, len);
   ::close(fd);

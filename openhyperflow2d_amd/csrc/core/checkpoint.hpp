@@ -15,6 +15,8 @@ namespace hf2d {
 bool read_hf2d(const std::string& path, Field& J);
 // zero-filled image of the full size (the reference's swap file of a cold start)
 void create_zero_hf2d(const std::string& path, int nx, int ny);
+// a file of exactly nx*ny records exists at path
+bool checkpoint_image_present(const std::string& path, int nx, int ny);
 // Writes the whole field (pwrite in <=1 GiB chunks).
 void write_hf2d(const std::string& path, const Field& J);
 // Writes a column slab [i0, i1) of a global-size file at its file offset

@@ -537,8 +537,10 @@ void SolverBase::failure_snapshot(const RunOptions& opt, const std::string& dir,
         }
       }
     *log << "\nError snapshot: " << dir << "/" << name;
-    if (opt.write_checkpoint)
+    if (opt.write_checkpoint && (ckpt_written || cs.preloaded))
       *log << "; last good checkpoint (iteration " << last_iter << "): " << dir << "/" << C.swap_file;
+    else if (opt.write_checkpoint)
+      *log << "; no checkpoint was written before the failure";
     *log << "\n" << std::flush;
   }
 }
@@ -595,10 +597,11 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
       if (t) std::fclose(t);
     }
   }
-  if (root && opt.write_checkpoint && !cs.preloaded) {
+  if (root && opt.write_checkpoint && !cs.preloaded && !checkpoint_image_present(dir + "/" + C.swap_file, C.MaxX, C.MaxY)) {
     // LoadSwapFile2D creates the swap file zero-filled at its full size on a
     // cold start (obj_data.cpp:173-219): a run that fails before its first
-    // cycle end leaves that image
+    // cycle end leaves that image.  A full-size image that was only ignored
+    // (use_checkpoint off) is kept until the first cycle end overwrites it.
     create_zero_hf2d(dir + "/" + C.swap_file, C.MaxX, C.MaxY);
   }
   if (root && opt.write_outputs) {
@@ -733,6 +736,7 @@ int SolverBase::run_cycles(const RunOptions& opt, std::ostream* log) {
       PhaseScope ph(*this, "outputs.checkpoint");   // nested in "outputs"
       strip_write_hf2d(*comm, dir + "/" + C.swap_file, J, own.first, own.second);
       if (root) write_meta(dir + "/" + C.swap_file, last_iter, dt, cs.global_time);
+      ckpt_written = true;
     }
     if (opt.write_checkpoint && C.mech_mode()) {
       // versioned species sidecar (mechanism_io.hpp): each rank writes the

@@ -116,6 +116,7 @@ class SolverBase {
   real dt_running = 1.0;     // serial semantics: never reset
   long iter = 0;             // iteration inside the current cycle
   long last_iter = 0;        // completed iterations of previous cycles
+  bool ckpt_written = false; // a cycle-end checkpoint of this run exists
   real cur_time_part = 0;
   int cycle = 0;
   ResidualSummary last_res{};

@@ -92,18 +92,36 @@ int listen_on(const std::string& addr, int port, int backlog, int* bound_port) {
   return fd;
 }
 
-int accept_one(int lfd, double timeout_s) {
+// poll() that survives signals: SIGINT/SIGTERM handlers (installed without
+// SA_RESTART so the solver can checkpoint) interrupt it with EINTR; retry with
+// the remaining time.  Returns poll's result (0 = timed out).
+int poll_retry(pollfd* p, int np, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const double left = timeout_s - std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const int rc = ::poll(p, np, left > 0 ? (int)(left * 1000) : 0);
+    if (rc >= 0 || errno != EINTR) return rc;
+  }
+}
+
+int accept_one(int lfd, double timeout_s, uint32_t* peer_addr = nullptr) {
   pollfd p{lfd, POLLIN, 0};
-  const int rc = ::poll(&p, 1, (int)(timeout_s * 1000));
+  const int rc = poll_retry(&p, 1, timeout_s);
   if (rc <= 0) fail("timed out waiting for a peer to connect");
-  const int fd = ::accept(lfd, nullptr, nullptr);
+  sockaddr_in a{};
+  socklen_t l = sizeof a;
+  int fd;
+  do fd = ::accept(lfd, (sockaddr*)&a, &l);
+  while (fd < 0 && errno == EINTR);
   if (fd < 0) fail("accept");
+  if (peer_addr) *peer_addr = a.sin_addr.s_addr;
   tune(fd);
   return fd;
 }
 
+int connect_retry(sockaddr_in a, const std::string& addr, double timeout_s);
+
 int connect_retry(const std::string& addr, int port, double timeout_s) {
-  const auto t0 = std::chrono::steady_clock::now();
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_port = htons((uint16_t)port);
@@ -115,6 +133,11 @@ int connect_retry(const std::string& addr, int port, double timeout_s) {
     a.sin_addr = ((sockaddr_in*)res->ai_addr)->sin_addr;
     ::freeaddrinfo(res);
   }
+  return connect_retry(a, addr, timeout_s);
+}
+
+int connect_retry(sockaddr_in a, const std::string& addr, double timeout_s) {
+  const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
     if (fd < 0) fail("socket");
@@ -124,7 +147,7 @@ int connect_retry(const std::string& addr, int port, double timeout_s) {
     }
     ::close(fd);
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
-      fail("cannot connect to " + addr + ":" + std::to_string(port));
+      fail("cannot connect to " + addr + ":" + std::to_string(ntohs(a.sin_port)));
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
   }
 }
@@ -134,15 +157,19 @@ int connect_retry(const std::string& addr, int port, double timeout_s) {
 TcpComm::TcpComm(int rank, int size, const std::string& addr, int port, double timeout_s) : r_(rank), n_(size) {
   if (size < 1 || rank < 0 || rank >= size) throw std::runtime_error("TcpComm: bad rank/size");
   if (size == 1) return;
-  // every rank >= 1 listens for its left neighbour on an ephemeral port
+  // every rank >= 1 listens for its left neighbour on an ephemeral port of
+  // all its interfaces; rank 0 learns each rank's address from its control
+  // connection and publishes (address, port) pairs, so the neighbour chain
+  // also forms across hosts
   int nb_lfd = -1, nb_port = 0;
-  if (r_ > 0) nb_lfd = listen_on(addr, 0, 1, &nb_port);
-  std::vector<int> nb_ports(n_, 0);
+  if (r_ > 0) nb_lfd = listen_on("0.0.0.0", 0, 1, &nb_port);
+  std::vector<uint32_t> nb_tab(2 * n_, 0);   // [2r] = IPv4 (network order), [2r+1] = port
   if (r_ == 0) {
     const int lfd = listen_on(addr, port, n_, nullptr);
     ctrl_.assign(n_, -1);
     for (int k = 1; k < n_; k++) {
-      const int fd = accept_one(lfd, timeout_s);
+      uint32_t peer = 0;
+      const int fd = accept_one(lfd, timeout_s, &peer);
       int hello[2];
       recv_all(fd, hello, sizeof hello);
       if (hello[0] <= 0 || hello[0] >= n_ || ctrl_[hello[0]] >= 0) {
@@ -150,19 +177,26 @@ TcpComm::TcpComm(int rank, int size, const std::string& addr, int port, double t
         throw std::runtime_error("TcpComm: bad or duplicate rank " + std::to_string(hello[0]));
       }
       ctrl_[hello[0]] = fd;
-      nb_ports[hello[0]] = hello[1];
+      nb_tab[2 * hello[0]] = peer;
+      nb_tab[2 * hello[0] + 1] = (uint32_t)hello[1];
     }
     ::close(lfd);
-    for (int k = 1; k < n_; k++) send_all(ctrl_[k], nb_ports.data(), sizeof(int) * n_);
+    for (int k = 1; k < n_; k++) send_all(ctrl_[k], nb_tab.data(), sizeof(uint32_t) * nb_tab.size());
   } else {
     ctrl_.assign(1, connect_retry(addr, port, timeout_s));
     const int hello[2] = {r_, nb_port};
     send_all(ctrl_[0], hello, sizeof hello);
-    recv_all(ctrl_[0], nb_ports.data(), sizeof(int) * n_);
+    recv_all(ctrl_[0], nb_tab.data(), sizeof(uint32_t) * nb_tab.size());
   }
   // neighbour chain: rank r connects to r+1's listener, r+1 accepts it
   if (r_ + 1 < n_) {
-    right_ = connect_retry(addr, nb_ports[r_ + 1], timeout_s);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)nb_tab[2 * (r_ + 1) + 1]);
+    a.sin_addr.s_addr = nb_tab[2 * (r_ + 1)];
+    char txt[INET_ADDRSTRLEN] = "?";
+    ::inet_ntop(AF_INET, &a.sin_addr, txt, sizeof txt);
+    right_ = connect_retry(a, txt, timeout_s);
     send_all(right_, &r_, sizeof r_);
   }
   if (r_ > 0) {
@@ -275,7 +309,9 @@ void TcpComm::neighbor_exchange(const void* to_left, void* from_left, size_t nle
         map[np++] = k;
       }
     if (!np) return;
-    if (::poll(p, np, 300000) <= 0) fail("halo exchange timed out");
+    const int rc = poll_retry(p, np, 300.0);
+    if (rc == 0) throw std::runtime_error("TcpComm: halo exchange timed out");
+    if (rc < 0) fail("halo exchange poll");
     for (int q = 0; q < np; q++) {
       if (!p[q].revents) continue;
       Xfer& t = x[map[q]];

@@ -82,3 +82,34 @@ def test_launcher_native_ranks_match_one_rank(hf, tmp_path, n):
         assert (tmp_path / "r1" / name).read_bytes() == (tmp_path / ("r%d" % n) / name).read_bytes(), name
     cut = [ln for ln in logs[1].splitlines() if ln.startswith(("Cut(", "Cx ="))]
     assert cut and cut == [ln for ln in logs[n].splitlines() if ln.startswith(("Cut(", "Cx ="))]
+
+
+def test_sigint_two_native_ranks_checkpoint(hf, tmp_path):
+    """Ctrl-C on a 2-rank native run (both ranks get SIGINT, as from a
+    terminal): a signal landing inside the TCP halo exchange must not abort
+    the exchange (poll EINTR is retried); the ranks agree to stop at the next
+    output step and write the cycle outputs and the checkpoint."""
+    from openhyperflow2d_amd.models import decks
+
+    text = decks.wedge15(300, 80, nmax=10 ** 7, nout=20)
+    (tmp_path / "w.dat").write_text(text)
+    exe = os.path.join(ROOT, "openhyperflow2d_amd", "bin", "hf2d_cpu")
+    port = 29800 + os.getpid() % 100
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([exe, "--backend", "cpu", "w.dat"], cwd=tmp_path, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    time.sleep(6)
+    for _ in range(5):   # several signals, most land inside an exchange
+        for p in procs:
+            p.send_signal(signal.SIGINT)
+        time.sleep(0.05)
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+    assert "Interrupted by user" in outs[0]
+    assert (tmp_path / "Wedge15_300x80.hf2d").stat().st_size == 300 * 80 * 1248
+    meta = json.loads((tmp_path / "Wedge15_300x80.hf2d.meta").read_text())
+    assert meta["iteration"] > 0
