@@ -163,11 +163,14 @@ HF_HD inline void mech_transport(const MechData& m, const real* Y, real T, real*
     l0[s] = m.lam_tab[s][i];
     l1[s] = m.lam_tab[s][i + 1];
   }
+  // (predicated, not `break`: a runtime trip count makes the compiler roll
+  // the loop and index the register arrays dynamically, through scratch)
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
-    if (s >= m.ns) break;
-    smu += Y[s] * (m0[s] + (m1[s] - m0[s]) * w);
-    slam += Y[s] * (l0[s] + (l1[s] - l0[s]) * w);
+    if (s < m.ns) {
+      smu += Y[s] * (m0[s] + (m1[s] - m0[s]) * w);
+      slam += Y[s] * (l0[s] + (l1[s] - l0[s]) * w);
+    }
   }
   *mu = smu;
   *lam = slam;
