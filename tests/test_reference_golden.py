@@ -39,7 +39,9 @@ def cli(hf):
 def test_reference_outputs_bitwise(case, cli, tmp_path):
     d = os.path.join(FIXTURES, "ref", case)
     want = json.load(open(os.path.join(d, "sha256.json")))
-    shutil.copy(os.path.join(d, "deck.dat"), tmp_path / "deck.dat")
+    for fn in os.listdir(d):   # the deck and any file it names (airfoil tables)
+        if fn != "sha256.json":
+            shutil.copy(os.path.join(d, fn), tmp_path / fn)
     # _runs > 1: later runs resume from the .hf2d the previous run wrote
     for _ in range(want.get("_runs", 1)):
         r = subprocess.run([cli, "--backend", "ref", "--semantics", "serial", "--reference-exit-status", "deck.dat"],

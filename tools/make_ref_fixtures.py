@@ -105,7 +105,47 @@ def cases():
                                        y_max=20, y_min=0, isOutHeatFluxY=1, is_Cx_calc=1, x_body=0.07,
                                        y_body=0.0, dx_body=0.05, dy_body=0.012, Cx_Flow_Index=1),
         "restart_from_hf2d": (_wedge(steps=20), 2),
+        # round 3: the last unpinned paths
+        # TsAGI table airfoil (hyper_flow_airfoil.cpp:99-150): the contour
+        # comes from the UpperSurface / LowerSurface tables of a second file
+        "tsagi_airfoil": (_wedge(NumAirfoils=1, Airfoil1__Xstart=0.03, Airfoil1__Ystart=0.022, Airfoil1__Type=1,
+                                 Airfoil1__InputData="airfoil_tsagi.dat", Airfoil1__scale=0.035,
+                                 Airfoil1__attack_angle=4.0, Airfoil1__Flow2D=1, Airfoil1__TurbulenceModel=0,
+                                 # (the reference prints the airfoil Re from Cx_Flow_Index, so the Cx block is on)
+                                 is_Cx_calc=1, x_body=0.025, y_body=0.01, dx_body=0.05, dy_body=0.025,
+                                 Cx_Flow_Index=1), 1,
+                          {"airfoil_tsagi.dat": _tsagi_table()}),
+        # wall-law nodes (NT_WALL_LAW_2D, hyper_flow_node.hpp:447 ff): the ramp
+        # and the plate ahead of it as wall-law boundaries of the turbulent
+        # wedge.  The reference's wall-law projection diverges on this deck at
+        # iteration 3 (next to the inflow corner): three full steps of the
+        # path and the error snapshot are pinned
+        "wall_law": decks.set_key(decks.set_key(_wedge(turb=4), "Contour1.Bound3.Cond",
+                                                "NT_WALL_LAW_2D, TCT_eps_Cmk2kXn_WALL_2D"),
+                                  "Contour1.Bound4.Cond", "NT_WALL_LAW_2D, TCT_eps_Cmk2kXn_WALL_2D"),
+        # the Integral turbulence model (TurbulenceModel = 1: Re_local only,
+        # hyper_flow_node.hpp:921-924)
+        "integral_model": _wedge(turb=1),
     }
+
+
+def _tsagi_table():
+    """A 12 % thick cambered section as UpperSurface / LowerSurface tables
+    (x, y in chord units), the external-deck format of the TsAGI airfoil."""
+    import math
+
+    xs = [0.0, 0.0125, 0.025, 0.05, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 1.0]
+
+    def half(x):   # NACA-00xx thickness with a closed trailing edge
+        return 0.6 * (0.2969 * math.sqrt(x) - 0.126 * x - 0.3516 * x * x + 0.2843 * x ** 3 - 0.1036 * x ** 4)
+
+    def camber(x):
+        return 0.02 * x * (1.0 - x) * 4.0
+
+    up = ["%.6f %.6f" % (x, camber(x) + half(x)) for x in xs]
+    lo = ["%.6f %.6f" % (x, camber(x) - half(x)) for x in xs]
+    return ("<start/Airfoil>\n<table=UpperSurface/%d>\n%s\n<endtable>\n<table=LowerSurface/%d>\n%s\n<endtable>\n"
+            "<end/Airfoil>\n" % (len(up), "\n".join(up), len(lo), "\n".join(lo)))
 
 
 def sha256(path):
@@ -124,18 +164,22 @@ def main():
     for name, spec in cases().items():
         if a.only and name not in a.only:
             continue
-        text, runs = spec if isinstance(spec, tuple) else (spec, 1)
+        text, runs, extra = (spec + ({},))[:3] if isinstance(spec, tuple) else (spec, 1, {})
         d = os.path.join(FIX, "ref", name)
         os.makedirs(d, exist_ok=True)
         with open(os.path.join(d, "deck.dat"), "w") as f:
             f.write(text)
+        for fn, body in extra.items():   # files the deck names (e.g. an airfoil table deck)
+            with open(os.path.join(d, fn), "w") as f:
+                f.write(body)
         with tempfile.TemporaryDirectory() as tmp:
-            shutil.copy(os.path.join(d, "deck.dat"), tmp)
+            for fn in ["deck.dat"] + list(extra):
+                shutil.copy(os.path.join(d, fn), tmp)
             # runs > 1: the later runs resume from the .hf2d the previous one wrote
             for _ in range(runs):
                 r = subprocess.run([a.ref, "deck.dat"], cwd=tmp, capture_output=True, text=True, errors="replace",
                                    timeout=1800)
-            outs = sorted(f for f in os.listdir(tmp) if f.endswith((".plt", ".hf2d")))
+            outs = sorted(f for f in os.listdir(tmp) if f.endswith((".plt", ".hf2d")) and f not in extra)
             rec = {f: sha256(os.path.join(tmp, f)) for f in outs}
             rec["_returncode"] = r.returncode
             rec["_runs"] = runs
