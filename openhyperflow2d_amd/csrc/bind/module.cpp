@@ -592,7 +592,6 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("p2p_fallback", &DeviceSolver::p2p_fallback, py::call_guard<py::gil_scoped_release>())
       .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
-      .def_readwrite("lean_persist", &DeviceSolver::lean_persist)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("split_xcd", &DeviceSolver::split_xcd)
       .def_readwrite("grad_every", &DeviceSolver::grad_every)
@@ -605,12 +604,6 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("lns_state", &DeviceSolver::lns_state)
       .def_readonly("lns_steps", &DeviceSolver::lns_steps)
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
-      .def_readwrite("persist_steps", &DeviceSolver::persist_steps)
-      .def_readonly("persist_launches", &DeviceSolver::persist_launches)
-      .def_readonly("persist_why", &DeviceSolver::persist_why)
-      .def("persist_trace", &DeviceSolver::persist_trace, py::arg("steps") = 8,
-           py::call_guard<py::gil_scoped_release>())
-      .def_readonly("persist_trace_tiles", &DeviceSolver::persist_trace_tiles)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())
@@ -632,12 +625,10 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("chem_fast_ok", &DeviceSolver::chem_fast_ok)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
-      .def_readwrite("lean_march", &DeviceSolver::lean_march)
       .def_readwrite("sgl", &DeviceSolver::sgl)
       .def_readonly("sgl_ok", &DeviceSolver::sgl_ok)
       .def_readonly("sgl_why", &DeviceSolver::sgl_why)
       .def_readonly("sk_mode", &DeviceSolver::sk_mode)
-      .def_readwrite("lean_pipe", &DeviceSolver::lean_pipe)
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_readonly("lean_has_cauchy_x", &DeviceSolver::lean_has_cauchy_x)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },

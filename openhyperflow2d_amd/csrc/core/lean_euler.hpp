@@ -538,117 +538,6 @@ struct TileIO : LeanIOCommon {
   }
 };
 
-// ---------------------------------------------------------------------------
-// Register-marching form.  One wavefront owns 64 consecutive "rows"
-// q = chunk * ny + j of a set of column chunks (C columns wide) and marches
-// through the chunk's columns: the staged fields of the previous, current
-// and next column stay in registers (x neighbours without re-reads), the
-// y neighbours are the adjacent lanes (the wave's two edge lanes load the
-// row beyond it), and the column two steps ahead is in flight while the
-// current one is computed.  MarchIO gives lean_cell() the same values
-// TileIO reads from LDS, so the result is bitwise identical.
-// Field slots as in TileIO: S[0..NE), pre-chemistry species (non-SG), U, V, p.
-// ---------------------------------------------------------------------------
-template <bool SG>
-struct MarchIO : LeanIOCommon {
-  static constexpr int NE = SG ? 4 : 4 + NCOMP;
-  static constexpr int FU = SG ? 4 : 10, FV = FU + 1, FP = FU + 2, NF = FU + 3;
-  const real (&C)[NF];
-  const real (&Lf)[NF];
-  const real (&Rf)[NF];
-  const real (&Uf)[NF];
-  const real (&Df)[NF];
-  int n1 = 0, n2 = 0, n3 = 0, n4 = 0;
-
-  HF_HD MarchIO(const LeanSoA& l, long i, const real (&c)[NF], const real (&lf)[NF], const real (&rf)[NF],
-                const real (&uf)[NF], const real (&df)[NF])
-      : LeanIOCommon(l, i), C(c), Lf(lf), Rf(rf), Uf(uf), Df(df) {}
-  HF_HD real U0() const { return C[FU]; }
-  HF_HD real V0() const { return C[FV]; }
-  HF_HD real P0() const { return C[FP]; }
-  HF_HD void set_nb(int i, int j, int ny, int a1, int a2, int a3, int a4) {
-    set_nb_global(i, j, ny, a1, a2, a3, a4);
-    n1 = a1;
-    n2 = a2;
-    n3 = a3;
-    n4 = a4;
-  }
-  // a missing neighbour resolves to the cell itself (TileIO: c -/+ 0)
-  HF_HD real L_(int f) const { return n1 ? Lf[f] : C[f]; }
-  HF_HD real R_(int f) const { return n2 ? Rf[f] : C[f]; }
-  HF_HD real U_(int f) const { return n3 ? Uf[f] : C[f]; }
-  HF_HD real D_(int f) const { return n4 ? Df[f] : C[f]; }
-  HF_HD real S(int k) const { return C[k]; }
-  HF_HD real SL(int k) const { return L_(k); }
-  HF_HD real SR(int k) const { return R_(k); }
-  HF_HD real SU(int k) const { return U_(k); }
-  HF_HD real SD(int k) const { return D_(k); }
-  template <class G>
-  HF_HD static real fA(int k, G at) {
-    const real u = at(FU), p = at(FP);
-    switch (k) {
-      case I_RHO: return at(1);
-      case I_RHOU: return p + at(1) * u;
-      case I_RHOV: return at(2) * u;
-      case I_RHOE: return (at(3) + p) * u;
-      default: return at(k + 3) * u;
-    }
-  }
-  template <class G>
-  HF_HD static real fB(int k, G at) {
-    const real u = at(FU), v = at(FV), p = at(FP);
-    switch (k) {
-      case I_RHO: return at(2);
-      case I_RHOU: return at(2) * u;
-      case I_RHOV: return p + at(2) * v;
-      case I_RHOE: return (at(3) + p) * v;
-      default: return at(k + 3) * v;
-    }
-  }
-  HF_HD real AL(int k) const { return fA(k, [&](int f) { return L_(f); }); }
-  HF_HD real AR(int k) const { return fA(k, [&](int f) { return R_(f); }); }
-  HF_HD real BU(int k) const { return fB(k, [&](int f) { return U_(f); }); }
-  HF_HD real BD(int k) const { return fB(k, [&](int f) { return D_(f); }); }
-  HF_HD real F(int k) const {
-    const real u0 = U0(), v0 = V0(), p0 = P0();
-    switch (k) {
-      case I_RHO: return FT * C[2];
-      case I_RHOU: return FT * (C[2] * u0);
-      case I_RHOV: return FT * (FT * C[2]) * v0;
-      case I_RHOE: return FT * ((C[3] + p0) * v0);
-      default: return FT * (C[k + 3] * v0);
-    }
-  }
-};
-
-// Load the staged fields of global cell g (march / tile field order).
-template <bool SG>
-HF_HD inline void march_load(const LeanSoA& L, long g, real (&v)[MarchIO<SG>::NF]) {
-  const long N = L.N;
-  constexpr int NS = MarchIO<SG>::NE, FU = MarchIO<SG>::FU;
-#pragma unroll
-  for (int f = 0; f < NS; f++) v[f] = L.Sin[f * N + g];
-  if (!SG)
-#pragma unroll
-    for (int f = 0; f < NCOMP; f++) v[4 + NCOMP + f] = L.Pin_s[f * N + g];
-  v[FU] = L.Uin[g];
-  v[FU + 1] = L.Vin[g];
-  v[FU + 2] = L.Pin[g];
-}
-
-// March geometry: owned columns [i0, i1) in chunks of C columns; rows
-// q = chunk * ny + j, 64 per wavefront.
-struct MarchGeom {
-  int C, nchunks;
-  long nrows;   // nchunks * ny
-};
-inline MarchGeom march_geom(int ncols, int ny, int C) {
-  MarchGeom G;
-  G.C = C;
-  G.nchunks = (ncols + C - 1) / C;
-  G.nrows = (long)G.nchunks * ny;
-  return G;
-}
 
 // Logical tile b -> cell layer q of thread t; returns false for idle threads.
 HF_HD inline bool lean_tile_cell(const StepParams& P, const LeanTile& T, int b, int t, int* i, int* j, int* c,

@@ -635,470 +635,6 @@ void hf2d_lean_tile_occ(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc, int
   lean_tile_body<RES, OUT, SG, CPT>(P, L, T, sc, slot, slot_next, serial, partials);
 }
 
-// ---------------------------------------------------------------------------
-// Persistent multi-step lean kernel (one rank, single GPU).  The one-shot
-// tile kernel re-stages every tile from HBM each step and the whole chip runs
-// "all staging, then all compute" (profiles/tile_phase_trace.md).  Here one
-// cooperative launch runs a window of plain steps: every workgroup keeps its
-// tile's lean state (S, U, V, p) in LDS and its cells' own persistent values
-// (beta, Cp, R, flags) in registers for the whole window, publishes only the
-// tile-border cells of each step to the global ping-pong arrays, and meets the
-// other workgroups at one grid barrier per step (the global dt MIN and the
-// halo are the only cross-tile dependencies), after which it reads its halo
-// ring.  Cross-workgroup traffic (border cells, dt, scenario values, Cauchy
-// dS) uses system-coherent loads/stores: the tiles of one step live on all
-// eight XCDs, whose L2s are not coherent with each other.  Same lean_cell()
-// arithmetic through PersistIO: bitwise equal to the per-step kernels.
-// ---------------------------------------------------------------------------
-constexpr int PERSIST_ERR = 4;               // neg_T bit: a grid barrier timed out
-constexpr int PERSIST_TRACE_STEPS = 8;       // steps recorded by the phase trace
-constexpr long PERSIST_SPIN_LIMIT = 1L << 24;
-
-__device__ inline unsigned long long load_sys_u64(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ inline void store_sys_u64(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// The per-step tile kernel's IO, except that a tile-border node publishes its
-// new lean state with system-coherent stores (other XCDs read it as halo after
-// the grid barrier) and Cauchy nodes exchange dS the same way.
-template <bool SG>
-struct PersistIO : TileIO<SG> {
-  using Base = TileIO<SG>;
-  bool border;
-  HF_HD PersistIO(const LeanSoA& l, long i, const real* s, int nc, int w, int cc, bool b)
-      : Base(l, i, s, nc, w, cc), border(b) {}
-  HF_HD void out_S(int k, real v) const {
-    real* d = &this->L.Sout[k * this->N + this->idx];
-    if (border) p2p_store(d, v);
-    else *d = v;
-  }
-  HF_HD void out_Ps(int k, real v) const {
-    real* d = &this->L.Pout_s[k * this->N + this->idx];
-    if (border) p2p_store(d, v);
-    else *d = v;
-  }
-  HF_HD void out_UVP(real u, real v, real p) const {
-    if (border) {
-      p2p_store(&this->L.Uout[this->idx], u);
-      p2p_store(&this->L.Vout[this->idx], v);
-      p2p_store(&this->L.Pout[this->idx], p);
-    } else {
-      this->L.Uout[this->idx] = u;
-      this->L.Vout[this->idx] = v;
-      this->L.Pout[this->idx] = p;
-    }
-  }
-  // Cauchy nodes read dS/dx, dS/dy published by another tile in the previous step
-  HF_HD real dxL(int k) const { return p2p_load(&this->L.dSdx_in[k * this->N + this->iL]); }
-  HF_HD real dxR(int k) const { return p2p_load(&this->L.dSdx_in[k * this->N + this->iR]); }
-  HF_HD real dyU(int k) const { return p2p_load(&this->L.dSdy_in[k * this->N + this->iU]); }
-  HF_HD real dyD(int k) const { return p2p_load(&this->L.dSdy_in[k * this->N + this->iD]); }
-  HF_HD void put_dS(int k, real a, real b) const {
-    if (this->lb & LB_DX_OUT) p2p_store(&this->L.dSdx_out[k * this->N + this->idx], a);
-    if (this->lb & LB_DY_OUT) p2p_store(&this->L.dSdy_out[k * this->N + this->idx], b);
-  }
-  HF_HD void keep_dS(int k) const {
-    const long o2 = k * this->N + this->idx;
-    if (this->lb & LB_DX_OUT) p2p_store(&this->L.dSdx_out[o2], p2p_load(&this->L.dSdx_in[o2]));
-    if (this->lb & LB_DY_OUT) p2p_store(&this->L.dSdy_out[o2], p2p_load(&this->L.dSdy_in[o2]));
-  }
-};
-
-template <bool SG, int CPT>
-// 4 waves per SIMD: every tile of the headline grid must be co-resident
-__global__ __launch_bounds__(BLOCK, 4) void hf2d_lean_persist(StepParams P, LeanSoA L, LeanTile T,
-                                                           DevScalars* sc, int slot0, int nsteps, int serial,
-                                                           unsigned long long* bar, int dbg,
-                                                           unsigned long long* trace) {
-  extern __shared__ real lds[];
-  constexpr int NS = SG ? 4 : 4 + NCOMP;
-  constexpr int FU = SG ? 4 : 10;
-  __shared__ int s_abort;
-  __shared__ double sdt[BLOCK / WAVE];
-  __shared__ double s_scal[3];
-  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
-  const unsigned long long nwg = gridDim.x;
-  const int t = threadIdx.x;
-  const int NC = T.NC;
-  const long N = L.N;
-  // (cell coordinates are recomputed where used: fewer registers live
-  // across the step loop, which must fit 128 VGPRs for co-residency)
-  int i0, j0;
-  {
-    int ti, tjj, tc;
-    (void)lean_tile_cell(P, T, (int)b, t, &ti, &tjj, &tc, &i0, &j0, 0);
-  }
-  lean_tile_stage<SG>(P, L, T, i0, j0, lds, t, BLOCK);
-  if (t == 0) s_abort = 0;
-  __syncthreads();
-  int done = 0;   // steps completed
-  for (int s = 0; s < nsteps; s++) {
-    if (s > 0) {   // ping-pong: last step's outputs are this step's inputs
-      const real* in;
-      in = L.Sin; L.Sin = L.Sout; L.Sout = const_cast<real*>(in);
-      in = L.Pin_s; L.Pin_s = L.Pout_s; L.Pout_s = const_cast<real*>(in);
-      in = L.Uin; L.Uin = L.Uout; L.Uout = const_cast<real*>(in);
-      in = L.Vin; L.Vin = L.Vout; L.Vout = const_cast<real*>(in);
-      in = L.Pin; L.Pin = L.Pout; L.Pout = const_cast<real*>(in);
-      in = L.dSdx_in; L.dSdx_in = L.dSdx_out; L.dSdx_out = const_cast<real*>(in);
-      in = L.dSdy_in; L.dSdy_in = L.dSdy_out; L.dSdy_out = const_cast<real*>(in);
-    }
-    const int slot = (slot0 + s) % 3, slot_next = (slot + 1) % 3;
-    // dt and scenario values of this step (folded / written by the previous
-    // step): one coherent load per workgroup, broadcast through LDS (204k
-    // uncached loads of one address per step would serialise on its channel)
-    if (t == 0) {
-      s_scal[0] = bits_to_d(load_sys_u64(&sc->dt_bits[slot]));
-      if (P.scen) {
-        s_scal[1] = p2p_load(&sc->beta_min[slot]);
-        s_scal[2] = p2p_load(&sc->cfl_min[slot]);
-      }
-    }
-    __syncthreads();
-    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 0] = rt_clock();
-    P.dt = s_scal[0];
-    P.dtdx = P.dt / P.dx;
-    P.dtdy = P.dt / P.dy;
-    if (P.scen) {
-      P.beta_min = s_scal[1];
-      P.CFL_min = s_scal[2];
-    }
-    if (b == 0 && t == 0) {
-      store_sys_u64(&sc->dt_bits[slot_reset(slot)], d_to_bits(1.0));
-      sc->time_part += P.dt;   // block 0 only; the host reads it after the kernel
-      const double it = p2p_load(&sc->iter[slot]) + 1.0;
-      p2p_store(&sc->iter[slot_next], it);
-      if (P.scen) {
-        const real bs = table_eval(P.scen->beta, it), cs = table_eval(P.scen->cfl, it);
-        p2p_store(&sc->beta_min[slot_next], (bs < P.scen->beta0) ? bs : P.scen->beta0);
-        p2p_store(&sc->cfl_min[slot_next], (cs < P.scen->CFL) ? cs : P.scen->CFL);
-      }
-    }
-    double dtl = 1.0;
-    int neg = 0;
-    ResidualPack r;
-#pragma unroll
-    for (int q = 0; q < CPT; q++) {
-      int ci, cj, cc, a0, b0;
-      if (!lean_tile_cell(P, T, (int)b, t, &ci, &cj, &cc, &a0, &b0, q)) continue;
-      LeanOwn own;
-      lean_load_own<NS>(L, (long)ci * P.ny + cj, own);
-      const int ii = ci - a0, jj = cj - b0;
-      PersistIO<SG> io(L, (long)ci * P.ny + cj, lds, NC, T.W, cc,
-                       !(dbg & 8) && (ii == 0 || ii == T.TI - 1 || jj == 0 || jj == T.TJ - 1));
-      dtl = fmin(dtl, lean_cell<false, false>(P, L, io, own, ci, cj, r, &neg));
-    }
-    for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
-    if ((t & (WAVE - 1)) == 0) sdt[t / WAVE] = dtl;
-    if (neg) atomicOr(&sc->neg_T, 1);
-    __syncthreads();   // every LDS read of this step is done
-    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 1] = rt_clock();
-    if (t == 0) {
-      double m = sdt[0];
-      for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
-      if (serial) m = fmin(m, P.dt);
-      if (dbg & 4)
-        atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
-      else
-        __hip_atomic_fetch_min(&sc->dt_bits[slot_next], d_to_bits(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    // this step's state of the own cells back into LDS: exactly what the
-    // per-step kernel would stage next (nodes the step does not fill keep
-    // whatever the output arrays hold).  Written by this very thread, so
-    // L2/L1-resident; border nodes were stored system-coherent -> read alike.
-#pragma unroll
-    for (int q = 0; q < CPT; q++) {
-      int ci, cj, cc, a0, b0;
-      if (s + 1 == nsteps || !lean_tile_cell(P, T, (int)b, t, &ci, &cj, &cc, &a0, &b0, q)) continue;
-      const long g = (long)ci * P.ny + cj;
-      const int ii = ci - a0, jj = cj - b0;
-      if (!(dbg & 8) && (ii == 0 || ii == T.TI - 1 || jj == 0 || jj == T.TJ - 1)) {
-#pragma unroll
-        for (int f = 0; f < NS; f++) lds[f * NC + cc] = p2p_load(&L.Sout[f * N + g]);
-        if (!SG)
-#pragma unroll
-          for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = p2p_load(&L.Pout_s[f * N + g]);
-        lds[FU * NC + cc] = p2p_load(&L.Uout[g]);
-        lds[(FU + 1) * NC + cc] = p2p_load(&L.Vout[g]);
-        lds[(FU + 2) * NC + cc] = p2p_load(&L.Pout[g]);
-      } else {
-#pragma unroll
-        for (int f = 0; f < NS; f++) lds[f * NC + cc] = L.Sout[f * N + g];
-        if (!SG)
-#pragma unroll
-          for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = L.Pout_s[f * N + g];
-        lds[FU * NC + cc] = L.Uout[g];
-        lds[(FU + 1) * NC + cc] = L.Vout[g];
-        lds[(FU + 2) * NC + cc] = L.Pout[g];
-      }
-    }
-    vm_drain();
-    __syncthreads();
-    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 2] = rt_clock();
-    // grid barrier: monotonic arrival counter, bounded wait
-    if (t == 0 && !(dbg & 1)) {
-      if (dbg & 2)
-        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const unsigned long long target = (unsigned long long)(s + 1) * nwg;
-      long spins = 0;
-      while (((dbg & 2) ? __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : load_sys_u64(bar)) <
-             target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > PERSIST_SPIN_LIMIT) {
-          atomicOr(&sc->neg_T, PERSIST_ERR);
-          break;
-        }
-      }
-      (void)__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-      s_abort = (__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & PERSIST_ERR) ? 1 : 0;
-    }
-    __syncthreads();
-    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 3] = rt_clock();
-    done = s + 1;
-    if (s_abort || done == nsteps) break;   // the last step's output arrays are complete
-    // the next step's halo ring: the neighbour tiles' border cells of this step
-    for (int cc = t; cc < NC; cc += BLOCK) {
-      const int ii = cc / T.W - 1, jj = cc - (ii + 1) * T.W - 1;
-      const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
-      const int gi = i0 + ii, gj = j0 + jj;
-      if (!(xh || yh) || (xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
-      const long g = (long)gi * P.ny + gj;
-      if (dbg & 8) {
-#pragma unroll
-        for (int f = 0; f < NS; f++) lds[f * NC + cc] = L.Sout[f * N + g];
-        lds[FU * NC + cc] = L.Uout[g];
-        lds[(FU + 1) * NC + cc] = L.Vout[g];
-        lds[(FU + 2) * NC + cc] = L.Pout[g];
-        continue;
-      }
-#pragma unroll
-      for (int f = 0; f < NS; f++) lds[f * NC + cc] = p2p_load(&L.Sout[f * N + g]);
-      if (!SG)
-#pragma unroll
-        for (int f = 0; f < NCOMP; f++) lds[(4 + NCOMP + f) * NC + cc] = p2p_load(&L.Pout_s[f * N + g]);
-      lds[FU * NC + cc] = p2p_load(&L.Uout[g]);
-      lds[(FU + 1) * NC + cc] = p2p_load(&L.Vout[g]);
-      lds[(FU + 2) * NC + cc] = p2p_load(&L.Pout[g]);
-    }
-    __syncthreads();
-    if (trace && t == 0 && s < PERSIST_TRACE_STEPS) trace[((size_t)b * PERSIST_TRACE_STEPS + s) * 6 + 4] = rt_clock();
-    if (trace && t == 0 && s == 0) trace[((size_t)b * PERSIST_TRACE_STEPS) * 6 + 5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);
-  }
-  (void)done;   // the output arrays of the last step hold the complete state
-}
-
-// Software-pipelined lean step: a persistent grid (a few workgroups per CU)
-// walks the CPT=1 tiles tile = b, b + G, b + 2G, ...; while tile k is
-// computed from LDS, the staged fields and own-cell data of tile k+G are
-// already in flight into registers, and are written to LDS after the barrier
-// that ends tile k.  The one-shot tile kernel runs every workgroup's load
-// phase at once and then every compute phase; here HBM streaming overlaps
-// the FP64 work.  Same lean_cell() / TileIO arithmetic: fields bitwise equal
-// to hf2d_lean_tile (residual sums accumulate in a different order).
-constexpr int PIPE_SLOTS = 2;   // LDS slots per thread: (TIh + 2) * (TJ + 2) <= 2 * BLOCK for CPT = 1
-
-template <int NE>
-__device__ __forceinline__ void lean_load_own_all(const LeanSoA& L, long idx, LeanOwn& o) {
-  const long N = L.N;   // unconditional: a prefetch must not wait for CT
-  o.CT = L.CT[idx];
-  o.lb = L.lb[idx];
-#pragma unroll
-  for (int k = 0; k < NE; k++) o.beta[k] = L.beta[k * N + idx];
-  o.CP = L.CP[idx];
-  o.R = L.R[idx];
-  o.kk = L.kk[idx];
-}
-
-template <bool RES, bool OUT, bool SG>
-__global__ __launch_bounds__(BLOCK) void hf2d_lean_pipe(StepParams P, LeanSoA L, LeanTile T, int ntiles,
-                                                        DevScalars* sc, int slot, int slot_next, int serial,
-                                                        ResidualPack* partials) {
-  extern __shared__ real lds[];
-  constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
-  constexpr int NS = SG ? 4 : 4 + NCOMP;
-  constexpr int FU = SG ? 4 : 10;
-  apply_dt(P, sc, slot);
-  const unsigned G = gridDim.x;
-  const unsigned b = xcd_remap(blockIdx.x, G);
-  if (b == 0 && threadIdx.x == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
-    sc->time_part += P.dt;
-    scenario_next(P, sc, slot, slot_next);
-  }
-  const long N = L.N;
-  const int t = threadIdx.x;
-  real st[PIPE_SLOTS][NF];
-  bool sv[PIPE_SLOTS];
-  LeanOwn own;
-  bool mine = false;
-  int ci = 0, cj = 0, cc = 0;
-  auto issue = [&](int tile) {
-    int i0, j0;
-    mine = lean_tile_cell(P, T, tile, t, &ci, &cj, &cc, &i0, &j0, 0);
-    if (mine) lean_load_own_all<NS>(L, (long)ci * P.ny + cj, own);
-#pragma unroll
-    for (int s = 0; s < PIPE_SLOTS; s++) {
-      const int c = t + s * BLOCK;
-      const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
-      const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
-      const int gi = i0 + ii, gj = j0 + jj;
-      sv[s] = c < T.NC && !(xh && yh) && gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny;
-      if (sv[s]) {
-        const long g = (long)gi * P.ny + gj;
-#pragma unroll
-        for (int f = 0; f < NS; f++) st[s][f] = L.Sin[f * N + g];
-        if (!SG)
-#pragma unroll
-          for (int f = 0; f < NCOMP; f++) st[s][4 + NCOMP + f] = L.Pin_s[f * N + g];
-        st[s][FU] = L.Uin[g];
-        st[s][FU + 1] = L.Vin[g];
-        st[s][FU + 2] = L.Pin[g];
-      }
-    }
-  };
-  ResidualPack r;
-  if (RES) {
-    residual_reset(r);
-#pragma unroll
-    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
-  }
-  double dtl = 1.0;
-  int neg = 0;
-  if ((int)b < ntiles) issue((int)b);
-  for (int tile = (int)b; tile < ntiles; tile += (int)G) {
-#pragma unroll
-    for (int s = 0; s < PIPE_SLOTS; s++)
-      if (sv[s])
-#pragma unroll
-        for (int f = 0; f < NF; f++) lds[f * T.NC + t + s * BLOCK] = st[s][f];
-    LeanOwn cur = own;
-    cur.filled = mine && !has_all(cur.CT, CT_SOLID) && has_all(cur.CT, CT_NODE_IS_SET);
-    const bool cm = mine;
-    const int i = ci, j = cj, c = cc;
-    __syncthreads();
-    if (tile + (int)G < ntiles) issue(tile + (int)G);
-    if (cm) {
-      TileIO<SG> io(L, (long)i * P.ny + j, lds, T.NC, T.W, c);
-      dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, cur, i, j, r, &neg));
-    }
-    __syncthreads();
-  }
-  if (RES) {
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
-    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
-  }
-  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
-  __shared__ double sdt[BLOCK / WAVE];
-  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
-  if (neg) atomicOr(&sc->neg_T, 1);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double m = sdt[0];
-    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
-    if (serial) m = fmin(m, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
-  }
-}
-
-// Register-marching lean step (lean_euler.hpp MarchIO): one wavefront per
-// workgroup owns 64 consecutive rows q = chunk * ny + j and marches through
-// the chunk's C columns.  Each column's staged fields are loaded once per
-// wave (no x halo re-reads, no LDS, no barrier), the column two ahead and the
-// next column's own data are in flight while the current one is computed.
-constexpr int MARCH_BLOCK = WAVE;
-
-template <bool RES, bool OUT, bool SG>
-__global__ __launch_bounds__(MARCH_BLOCK) void hf2d_lean_march(StepParams P, LeanSoA L, MarchGeom G, DevScalars* sc,
-                                                               int slot, int slot_next, int serial,
-                                                               ResidualPack* partials) {
-  using IO = MarchIO<SG>;
-  constexpr int NF = IO::NF;
-  apply_dt(P, sc, slot);
-  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
-  if (b == 0 && threadIdx.x == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
-    sc->time_part += P.dt;
-    scenario_next(P, sc, slot, slot_next);
-  }
-  const int lane = threadIdx.x;
-  const long ny = P.ny;
-  const long q = (long)b * MARCH_BLOCK + lane;
-  const bool live = q < G.nrows;
-  const int chunk = live ? (int)(q / ny) : 0;
-  const int j = live ? (int)(q - (long)chunk * ny) : 0;
-  const int ia = P.i0 + chunk * G.C;
-  // the wave's edge lanes also carry the row beyond it (lane 0: j-1, lane 63: j+1)
-  const int hj = lane == 0 ? j - 1 : (lane == MARCH_BLOCK - 1 ? j + 1 : -1);
-  const bool hl = live && hj >= 0 && hj < P.ny;
-  real Lc[NF], Cc[NF], Rc[NF], Xc[NF], Hc[NF], Hr[NF], Hx[NF];
-#pragma unroll
-  for (int f = 0; f < NF; f++) Lc[f] = Cc[f] = Rc[f] = Xc[f] = Hc[f] = Hr[f] = Hx[f] = 0.0;
-  if (live && ia - 1 >= 0) march_load<SG>(L, (long)(ia - 1) * ny + j, Lc);
-  if (live) march_load<SG>(L, (long)ia * ny + j, Cc);
-  if (hl) march_load<SG>(L, (long)ia * ny + hj, Hc);
-  if (live && ia + 1 < P.nx) march_load<SG>(L, (long)(ia + 1) * ny + j, Rc);
-  if (hl && ia + 1 < P.nx) march_load<SG>(L, (long)(ia + 1) * ny + hj, Hr);
-  LeanOwn oc, on;
-  if (live && ia < P.i1) lean_load_own<IO::NE>(L, (long)ia * ny + j, oc);
-  ResidualPack r;
-  if (RES) {
-    residual_reset(r);
-#pragma unroll
-    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
-  }
-  double dtl = 1.0;
-  int neg = 0;
-  for (int s = 0; s < G.C; s++) {
-    const int i = ia + s;
-    // in flight during this column: column i+2 (right neighbour of the next
-    // one) and the next column's own data
-    if (s + 2 <= G.C && i + 2 < P.nx) {
-      if (live) march_load<SG>(L, (long)(i + 2) * ny + j, Xc);
-      if (hl) march_load<SG>(L, (long)(i + 2) * ny + hj, Hx);
-    }
-    if (live && s + 1 < G.C && i + 1 < P.i1) lean_load_own<IO::NE>(L, (long)(i + 1) * ny + j, on);
-    real Uc[NF], Dc[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) {
-      const real up = __shfl_down(Cc[f], 1, MARCH_BLOCK);
-      const real dn = __shfl_up(Cc[f], 1, MARCH_BLOCK);
-      Uc[f] = lane == MARCH_BLOCK - 1 ? Hc[f] : up;
-      Dc[f] = lane == 0 ? Hc[f] : dn;
-    }
-    if (live && i < P.i1) {
-      IO io(L, (long)i * ny + j, Cc, Lc, Rc, Uc, Dc);
-      dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, oc, i, j, r, &neg));
-    }
-#pragma unroll
-    for (int f = 0; f < NF; f++) {
-      Lc[f] = Cc[f];
-      Cc[f] = Rc[f];
-      Rc[f] = Xc[f];
-      Hc[f] = Hr[f];
-      Hr[f] = Hx[f];
-    }
-    oc = on;
-  }
-  if (RES) {
-#pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
-    if (lane == 0) partials[b] = r;
-  }
-  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
-  if (neg) atomicOr(&sc->neg_T, 1);
-  if (lane == 0) {
-    double m = dtl;
-    if (serial) m = fmin(m, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
-  }
-}
-
 // K8 monitors: p and Tg of the probe cells this rank owns (idx < 0: not
 // owned) gathered on the device, so an output step moves 16 bytes per probe
 // instead of the whole state.
@@ -1509,6 +1045,67 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
 // ---------------------------------------------------------------------------
 // DeviceSolver
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Kernel tables: the template variants a step can select, indexed by the
+// selecting parameters (the host dispatch is a table lookup, not a ladder).
+// ---------------------------------------------------------------------------
+using PredictK = void (*)(StepParams, SoA, SoA, long, long, DevScalars*, int, int, int, ResidualPack*);
+// [residual][SK_* mode]
+static const PredictK kPredict[2][4] = {
+    {hf2d_predict<false, SK_GENERIC>, hf2d_predict<false, SK_SGL>, hf2d_predict<false, SK_SGT>,
+     hf2d_predict<false, SK_MECH>},
+    {hf2d_predict<true, SK_GENERIC>, hf2d_predict<true, SK_SGL>, hf2d_predict<true, SK_SGT>,
+     hf2d_predict<true, SK_MECH>}};
+
+using FillK = void (*)(StepParams, SoA, SoA, SoA, long, long, DevScalars*, int, int, int, int);
+// register-budget slot of a fill: compiler default, 2, 3, 4 waves per SIMD
+inline int occ_slot(int occ) { return occ == 2 ? 1 : occ == 3 ? 2 : occ == 4 ? 3 : 0; }
+// [SK_* mode][occ_slot] (mechanism: the 9-species block)
+static const FillK kFill[4][4] = {
+    {hf2d_fill<SK_GENERIC>, hf2d_fill<SK_GENERIC>, hf2d_fill<SK_GENERIC>, hf2d_fill<SK_GENERIC>},
+    {hf2d_fill<SK_SGL, 1>, hf2d_fill_occ<SK_SGL, 1, 2>, hf2d_fill_occ<SK_SGL, 1, 3>, hf2d_fill_occ<SK_SGL, 1, 4>},
+    {hf2d_fill<SK_SGT, 1>, hf2d_fill_occ<SK_SGT, 1, 2>, hf2d_fill_occ<SK_SGT, 1, 3>, hf2d_fill_occ<SK_SGT, 1, 4>},
+    {hf2d_fill<SK_MECH, 9>, hf2d_fill_occ<SK_MECH, 9, 2>, hf2d_fill_occ<SK_MECH, 9, 3>, hf2d_fill_occ<SK_MECH, 9, 4>}};
+
+using TileK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*, int);
+using TileFxK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*, FusedX);
+using TileTrK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*,
+                         unsigned long long*);
+// [single gas][cells per thread - 1][0 plain, 1 outputs, 2 residual]
+static const TileK kTile[2][2][3] = {
+    {{hf2d_lean_tile<false, false, false, 0, 1>, hf2d_lean_tile<false, true, false, 0, 1>,
+      hf2d_lean_tile<true, true, false, 0, 1>},
+     {hf2d_lean_tile<false, false, false, 0, 2>, hf2d_lean_tile<false, true, false, 0, 2>,
+      hf2d_lean_tile<true, true, false, 0, 2>}},
+    {{hf2d_lean_tile<false, false, true, 0, 1>, hf2d_lean_tile<false, true, true, 0, 1>,
+      hf2d_lean_tile<true, true, true, 0, 1>},
+     {hf2d_lean_tile<false, false, true, 0, 2>, hf2d_lean_tile<false, true, true, 0, 2>,
+      hf2d_lean_tile<true, true, true, 0, 2>}}};
+static const TileFxK kTileFx[2][2][3] = {
+    {{hf2d_lean_tile_fx<false, false, false, 1>, hf2d_lean_tile_fx<false, true, false, 1>,
+      hf2d_lean_tile_fx<true, true, false, 1>},
+     {hf2d_lean_tile_fx<false, false, false, 2>, hf2d_lean_tile_fx<false, true, false, 2>,
+      hf2d_lean_tile_fx<true, true, false, 2>}},
+    {{hf2d_lean_tile_fx<false, false, true, 1>, hf2d_lean_tile_fx<false, true, true, 1>,
+      hf2d_lean_tile_fx<true, true, true, 1>},
+     {hf2d_lean_tile_fx<false, false, true, 2>, hf2d_lean_tile_fx<false, true, true, 2>,
+      hf2d_lean_tile_fx<true, true, true, 2>}}};
+static const TileTrK kTileTr[2][2] = {{hf2d_lean_tile_tr<false, 1>, hf2d_lean_tile_tr<false, 2>},
+                                      {hf2d_lean_tile_tr<true, 1>, hf2d_lean_tile_tr<true, 2>}};
+
+using LeanEulerK = void (*)(StepParams, LeanSoA, long, long, DevScalars*, int, int, int, ResidualPack*);
+// [residual][first lean step: from the generic arrays]
+static const LeanEulerK kLeanEuler[2][2] = {{hf2d_lean_euler<false, false>, hf2d_lean_euler<false, true>},
+                                            {hf2d_lean_euler<true, false>, hf2d_lean_euler<true, true>}};
+
+using LnsK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*);
+// [k-eps][residual][register budget: default, 3, 5 waves per SIMD]
+static const LnsK kLns[2][2][3] = {
+    {{hf2d_lns_step<false, SK_SGL>, hf2d_lns_step_occ<false, SK_SGL, 3>, hf2d_lns_step_occ<false, SK_SGL, 5>},
+     {hf2d_lns_step<true, SK_SGL>, hf2d_lns_step<true, SK_SGL>, hf2d_lns_step<true, SK_SGL>}},
+    {{hf2d_lns_step<false, SK_SGT>, hf2d_lns_step_occ<false, SK_SGT, 3>, hf2d_lns_step_occ<false, SK_SGT, 5>},
+     {hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>}}};
+
 struct DevBuf {
   std::vector<void*> ptrs;
   template <class T>
@@ -1572,12 +1169,6 @@ struct DeviceSolver::Impl {
   real *CP2 = nullptr, *mu2 = nullptr, *lam2 = nullptr, *kk2 = nullptr, *mu_t2 = nullptr;
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
-  unsigned long long* persist_bar = nullptr;   // grid-barrier counter of hf2d_lean_persist
-  // hf2d_lean_persist launch geometry, cached per strip shape
-  long persist_key = -1;
-  LeanTile persist_T{};
-  const void* persist_fn = nullptr;
-  size_t persist_shmem = 0;
   int32_t* wslot;
   // K10 (y+): owned wall nodes, their friction velocities, all strips' values
   long* wall_own = nullptr;
@@ -1862,8 +1453,6 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
     // any tile shape (lean_tj) covers >= LEAN_TILE_MIN_TJ cells per workgroup
     const long nb_tile = (long)(gi1 - gi0 + 1) * ((h.ny + LEAN_TILE_MIN_TJ - 1) / LEAN_TILE_MIN_TJ);
     m.max_partials = std::max((N + BLOCK - 1) / BLOCK, nb_tile) * (BLOCK / WAVE);
-    // marching kernel: one partial per wave, rows rounded up to whole chunks (C <= 64)
-    m.max_partials = std::max(m.max_partials, (N + 64L * h.ny) / WAVE + 1);
   }
   m.partials = m.mem.alloc<ResidualPack>(m.max_partials);
   m.res_out = m.mem.alloc<ResidualPack>(1);
@@ -2256,12 +1845,6 @@ void DeviceSolver::sync_scalars() {
   if (err & LNS_SKIP_ERR) {
     char b[256];
     std::snprintf(b, sizeof b, "ERROR: lean N-S step: FillNode2D skipped a node (rho = 0 or k < 1) before iteration %ld",
-                  last_iter + iter);
-    throw std::runtime_error(b);
-  }
-  if (err & PERSIST_ERR) {
-    char b[256];
-    std::snprintf(b, sizeof b, "ERROR: persistent step kernel: grid barrier timed out before iteration %ld",
                   last_iter + iter);
     throw std::runtime_error(b);
   }
@@ -2832,24 +2415,15 @@ void DeviceSolver::p2p_complete() {
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int GRAPH_STEPS = 6;
-uint64_t graph_signature(const StepParams& P, int lean_state, bool lean, bool fused, bool tile, bool sg, int cpt,
-                         int tj, int march, int pipe, int fuse, int sglf) {
+// Everything that selects the kernels of a step besides the step parameters
+// (DeviceSolver::mode_signature): a window replays only under the same one.
+uint64_t graph_signature(const StepParams& P, uint64_t mode) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
   mix((uint64_t)P.fpa.is_mu_t);
   mix((uint64_t)P.fpa.is_init);
   mix((uint64_t)P.fpa.isSrcAdd);
-  mix((uint64_t)lean_state);
-  mix((uint64_t)lean);
-  mix((uint64_t)fused);
-  mix((uint64_t)tile);
-  mix((uint64_t)sg);
-  mix((uint64_t)cpt);
-  mix((uint64_t)tj);
-  mix((uint64_t)march);
-  mix((uint64_t)pipe);
-  mix((uint64_t)fuse);
-  mix((uint64_t)sglf);
+  mix(mode);
   return h;
 }
 }  // namespace
@@ -2864,156 +2438,18 @@ struct DeviceSolver::GraphCache {
 
 void DeviceSolver::flush_pending() {
   if (pending.empty()) return;
-  if (pending_persist && pending.size() >= 2) {
-    run_persist();
-    return;
-  }
-  pending_persist = false;
   std::vector<StepParams> q;
   q.swap(pending);
   for (const StepParams& p : q) do_step_eager(p, false);
 }
 
-// The lean tile step of one rank, eligible for the persistent window kernel.
-bool DeviceSolver::persist_eligible() const {
-  const Impl& m = *impl;
-  // single-gas only: the multi-gas variant spills heavily at 4 waves / SIMD
-  return lean_persist > 0 && persist_steps >= 2 && lean && lean_ok && lean_sg && lean_sg_ok && lean_tile &&
-         lean_march <= 0 &&
-         lean_pipe <= 0 && lean_state == 1 && h.ny >= LEAN_TILE_MIN_TJ && cs.cfg.ProblemType != SM_NS &&
-         m.nranks <= 1 && !m.p2p.on && !m.local && !m.comm && !tile_trace && lean_wgcu <= 0 && lean_occ == 0;
-}
-
-void DeviceSolver::run_persist() {
-  Impl& m = *impl;
-  std::vector<StepParams> q;
-  q.swap(pending);
-  pending_persist = false;
-  auto eager = [&](const std::string& why) {
-    if (!why.empty()) {
-      lean_persist = 0;
-      persist_why = why;
-    }
-    for (const StepParams& p : q) do_step_eager(p, false);
-  };
-  const uint64_t sig = graph_signature(q[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                       lean_tj, 0, 0, 0, 0);
-  for (const StepParams& p : q)
-    if (graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt, lean_tj, 0, 0, 0, 0) !=
-        sig)
-      return eager("");
-  StepParams P = q[0];
-  P.nx = h.nx;
-  P.ny = h.ny;
-  P.i0 = l_off;
-  P.i1 = l_off + (gi1 - gi0);
-  P.gx0 = gi0 - l_off;
-  P.do_residual = 0;
-  P.species = m.species;
-  P.scen = m.scen;
-  const bool sg = lean_sg && lean_sg_ok;
-  if (!sg) return eager("multi-gas lean state");
-  // geometry of its own (the per-step autotuner's choice may not fit): two
-  // cells per thread, the auto tile height, then taller tiles until every
-  // tile is co-resident
-  const long key = (long)(P.i1 - P.i0) * 100000 + P.ny;
-  if (m.persist_key != key) {
-    int ncu = 0;
-    HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    int ntile = 0, per_cu = 0;
-    bool fits = false;
-    std::string tried;
-    const char* fc = std::getenv("HF2D_PERSIST_CPT");   // tuning / diagnosis: force 1 or 2 cells per thread
-    const int only_cpt = fc ? std::atoi(fc) : 0;
-    for (int tj : {0, 32, 40, 50, 64}) {
-      for (int cpt : {2, 1}) {
-        if (only_cpt && cpt != only_cpt) continue;
-        m.persist_T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, tj, cpt);
-        ntile = m.persist_T.nbi * m.persist_T.nbj;
-        m.persist_shmem = (size_t)lean_tile_fields(true) * m.persist_T.NC * sizeof(real);
-        m.persist_fn = cpt == 2 ? (const void*)hf2d_lean_persist<true, 2> : (const void*)hf2d_lean_persist<true, 1>;
-        HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, m.persist_fn, BLOCK, m.persist_shmem));
-        char b[96];
-        std::snprintf(b, sizeof b, "%scpt=%d TJ=%d: %d tiles, %d/CU", tried.empty() ? "" : "; ", cpt, m.persist_T.TJ,
-                      ntile, per_cu);
-        tried += b;
-        if ((long)per_cu * ncu >= ntile) {
-          fits = true;
-          break;
-        }
-      }
-      if (fits) break;
-    }
-    if (!fits) return eager("no tile geometry is co-resident on " + std::to_string(ncu) + " CUs (" + tried + ")");
-    m.persist_key = key;
-  }
-  const LeanTile T = m.persist_T;
-  const void* fn = m.persist_fn;
-  const size_t shmem = m.persist_shmem;
-  const int ntile = T.nbi * T.nbj;
-  if (!m.persist_bar) m.persist_bar = m.mem.alloc<unsigned long long>(1);
-  LeanSoA L0 = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
-  int slot0 = (int)(nstep % 3), n = (int)q.size();
-  int serial = cs.cfg.semantics == Semantics::SERIAL ? 1 : 0;
-  DevScalars* sc = m.sc;
-  unsigned long long* bar = m.persist_bar;
-  LeanTile Tt = T;
-  static const int dbg = [] {
-    const char* e = std::getenv("HF2D_PERSIST_DBG");
-    return e ? std::atoi(e) : 0;
-  }();
-  int dbgv = dbg;
-  unsigned long long* trace = persist_trace_buf;
-  void* args[] = {&P, &L0, &Tt, &sc, &slot0, &n, &serial, &bar, &dbgv, &trace};
-  HIP_CHECK(hipMemsetAsync(bar, 0, sizeof(unsigned long long), m.stream));
-  const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(ntile), dim3(BLOCK), args, (unsigned)shmem, m.stream);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return eager(std::string("cooperative launch failed: ") + hipGetErrorString(e));
-  }
-  nstep += n;
-  if (n & 1) {
-    sbuf = 1 - sbuf;
-    dsbuf = 1 - dsbuf;
-    pbuf = 1 - pbuf;
-  }
-  persist_launches++;
-  persist_trace_tiles = ntile;
-}
-
-std::vector<unsigned long long> DeviceSolver::persist_trace(int steps) {
-  Impl& m = *impl;
-  flush_pending();
-  std::vector<unsigned long long> out;
-  if (!persist_eligible()) return out;
-  // the window's geometry is known after one launch
-  if (m.persist_key < 0) {
-    run_steps(std::max(steps, 2), false);
-    flush_pending();
-  }
-  const int ntile = m.persist_T.nbi * m.persist_T.nbj;
-  const size_t words = (size_t)ntile * 8 * 6;
-  unsigned long long* d = nullptr;
-  HIP_CHECK(hipMalloc((void**)&d, words * sizeof(unsigned long long)));
-  HIP_CHECK(hipMemset(d, 0, words * sizeof(unsigned long long)));
-  persist_trace_buf = d;
-  const int ps = persist_steps;
-  persist_steps = 8;
-  try {
-    run_steps(9, false);   // one window of 8 plain steps + the eager last step
-  } catch (...) {
-    persist_steps = ps;
-    persist_trace_buf = nullptr;
-    (void)hipFree(d);
-    throw;
-  }
-  persist_steps = ps;
-  persist_trace_buf = nullptr;
-  HIP_CHECK(hipDeviceSynchronize());
-  out.resize(words);
-  HIP_CHECK(hipMemcpy(out.data(), d, words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  HIP_CHECK(hipFree(d));
-  return out;
+uint64_t DeviceSolver::mode_signature() const {
+  const int fields[] = {lean_state, (int)lean, (int)fused, (int)lean_tile, (int)(lean_sg && lean_sg_ok), lean_cpt,
+                        lean_tj, lean_wgcu, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok), lns_state,
+                        (int)lean_ns};
+  uint64_t h = 0;
+  for (int f : fields) h = h * 1000003ull + (uint64_t)(f + 1);
+  return h;
 }
 
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
@@ -3022,16 +2458,6 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
                      !(lean && lean_ok && lean_state == 0) &&
                      !(lns_state == 0 && lns_entry(P0));   // lean N-S entry step: eager
-  if (plain && persist_eligible()) {
-    if (!pending.empty() && !pending_persist) flush_pending();
-    pending_persist = true;
-    pending.push_back(P0);
-    if ((int)pending.size() >= persist_steps) run_persist();
-    StepResult r;
-    r.async = true;
-    return r;
-  }
-  if (pending_persist) flush_pending();
   if (!plain || (pending.empty() && nstep % GRAPH_STEPS != 0)) {
     flush_pending();
     return do_step_eager(P0, want_res);
@@ -3045,12 +2471,10 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
-  const uint64_t sig = graph_signature(pending[0], lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok,
-                                       lean_cpt, lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok) + 2 * lns_state + 4 * (int)lean_ns);
+  const uint64_t mode = mode_signature();
+  const uint64_t sig = graph_signature(pending[0], mode);
   bool same = true;
-  for (const StepParams& p : pending)
-    same = same && graph_signature(p, lean_state, lean, fused, lean_tile, lean_sg && lean_sg_ok, lean_cpt,
-                                   lean_tj + 1000 * lean_wgcu, lean_march, lean_pipe, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok) + 2 * lns_state + 4 * (int)lean_ns) == sig;
+  for (const StepParams& p : pending) same = same && graph_signature(p, mode) == sig;
   if (!same) {
     flush_pending();
     return;
@@ -3121,21 +2545,8 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     // XCD-aware order: split Step 63.8 -> 59.2 us, resonator 117.7 -> 107.8 us
     // on 1x MI355X; the mechanism pair is 2 % slower with it (1.767 vs 1.800 ms)
     P.xcd = (split_xcd && (mode != SK_MECH || split_xcd_mech)) ? 1 : 0;
-#define HF2D_PRED(R, M)                                                                                     \
-  hipLaunchKernelGGL((hf2d_predict<R, M>), dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot, slot_next, \
-                     serial, m.partials)
-    if (want_res) {
-      if (mode == SK_SGL) HF2D_PRED(true, SK_SGL);
-      else if (mode == SK_SGT) HF2D_PRED(true, SK_SGT);
-      else if (mode == SK_MECH) HF2D_PRED(true, SK_MECH);
-      else HF2D_PRED(true, SK_GENERIC);
-    } else {
-      if (mode == SK_SGL) HF2D_PRED(false, SK_SGL);
-      else if (mode == SK_SGT) HF2D_PRED(false, SK_SGT);
-      else if (mode == SK_MECH) HF2D_PRED(false, SK_MECH);
-      else HF2D_PRED(false, SK_GENERIC);
-    }
-#undef HF2D_PRED
+    hipLaunchKernelGGL(kPredict[want_res][mode], dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, c0, c1, m.sc, slot,
+                       slot_next, serial, m.partials);
     HIP_CHECK(hipGetLastError());
     const bool multi = (m.comm || m.local || m.p2p.on) && m.nranks > 1;
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
@@ -3168,38 +2579,18 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     // mechanism fill is 10 % faster at 2 waves/SIMD (256 VGPRs, a few spills)
     // than at the compiler's 1; SGL / SGT are fastest at the default
     const int focc = fill_occ >= 0 ? fill_occ : (mode == SK_MECH ? 2 : 0);
-#define HF2D_FILL(MD, NS, SGO)                                                                                  \
-  do {                                                                                                          \
-    if (focc == 2)                                                                                          \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 2>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else if (focc == 3)                                                                                         \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 3>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else if (focc == 4)                                                                                         \
-      hipLaunchKernelGGL((hf2d_fill_occ<MD, NS, 4>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, \
-                         m.sc, slot, slot_next, serial, SGO);                                                  \
-    else                                                                                                        \
-      hipLaunchKernelGGL((hf2d_fill<MD, NS>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc,  \
-                         slot, slot_next, serial, SGO);                                                        \
-  } while (0)
+    FillK fk;
+    int store = 1;
     if (mode == SK_MECH) {
-      if (m.nsp <= 9 && mech_lazy && focc == 2)
-        hipLaunchKernelGGL((hf2d_fill_occ<SK_MECH, 9, 2, true>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0,
-                           c1, m.sc, slot, slot_next, serial, tg_out);
-      else if (m.nsp <= 9)
-        HF2D_FILL(SK_MECH, 9, tg_out);
-      else
-        hipLaunchKernelGGL((hf2d_fill<SK_MECH, MECH_MAXSP>), dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1,
-                           m.sc, slot, slot_next, serial, tg_out);
-    } else if (mode == SK_SGL)
-      HF2D_FILL(SK_SGL, 1, sg_out);
-    else if (mode == SK_SGT)
-      HF2D_FILL(SK_SGT, 1, tg_out);
-    else
-      hipLaunchKernelGGL(hf2d_fill<SK_GENERIC>, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot,
-                         slot_next, serial, 1);
-#undef HF2D_FILL
+      store = tg_out;
+      fk = m.nsp > 9 ? hf2d_fill<SK_MECH, MECH_MAXSP>
+                     : (mech_lazy && focc == 2) ? hf2d_fill_occ<SK_MECH, 9, 2, true> : kFill[SK_MECH][occ_slot(focc)];
+    } else {
+      store = mode == SK_SGL ? sg_out : mode == SK_SGT ? tg_out : 1;
+      fk = kFill[mode][mode == SK_GENERIC ? 0 : occ_slot(focc)];
+    }
+    hipLaunchKernelGGL(fk, dim3(nblk), dim3(BLOCK), 0, st, P, sin, sin, out, c0, c1, m.sc, slot, slot_next, serial,
+                       store);
     HIP_CHECK(hipGetLastError());
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
@@ -3240,62 +2631,12 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   const bool euler = P.sm != SM_NS;
   hipStream_t st = m.stream;
   unsigned nres = nblk;   // workgroups that wrote residual partials
-  long npart = -1;        // residual partials written (-1: nres * waves per block)
   const bool sg_now = lean_sg && lean_sg_ok;
   fx_step = false;
-  const bool tile_path = euler && lean && lean_ok && lean_march <= 0 && lean_pipe <= 0 && lean_tile &&
+  const bool tile_path = euler && lean && lean_ok && lean_tile &&
                          lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ;
   if (!tile_path) p2p_complete();
-  if (euler && lean && lean_ok && lean_march > 0 && lean_state == 1) {
-    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
-    const MarchGeom G = march_geom(P.i1 - P.i0, P.ny, lean_march);
-    const unsigned nw = (unsigned)((G.nrows + MARCH_BLOCK - 1) / MARCH_BLOCK);
-    const bool out = step_outputs || want_res;
-#define HF2D_MARCH(R, O, S)                                                                                 \
-  hipLaunchKernelGGL((hf2d_lean_march<R, O, S>), dim3(nw), dim3(MARCH_BLOCK), 0, st, P, L, G, m.sc, slot, slot_next, \
-                     serial, m.partials)
-    if (sg_now) {
-      if (want_res) HF2D_MARCH(true, true, true);
-      else if (out) HF2D_MARCH(false, true, true);
-      else HF2D_MARCH(false, false, true);
-    } else {
-      if (want_res) HF2D_MARCH(true, true, false);
-      else if (out) HF2D_MARCH(false, true, false);
-      else HF2D_MARCH(false, false, false);
-    }
-#undef HF2D_MARCH
-    HIP_CHECK(hipGetLastError());
-    npart = nw;
-    sbuf = 1 - sbuf;
-    dsbuf = 1 - dsbuf;
-    pbuf = 1 - pbuf;
-  } else if (euler && lean && lean_ok && lean_pipe > 0 && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
-    LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
-    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 1);
-    const int ntile = T.nbi * T.nbj;
-    const unsigned G = (unsigned)std::max(1, std::min(ntile, cu_count * lean_pipe));
-    const size_t shmem = (size_t)lean_tile_fields(sg_now) * T.NC * sizeof(real);
-    if (T.NC > PIPE_SLOTS * BLOCK) throw std::runtime_error("lean_pipe: tile larger than the staging slots");
-    const bool out = step_outputs || want_res;
-#define HF2D_PIPE(R, O, S)                                                                                   \
-  hipLaunchKernelGGL((hf2d_lean_pipe<R, O, S>), dim3(G), dim3(BLOCK), shmem, st, P, L, T, ntile, m.sc, slot, slot_next, \
-                     serial, m.partials)
-    if (sg_now) {
-      if (want_res) HF2D_PIPE(true, true, true);
-      else if (out) HF2D_PIPE(false, true, true);
-      else HF2D_PIPE(false, false, true);
-    } else {
-      if (want_res) HF2D_PIPE(true, true, false);
-      else if (out) HF2D_PIPE(false, true, false);
-      else HF2D_PIPE(false, false, false);
-    }
-#undef HF2D_PIPE
-    HIP_CHECK(hipGetLastError());
-    nres = G;
-    sbuf = 1 - sbuf;
-    dsbuf = 1 - dsbuf;
-    pbuf = 1 - pbuf;
-  } else if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
+  if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
     // two cells per thread unless that leaves fewer than ~2 workgroups per CU
     // (small strips of a multi-GPU run)
@@ -3328,14 +2669,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       }
       const bool parts = T.nbi >= 3;
       const unsigned ne = parts ? (unsigned)(2 * T.nbj) : ntile, ni = parts ? (unsigned)((T.nbi - 2) * T.nbj) : 0u;
-#define HF2D_PART(G, C, PART, NB)                                                                               \
-  hipLaunchKernelGGL((hf2d_lean_tile<false, false, G, 0, C>), dim3(NB), dim3(BLOCK), shmem, st, P, L, T, m.sc,  \
-                     slot, slot_next, serial, m.partials, PART)
-      const int p1 = parts ? 1 : 0;
-      if (sg && cpt == 2) HF2D_PART(true, 2, p1, ne);
-      else if (sg) HF2D_PART(true, 1, p1, ne);
-      else if (cpt == 2) HF2D_PART(false, 2, p1, ne);
-      else HF2D_PART(false, 1, p1, ne);
+      const TileK pk = kTile[sg][cpt - 1][0];
+      hipLaunchKernelGGL(pk, dim3(ne), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
+                         parts ? 1 : 0);
       HIP_CHECK(hipGetLastError());
       sbuf = 1 - sbuf;   // the new state is this step's output arrays
       dsbuf = 1 - dsbuf;
@@ -3343,13 +2679,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       HIP_CHECK(hipEventRecord(m.ev_edge, st));
       // interior tiles in flight before the (possibly host-blocking) exchange
       // is issued; they write neither the edge columns nor the ghost columns
-      if (ni > 0) {
-        if (sg && cpt == 2) HF2D_PART(true, 2, 2, ni);
-        else if (sg) HF2D_PART(true, 1, 2, ni);
-        else if (cpt == 2) HF2D_PART(false, 2, 2, ni);
-        else HF2D_PART(false, 1, 2, ni);
-      }
-#undef HF2D_PART
+      if (ni > 0)
+        hipLaunchKernelGGL(pk, dim3(ni), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
+                           2);
       HIP_CHECK(hipGetLastError());
       if (m.local) {
         // in-process group: the host orders the two streams (waits on it).
@@ -3372,52 +2704,21 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       r.async = true;
       return r;
     }
-#define HF2D_LEAN_TILE(R, O, G, C)                                                                                 \
-  do {                                                                                                               \
-    if (tile_trace && !R && !O && !fx_step)                                                                          \
-      hipLaunchKernelGGL((hf2d_lean_tile_tr<G, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,       \
-                         slot_next, serial, m.partials, tile_trace);                                                 \
-    else if (fx_step)                                                                                                \
-      hipLaunchKernelGGL((hf2d_lean_tile_fx<R, O, G, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
-                         slot_next, serial, m.partials, X);                                                          \
-    else                                                                                                             \
-      hipLaunchKernelGGL((hf2d_lean_tile<R, O, G, 0, C>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, \
-                         slot_next, serial, m.partials);                                                             \
-  } while (0)
-    // all variants of one step must use the cpt the tile geometry was built for
-    if (sg && cpt == 2) {
-      if (want_res)
-        HF2D_LEAN_TILE(true, true, true, 2);
-      else if (out)
-        HF2D_LEAN_TILE(false, true, true, 2);
-      else
-        HF2D_LEAN_TILE(false, false, true, 2);
-    } else if (sg) {
-      if (want_res)
-        HF2D_LEAN_TILE(true, true, true, 1);
-      else if (out)
-        HF2D_LEAN_TILE(false, true, true, 1);
-      else if (lean_occ == 6 && !fx_step && !tile_trace)
-        hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
-                           m.sc, slot, slot_next, serial, m.partials);
-      else
-        HF2D_LEAN_TILE(false, false, true, 1);
-    } else if (cpt == 2) {
-      if (want_res)
-        HF2D_LEAN_TILE(true, true, false, 2);
-      else if (out)
-        HF2D_LEAN_TILE(false, true, false, 2);
-      else
-        HF2D_LEAN_TILE(false, false, false, 2);
-    } else {
-      if (want_res)
-        HF2D_LEAN_TILE(true, true, false, 1);
-      else if (out)
-        HF2D_LEAN_TILE(false, true, false, 1);
-      else
-        HF2D_LEAN_TILE(false, false, false, 1);
-    }
-#undef HF2D_LEAN_TILE
+    // variant: 0 plain, 1 outputs, 2 residual (all variants of one step use
+    // the cpt the tile geometry was built for)
+    const int var = want_res ? 2 : out ? 1 : 0;
+    if (tile_trace && var == 0 && !fx_step)
+      hipLaunchKernelGGL(kTileTr[sg][cpt - 1], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
+                         serial, m.partials, tile_trace);
+    else if (fx_step)
+      hipLaunchKernelGGL(kTileFx[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
+                         slot_next, serial, m.partials, X);
+    else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace)
+      hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
+                         m.sc, slot, slot_next, serial, m.partials);
+    else
+      hipLaunchKernelGGL(kTile[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
+                         slot_next, serial, m.partials, 0);
     HIP_CHECK(hipGetLastError());
     nres = ntile;
     sbuf = 1 - sbuf;
@@ -3426,21 +2727,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   } else if (euler && lean && lean_ok) {
     const bool fromg = lean_state == 0;
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, fromg);
-    if (want_res) {
-      if (fromg)
-        hipLaunchKernelGGL((hf2d_lean_euler<true, true>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else
-        hipLaunchKernelGGL((hf2d_lean_euler<true, false>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
-    } else {
-      if (fromg)
-        hipLaunchKernelGGL((hf2d_lean_euler<false, true>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
-                           slot_next, serial, m.partials);
-      else
-        hipLaunchKernelGGL((hf2d_lean_euler<false, false>), dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc,
-                           slot, slot_next, serial, m.partials);
-    }
+    hipLaunchKernelGGL(kLeanEuler[want_res][fromg], dim3(nblk), dim3(BLOCK), 0, st, P, L, c0, c1, m.sc, slot,
+                       slot_next, serial, m.partials);
     HIP_CHECK(hipGetLastError());
     sbuf = 1 - sbuf;
     dsbuf = 1 - dsbuf;
@@ -3454,12 +2742,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     SoA in = m.view(h, sbuf, abuf, dsbuf, pbuf);
     SoA mid = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     SoA out = m.view(h, 1 - sbuf, 1 - abuf, 1 - dsbuf, pbuf);
-    if (want_res)
-      hipLaunchKernelGGL(hf2d_fused_euler<true>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, out, c0, c1, m.sc, slot,
-                         slot_next, serial, m.partials);
-    else
-      hipLaunchKernelGGL(hf2d_fused_euler<false>, dim3(nblk), dim3(BLOCK), 0, st, P, in, mid, out, c0, c1, m.sc, slot,
-                         slot_next, serial, m.partials);
+    hipLaunchKernelGGL(want_res ? hf2d_fused_euler<true> : hf2d_fused_euler<false>, dim3(nblk), dim3(BLOCK), 0, st,
+                       P, in, mid, out, c0, c1, m.sc, slot, slot_next, serial, m.partials);
     HIP_CHECK(hipGetLastError());
     abuf = 1 - abuf;
     dsbuf = 1 - dsbuf;
@@ -3482,26 +2766,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // ~173 VGPRs (2 waves/SIMD); a 3-wave budget is 11 % faster (resonator
       // 2000x200: 110.7 -> 98.8 us/step); the laminar one is best unbounded
       const int occ = lns_occ > 0 ? lns_occ : (t2 ? 3 : 0);
-#define HF2D_LNS(R, MD)                                                                                           \
-  do {                                                                                                            \
-    if (!R && occ == 5)                                                                                           \
-      hipLaunchKernelGGL((hf2d_lns_step_occ<R, MD, 5>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, \
-                         slot_next, serial, m.partials);                                                          \
-    else if (!R && occ == 3)                                                                                      \
-      hipLaunchKernelGGL((hf2d_lns_step_occ<R, MD, 3>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, \
-                         slot_next, serial, m.partials);                                                          \
-    else                                                                                                          \
-      hipLaunchKernelGGL((hf2d_lns_step<R, MD>), dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,        \
-                         slot_next, serial, m.partials);                                                          \
-  } while (0)
-      if (t2) {
-        if (want_res) HF2D_LNS(true, SK_SGT);
-        else HF2D_LNS(false, SK_SGT);
-      } else {
-        if (want_res) HF2D_LNS(true, SK_SGL);
-        else HF2D_LNS(false, SK_SGL);
-      }
-#undef HF2D_LNS
+      // (a residual step runs the compiler's register budget)
+      const LnsK lk = kLns[t2][want_res][want_res ? 0 : (occ == 5 ? 2 : occ == 3 ? 1 : 0)];
+      hipLaunchKernelGGL(lk, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial, m.partials);
       HIP_CHECK(hipGetLastError());
       nres = (unsigned)ntile;
       sbuf = 1 - sbuf;
@@ -3534,7 +2801,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   r.async = true;
   if (want_res) {
     hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials,
-                       npart >= 0 ? npart : (long)nres * (BLOCK / WAVE), m.res_out);
+                       (long)nres * (BLOCK / WAVE), m.res_out);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(m.res_host, m.res_out, sizeof(ResidualPack), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));

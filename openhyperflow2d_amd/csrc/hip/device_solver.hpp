@@ -132,10 +132,8 @@ class DeviceSolver : public SolverBase {
   int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
   int lean_wgcu = 0;       // >0: at most this many tile workgroups resident per CU (LDS request)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
-  int lean_cpt = 2;
-  int lean_march = 0;
-  int lean_pipe = 0;       // > 0: software-pipelined persistent tile kernel, this many workgroups per CU      // > 0: register-marching kernel with chunks of this many columns
-  int cu_count = 256;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
+  int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
+  int cu_count = 256;
   bool lean_sg_ok = false;
   bool lean_has_cauchy_x = true;   // some node reads dS/dx of an x neighbour (halo must carry it)
   void set_lean_plain(bool on);
@@ -178,19 +176,6 @@ class DeviceSolver : public SolverBase {
   bool use_graph = true;
   long graph_launches = 0;
   void flush_pending();
-  // persistent multi-step lean kernel (hf2d_lean_persist): windows of up to
-  // persist_steps plain steps in one cooperative launch.  Off by default:
-  // bitwise equal but 3-5x slower per step than the per-step tile kernel on
-  // MI355X (profiles/persistent_kernel_trace.md)
-  int lean_persist = 0;
-  int persist_steps = 48;
-  long persist_launches = 0;
-  std::string persist_why;   // why the persistent kernel was disabled ("" if it was not)
-  // phase trace of one 8-step window: per tile and step [start, computed,
-  // committed, barrier passed, halo loaded, XCC_ID] (s_memrealtime, 100 MHz)
-  std::vector<unsigned long long> persist_trace(int steps = 8);
-  unsigned long long* persist_trace_buf = nullptr;
-  int persist_trace_tiles = 0;
 
  private:
   struct Impl;
@@ -198,10 +183,8 @@ class DeviceSolver : public SolverBase {
   struct GraphCache;
   std::unique_ptr<GraphCache> graph;
   std::vector<StepParams> pending;
-  bool pending_persist = false;   // `pending` holds a persistent window (else a graph window)
   void run_graph();
-  bool persist_eligible() const;
-  void run_persist();
+  uint64_t mode_signature() const;   // kernel-selecting state (graph windows replay only under the same)
   void step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk, bool to_lns);
   bool lns_step_ok(const StepParams& P) const;
   bool lns_entry(const StepParams& P0) const;

@@ -13,8 +13,6 @@ FIELDS = ["rho", "U", "V", "p", "T"]
 MODES = {
     "lean_tile": dict(lean=True, lean_tile=True),
     "lean_tile_nosg": dict(lean=True, lean_tile=True, lean_sg=False),
-    "lean_march": dict(lean=True, lean_tile=True, lean_march=8),
-    "lean_march3_nosg": dict(lean=True, lean_tile=True, lean_march=3, lean_sg=False),
     "lean_flat": dict(lean=True, lean_tile=False),
     "fused": dict(lean=False, fused=True),
     "split": dict(lean=False, fused=False),
@@ -25,11 +23,9 @@ def _gpu_sim(hf, text, mode):
     kw = dict(MODES[mode])
     tile = kw.pop("lean_tile", True)
     sg = kw.pop("lean_sg", True)
-    march = kw.pop("lean_march", 0)
     g = hf.Simulation(text, "gpu", **kw)
     g.solver.lean_tile = tile
     g.solver.lean_sg = sg
-    g.solver.lean_march = march
     return g
 
 
@@ -390,43 +386,6 @@ def test_rccl_single_rank_comm(gpu, tmp_path):
     assert any(p.suffix == ".plt" for p in tmp_path.iterdir())
 
 
-@pytest.mark.parametrize("deck,march,sg", [("wedge", 8, True), ("wedge", 3, True), ("step", 5, True),
-                                           ("triple_point", 4, False), ("oblique", 16, True),
-                                           ("wedge", -1, True), ("step", -2, True), ("triple_point", -1, False),
-                                           ("oblique", -4, True)])
-def test_march_kernel_bitwise_equals_tile(gpu, deck, march, sg):
-    """Register-marching (hf2d_lean_march) and software-pipelined
-    (hf2d_lean_pipe) lean kernels == LDS-tiled lean kernel bit for bit: same lean_cell() arithmetic, neighbours from
-    registers / lane shuffles instead of LDS (incl. strips whose column count
-    is not a multiple of the chunk, and the multi-gas non-SG path)."""
-    from tests.conftest import read_deck
-
-    if deck == "wedge":
-        text = decks.wedge15(301, 67, nmax=10 ** 6, nout=10 ** 5)
-    elif deck == "step":
-        text = read_deck("Step.dat")
-    elif deck == "oblique":
-        text = read_deck("ObliqueShock.dat")
-    else:
-        text = decks.triple_point(210, 90, nmax=10 ** 6, nout=10 ** 5)
-    a = gpu.Simulation(text, "gpu")
-    b = gpu.Simulation(text, "gpu")
-    for s in (a, b):
-        s.solver.lean_sg = sg
-    if march > 0:
-        b.solver.lean_march = march
-    else:   # negative: software-pipelined persistent kernel with -march workgroups per CU
-        b.solver.lean_pipe = -march
-    for n, res in [(3, True), (24, False), (5, True), (13, False)]:
-        a.step(n, residual=res)
-        b.step(n, residual=res)
-    assert b.solver.lean_ok
-    assert a.summary()["dt"] == b.summary()["dt"]
-    # residual sums are accumulated per wave instead of per workgroup
-    np.testing.assert_allclose(a.summary()["rms"], b.summary()["rms"], rtol=1e-12, atol=0)
-    assert a.records() == b.records()
-
-
 @pytest.mark.parametrize("deck", ["step", "step_ref_ns", "step_graphs", "resonator", "resonator_graphs"])
 def test_lean_ns_equals_split(gpu, deck):
     """Lean laminar N-S kernel (hip/lean_ns.hpp: fluxes recomputed in the LDS
@@ -544,29 +503,4 @@ def test_autotune_thread_block_size_zero(gpu, monkeypatch):
     assert a.summary()["dt"] == b.summary()["dt"] and a.summary()["iteration"] == b.summary()["iteration"]
     assert a.summary()["time"] == b.summary()["time"]
     for f in FIELDS:
-        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
-
-
-@pytest.mark.parametrize("nx,ny,steps", [(2000, 200, 101), (300, 64, 57)])
-def test_persistent_window_kernel_matches_per_step(gpu, nx, ny, steps):
-    """hf2d_lean_persist (one cooperative launch per window of plain steps,
-    tile state resident in LDS, grid barrier per step) == the per-step tile
-    kernel, bit for bit, including dt and the accumulated time."""
-    text = decks.wedge15(nx, ny, nmax=10 ** 6, nout=10 ** 5)
-    a = gpu.Simulation(text, "gpu", lean=True)
-    b = gpu.Simulation(text, "gpu", lean=True)
-    a.solver.lean_persist = 1   # opt-in (slower than the per-step kernel, see its docstring)
-    b.solver.lean_persist = 0
-    n0 = (a.solver.persist_launches, b.solver.persist_launches)   # (the autotuner may have stepped)
-    for sim in (a, b):
-        sim.step(3)                  # generic -> lean hand-over outside the window
-        sim.step(steps, residual=True)
-    assert a.solver.persist_launches > n0[0], a.solver.persist_why
-    assert b.solver.persist_launches == n0[1]
-    sa, sb = a.summary(), b.summary()
-    assert sa["dt"] == sb["dt"] and sa["time"] == sb["time"]
-    # (the residual partials are summed per tile: the two solvers' autotuned
-    # tile shapes may differ, so the sums may differ in the last bit)
-    np.testing.assert_allclose(np.array(sa["rms"]), np.array(sb["rms"]), rtol=1e-12, atol=0)
-    for f in FIELDS + ["mach"]:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)

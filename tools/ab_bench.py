@@ -33,10 +33,6 @@ def main():
             s.solver.use_graph = False
         elif v0 == "nosg":
             s.solver.lean_sg = False
-        elif v0.startswith("pipe"):
-            s.solver.lean_pipe = int(v0[4:])
-        elif v0.startswith("march"):
-            s.solver.lean_march = int(v0[5:])
         elif v0.startswith("cpt"):
             s.solver.lean_cpt = int(v0[3:])
         elif v0.startswith("occ"):
