@@ -24,7 +24,9 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("HF2D_OFFLOAD_ARCH", "gfx950")
 
 CORE_SRCS = ["deck.cpp", "gasdyn.cpp", "config.cpp", "preprocess.cpp", "checkpoint.cpp", "postproc.cpp", "stripio.cpp", "tcpcomm.cpp", "solver.cpp", "lean.cpp", "mechanism.cpp"]
-HIP_SRCS = ["device_solver.hip", "chem_mech.hip", "chem_fast.hip"]
+HIP_SRCS = ["device_solver.hip", "chem_mech.hip", "chem_fast.hip", "chem_rtc.hip"]
+# headers handed to hiprtc by chem_rtc.hip (embedded as string literals)
+RTC_EMBED = [("kChemTypesSrc", "chem_fast_types.hpp"), ("kChemDevSrc", "chem_fast_dev.hpp")]
 
 
 def ext_path() -> str:
@@ -46,9 +48,10 @@ def _ninja_file() -> str:
         "ninja_required_version = 1.5",
         f"hipcc = {hipcc}",
         f"cxxflags = {common} -x c++ -I{CSRC}",
-        f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC}",
+        f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC} -I{os.path.abspath(BUILD)}",
         f"pyflags = -I{_pybind_include()} -I{py_inc}",
-        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx",
+        f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lhiprtc -lrccl -lrocprofiler-sdk-roctx",
+        f"python = {sys.executable}",
         "rule cxx",
         "  command = $hipcc $cxxflags $extra -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -76,6 +79,10 @@ def _ninja_file() -> str:
         "rule link_gxx_asan",
         "  command = g++ -fsanitize=address,undefined $in -o $out",
     ]
+    lines.append("rule embed")
+    lines.append(f"  command = $python {os.path.abspath(__file__)} --embed $out $in")
+    emb = os.path.join(os.path.abspath(BUILD), "chem_rtc_embed.inc")
+    lines.append(f"build {emb}: embed " + " ".join(os.path.join(CSRC, "hip", f) for _, f in RTC_EMBED))
     objs = []
     for s in CORE_SRCS:
         o = f"core_{s[:-4]}.o"
@@ -84,7 +91,7 @@ def _ninja_file() -> str:
     hobjs = []
     for s in HIP_SRCS:
         o = f"hip_{s[:-4]}.o"
-        lines.append(f"build {o}: hip {os.path.join(CSRC, 'hip', s)}")
+        lines.append(f"build {o}: hip {os.path.join(CSRC, 'hip', s)}" + (f" || {emb}" if s == "chem_rtc.hip" else ""))
         hobjs.append(o)
     lines.append(f"build bind_module.o: cxx {os.path.join(CSRC, 'bind', 'module.cpp')}")
     lines.append("  extra = $pyflags")
@@ -154,5 +161,23 @@ def is_built() -> bool:
     return all(os.path.exists(p) for p in (ext_path(), os.path.join(bindir, "hf2d"), os.path.join(bindir, "hf2d_cpu")))
 
 
+def embed(out: str, inputs) -> None:
+    """chem_rtc_embed.inc: the RTC_EMBED headers as raw string literals."""
+    names = dict((f, v) for v, f in RTC_EMBED)
+    parts = ["// generated by _build.py from %s -- do not edit" % ", ".join(os.path.basename(i) for i in inputs)]
+    for path in inputs:
+        text = open(path).read()
+        if ")HF2DRTC\"" in text:
+            raise RuntimeError("embed delimiter found in " + path)
+        parts.append('static const char %s[] = R"HF2DRTC(%s)HF2DRTC";' % (names[os.path.basename(path)], text))
+    data = "\n".join(parts) + "\n"
+    if not os.path.exists(out) or open(out).read() != data:
+        with open(out, "w") as f:
+            f.write(data)
+
+
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    if len(sys.argv) > 1 and sys.argv[1] == "--embed":
+        embed(sys.argv[2], sys.argv[3:])
+    else:
+        print(build(verbose="-v" in sys.argv))

@@ -14,6 +14,7 @@
 #include "../core/solver.hpp"
 #include "../hip/chem_mech.hpp"
 #include "../hip/chem_fast.hpp"
+#include "../hip/chem_rtc.hpp"
 #include "../hip/device_solver.hpp"
 
 namespace py = pybind11;
@@ -535,6 +536,47 @@ PYBIND11_MODULE(_hf2d, m) {
     }
     return py::make_tuple(y, Tout, ms);
   });
+  // run-time specialised kinetics (chem_rtc.hip): name = built-in name, *.mech path or mechanism text
+  auto mech_of = [](const std::string& name) {
+    return name.find('\n') == std::string::npos ? load_mechanism(name) : parse_mechanism(name);
+  };
+  m.def("mech_struct_source", [mech_of](const std::string& name) { return mech_struct_source(mech_of(name)->data); });
+  m.def("chem_rtc_program", [mech_of](const std::string& name) { return chem_rtc_program(mech_of(name)->data); });
+  m.def("chem_rtc_cache_dir", &chem_rtc_cache_dir);
+  m.def("chem_rtc_compile", [mech_of](const std::string& name) {
+    // hiprtc compile of the mechanism's kernels (host only): (code bytes, cached, log)
+    std::string why;
+    bool cached = false;
+    long n;
+    {
+      auto mi = mech_of(name);
+      py::gil_scoped_release nogil;
+      n = chem_rtc_compile(mi->data, &why, &cached);
+    }
+    return py::make_tuple(n, cached, why);
+  });
+  m.def("chem_rtc_run", [mech_of](const std::string& name, py::array_t<double, py::array::c_style | py::array::forcecast> rhoY,
+                                  py::array_t<double, py::array::c_style | py::array::forcecast> rho,
+                                  py::array_t<double, py::array::c_style | py::array::forcecast> e,
+                                  py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub,
+                                  int repeats) {
+    // hiprtc-specialised kinetics kernel on the GPU: returns (rhoY, T, mean ms, code object was cached)
+    auto mi = mech_of(name);
+    const long n = (long)rho.size();
+    if (rhoY.ndim() != 2 || rhoY.shape(0) != mi->data.ns || rhoY.shape(1) != n || e.size() != n || T.size() != n)
+      throw std::runtime_error("chem_rtc_run: shapes [ns, n], [n], [n], [n]");
+    py::array_t<double> y({(long)rhoY.shape(0), n});
+    std::memcpy(y.mutable_data(), rhoY.data(), sizeof(double) * rhoY.size());
+    py::array_t<double> Tout(n);
+    std::memcpy(Tout.mutable_data(), T.data(), sizeof(double) * n);
+    double ms;
+    {
+      py::gil_scoped_release nogil;
+      ms = chem_rtc_run_host(mi->data, y.mutable_data(), rho.data(), e.data(), Tout.mutable_data(), n, dt, nsub,
+                             repeats);
+    }
+    return py::make_tuple(y, Tout, ms, chem_rtc_last_cached());
+  });
   m.def("mech_thermo_host", [](const std::string& name, std::vector<double> Y, double T) {
     auto mi = load_mechanism(name);
     double e, cv, R, cp, mu, lam;
@@ -621,6 +663,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
       .def_readwrite("chem_fast", &DeviceSolver::chem_fast)
       .def_readwrite("chem_kernel", &DeviceSolver::chem_kernel)
+      .def_readwrite("chem_rtc", &DeviceSolver::chem_rtc)
+      .def_readonly("chem_rtc_ok", &DeviceSolver::chem_rtc_ok)
+      .def_readonly("chem_rtc_why", &DeviceSolver::chem_rtc_why)
       .def_readonly("chem_kernel_used", &DeviceSolver::chem_kernel_used)
       .def_readonly("chem_fast_ok", &DeviceSolver::chem_fast_ok)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)

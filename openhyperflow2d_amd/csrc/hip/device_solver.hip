@@ -39,6 +39,7 @@
 #include "device_solver.hpp"
 #include "dev_common.hpp"
 #include "chem_fast.hpp"
+#include "chem_rtc.hpp"
 #include "chem_mech.hpp"
 #include "lean_ns.hpp"
 
@@ -1380,6 +1381,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_SPLIT_XCD")) split_xcd = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_SPLIT_XCD_MECH")) split_xcd_mech = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_MECH_LAZY")) mech_lazy = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_CHEM_KERNEL")) chem_kernel = std::atoi(e);   // 1 compiled 2 MFMA 3 generic 4 hiprtc
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
@@ -1550,6 +1552,10 @@ void DeviceSolver::upload() {
   cp(m.gf, h.gf.data(), N);
   chem_fast_ok = cs.cfg.mech_mode() && chem_fast_available(cs.cfg.mech->name) &&
                  mech_is_builtin(*cs.cfg.mech, cs.cfg.mech->name);
+  chem_rtc_ok = false;
+  chem_rtc_why.clear();
+  if (cs.cfg.mech_mode() && (chem_kernel == 4 || (chem_kernel == 0 && !chem_fast_ok && chem_rtc)))
+    chem_rtc_ok = chem_rtc_prepare(*cs.cfg.mech->data_ptr(), &chem_rtc_why);   // compile now, not in a step graph
   lean_ok = lean_eligible(cs, &lean_why);
   sk_mode = sk_eligible(cs, &sgl_why);
   sgl_ok = sk_mode != SK_GENERIC;
@@ -2816,7 +2822,19 @@ void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& o
   Impl& m = *impl;
   const real* Tprev = m.Tg[pbuf];
   const MechData& md = *cs.cfg.mech->data_ptr();
-  const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : 2);
+  const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : (chem_rtc && chem_rtc_ok) ? 4 : 2);
+  if (kind == 4) {
+    if (!chem_rtc_ok) throw std::runtime_error("chem_kernel=4: hiprtc kernels unavailable: " + chem_rtc_why);
+    if (chem_compact && !m.chem_list) {
+      m.chem_list = m.mem.alloc<int>(h.N);
+      m.chem_count = m.mem.alloc<unsigned>(1);
+    }
+    if (!chem_rtc_launch(md, mid, out, Tprev, k0, k1, m.sc, slot, md.Tchem, md.nsub, m.stream,
+                         chem_compact ? m.chem_list : nullptr, chem_compact ? m.chem_count : nullptr))
+      throw std::runtime_error("hf2d_rtc_chem launch failed");
+    chem_kernel_used = "hf2d_rtc_chem";
+    return;
+  }
   // compiled mechanism: register-resident VALU kernel (chem_fast.hip)
   if (kind == 1) {
     if (!chem_fast_ok) throw std::runtime_error("chem_kernel=1: no compiled kernel for mechanism " + cs.cfg.mech->name);

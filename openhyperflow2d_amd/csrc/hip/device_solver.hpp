@@ -142,10 +142,17 @@ class DeviceSolver : public SolverBase {
   bool chem_fast = true;  // mechanism mode: compiled-mechanism kinetics kernel when one exists
   bool chem_fast_ok = false;   // the loaded mechanism equals a compiled one
   bool chem_compact = true;    // compiled kinetics over a compacted list of the reacting cells
-  // kinetics kernel: 0 auto (compiled VALU kernel if the mechanism has one, else
-  // the MFMA kernel), 1 compiled, 2 MFMA, 3 generic runtime-data VALU
+  // kinetics kernel: 0 auto (compiled VALU kernel if the mechanism has one,
+  // else the hiprtc-specialised one, else the MFMA kernel), 1 compiled, 2 MFMA,
+  // 3 generic runtime-data VALU, 4 hiprtc-specialised
   int chem_kernel = 0;
   std::string chem_kernel_used;
+  // a mechanism without built-in kernels: hiprtc-specialised chem_fast kernels
+  // (chem_rtc.hip, compiled at upload, code object cached) instead of the
+  // runtime-data MFMA kernel; kernel kind 4
+  bool chem_rtc = true;
+  bool chem_rtc_ok = false;
+  std::string chem_rtc_why;
   bool sgl = true;        // single-gas laminar N-S specialisation (stepkern.hpp fill_cell<SGL>) if eligible
   bool sgl_ok = false;
   int sk_mode = 0;        // SK_GENERIC / SK_SGL / SK_SGT (stepkern.hpp)
