@@ -275,6 +275,46 @@ PYBIND11_MODULE(_hf2d, m) {
         return c.cfg.mech ? c.cfg.mech->species : std::vector<std::string>{};
       })
       .def_property_readonly("mech_name", [](const Case& c) { return c.cfg.mech ? c.cfg.mech->name : std::string(); })
+      .def("pack_strip",
+           [](const Case& c, int a, int b) {
+             std::string blob;
+             {
+               py::gil_scoped_release nogil;
+               blob = c.pack_strip(a, b);
+             }
+             return py::bytes(blob);
+           },
+           py::arg("a"), py::arg("b"),
+           "rank 0 of a strip run: the per-case data and columns [a, b) as bytes (Case.unpack_strip)")
+      .def_static(
+          "unpack_strip",
+          [](py::buffer b) {
+            // any contiguous byte buffer (bytes, numpy uint8): read in place, no copy
+            const py::buffer_info bi = b.request();
+            return std::make_shared<Case>(
+                Case::unpack_strip((const char*)bi.ptr, (size_t)bi.size * (size_t)bi.itemsize, nullptr));
+          },
+          "the strip Case of a pack_strip blob (columns [a, b) resident; no pre-processing)")
+      .def("pack_strip_header", [](const Case& c, int a, int b) { return py::bytes(c.pack_strip_header(a, b)); })
+      .def("strip_payload_bytes", &Case::strip_payload_bytes)
+      .def("read_strip_payload",
+           [](const Case& c, int a, int b, size_t off, py::buffer dst) {
+             const py::buffer_info bi = dst.request(true);
+             c.read_strip_payload(a, b, off, (char*)bi.ptr, (size_t)bi.size * (size_t)bi.itemsize);
+           })
+      .def_static("unpack_strip_header",
+                  [](py::buffer b) {
+                    const py::buffer_info bi = b.request();
+                    return std::make_shared<Case>(
+                        Case::unpack_strip_header((const char*)bi.ptr, (size_t)bi.size * (size_t)bi.itemsize));
+                  })
+      .def("write_strip_payload",
+           [](Case& c, size_t off, py::buffer src) {
+             const py::buffer_info bi = src.request();
+             c.write_strip_payload(off, (const char*)bi.ptr, (size_t)bi.size * (size_t)bi.itemsize);
+           })
+      .def("compute_facts", &Case::compute_facts)
+      .def_property_readonly("facts_valid", [](const Case& c) { return c.facts.valid; })
       .def("trim_to_columns", &Case::trim_to_columns, py::arg("a"), py::arg("b"),
            "strip rank: keep only columns [a, b) of the host field resident (after the solver uploaded its strip)")
       .def_property_readonly("resident_columns", [](const Case& c) { return py::make_tuple(c.J.i0, c.J.i0 + c.J.nxl); })

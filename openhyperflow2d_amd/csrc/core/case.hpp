@@ -113,6 +113,18 @@ struct Field {
   void trim(int a, int b);
 };
 
+// Whole-field eligibility of the specialised steppers (lean.cpp), evaluated
+// on the full pre-processed field: a strip rank that never held it
+// (Case::unpack_strip) uses these, so every rank takes the same kernel path.
+struct CaseFacts {
+  bool valid = false;
+  bool lean_ok = false;
+  std::string lean_why;
+  int sk_mode = 0;
+  std::string sk_why;
+  bool single_gas = false, any_cauchy_x = false, species_cauchy = false;
+};
+
 class Case {
  public:
   Config cfg;
@@ -135,6 +147,23 @@ class Case {
   // Strip ranks: keep only the columns [a, b) of J and mech_rhoY resident
   // (after the backend uploaded its strip; host RSS then scales with the strip)
   void trim_to_columns(int a, int b);
+  CaseFacts facts;
+
+  // Strip scatter (case_io.cpp; the reference pre-processes on rank 0 and
+  // sends each rank its subdomain, hf2d_start.cpp:143-205): the per-case data
+  // and the columns [a, b) of a whole Case as bytes, and the strip Case of
+  // such a blob (columns [a, b) resident, facts of the whole field).
+  void compute_facts();
+  std::string pack_strip(int a, int b) const;
+  static Case unpack_strip(const std::string& blob, std::ostream* log = nullptr);
+  static Case unpack_strip(const char* data, size_t size, std::ostream* log = nullptr);
+  // the same in pieces (the payload -- records, then species -- sent in
+  // chunks straight into the receiving Case: no whole-strip buffer)
+  std::string pack_strip_header(int a, int b) const;
+  size_t strip_payload_bytes(int a, int b) const;
+  void read_strip_payload(int a, int b, size_t off, char* dst, size_t n) const;
+  static Case unpack_strip_header(const char* data, size_t size, std::ostream* log = nullptr, size_t* used = nullptr);
+  void write_strip_payload(size_t off, const char* src, size_t n);
 
   // Build the whole problem from a deck.  workdir is where <Project>.hf2d is
   // looked up; checkpoint=false ignores any existing swap file.

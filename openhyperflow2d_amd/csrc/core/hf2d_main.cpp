@@ -19,6 +19,7 @@
 // into balanced strips and run the same driver; every rank writes its share
 // of the outputs (stripio.hpp).  The reference does the same with MPI inside
 // main (hf2d_start.cpp:79-289).
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -82,13 +83,44 @@ int main(int argc, char** argv) {
       device = deck.get_int_or("isSingleGPU", 0) ? deck.get_int_or("ActiveSingleGPU", 0) : 0;
       if (env.world > 1) device = env.local_rank;   // one GPU per local rank
     }
-    Case cs = Case::from_deck(deck, outdir, use_ckpt, root ? &std::cout : nullptr);
-    if (serial) cs.cfg.semantics = Semantics::SERIAL;
+    // Multi-rank: rank 0 pre-processes the deck once and sends every rank its
+    // strip (its columns + one ghost column each side, case_io.cpp), as the
+    // reference's rank 0 does (hf2d_start.cpp:143-205); no other rank builds
+    // the whole field
+    Case cs;
+    std::vector<std::pair<int, int>> parts;
+    if (env.world > 1) {
+      std::string my_blob, ptxt;
+      if (root) {
+        Case full = Case::from_deck(deck, outdir, use_ckpt, &std::cout);
+        if (serial) full.cfg.semantics = Semantics::SERIAL;
+        parts = balanced_columns(full.J, env.world);
+        for (const auto& p : parts) ptxt += std::to_string(p.first) + " " + std::to_string(p.second) + " ";
+        auto strip = [&](int r) {
+          return full.pack_strip(std::max(parts[r].first - 1, 0), std::min(parts[r].second + 1, full.J.nx));
+        };
+        tcp->broadcast(ptxt, 0);
+        for (int r = 1; r < env.world; r++) tcp->send_to(r, strip(r));
+        my_blob = strip(0);
+      } else {
+        ptxt = tcp->broadcast(std::string(), 0);
+        my_blob = tcp->recv_from_root();
+      }
+      if (!root) {
+        std::istringstream ps(ptxt);
+        int a, b;
+        while (ps >> a >> b) parts.push_back({a, b});
+      }
+      cs = Case::unpack_strip(my_blob, nullptr);
+    } else {
+      cs = Case::from_deck(deck, outdir, use_ckpt, &std::cout);
+      if (serial) cs.cfg.semantics = Semantics::SERIAL;
+      parts = balanced_columns(cs.J, 1);
+    }
     out << "X=" << cs.cfg.MaxX << "  Y=" << cs.cfg.MaxY << "  dx=" << cs.cfg.dx << "  dy=" << cs.cfg.dy << "\n";
     out << "\nInitial dt=" << cs.dt0 << "sec.\n";
     out << "\nSolver Mode: " << (cs.cfg.ProblemType == SM_NS ? "Navier-Stokes" : "Euler") << "/FP64\n\n";
     if (backend.empty()) backend = (gpu_available && gpu_available()) ? "gpu" : "cpu";
-    const auto parts = balanced_columns(cs.J, env.world);
     const int gi0 = parts[env.rank].first, gi1 = parts[env.rank].second;
     std::unique_ptr<SolverBase> solver;
     std::string used = "none";
@@ -120,10 +152,7 @@ int main(int argc, char** argv) {
         used = "tcp";
       }
     }
-    if (env.world > 1) {
-      cs.trim_to_columns(gi0 - 1, gi1 + 1);   // host keeps the strip and its ghost columns
-      out << "Ranks: " << env.world << " strips, halo transport " << used << "\n";
-    }
+    if (env.world > 1) out << "Ranks: " << env.world << " strips, halo transport " << used << "\n";
     out << "Start computation (" << backend << " backend)...\n" << std::flush;
     install_signal_handlers();
     RunOptions opt;

@@ -10,6 +10,10 @@
 namespace hf2d {
 
 bool lean_eligible(const Case& cs, std::string* why) {
+  if (!cs.J.whole() && cs.facts.valid) {   // strip rank: the whole field's answer
+    if (why) *why = cs.facts.lean_why;
+    return cs.facts.lean_ok;
+  }
   auto no = [&](const char* w) {
     if (why) *why = w;
     return false;
@@ -41,6 +45,10 @@ bool lean_eligible(const Case& cs, std::string* why) {
 // chemistry on) R = R_air everywhere -- then the generic stepper leaves every
 // skipped field unchanged.
 int sk_eligible(const Case& cs, std::string* why) {
+  if (!cs.J.whole() && cs.facts.valid) {
+    if (why) *why = cs.facts.sk_why;
+    return cs.facts.sk_mode;
+  }
   auto no = [&](const char* w) {
     if (why) *why = w;
     return (int)SK_GENERIC;
@@ -75,6 +83,7 @@ int sk_eligible(const Case& cs, std::string* why) {
 }
 
 bool mech_species_cauchy(const Case& cs) {
+  if (!cs.J.whole() && cs.facts.valid) return cs.facts.species_cauchy;
   for (const CellRecord& c : cs.J.c) {
     if (!is_active(c.CT)) continue;
     const EqFlags f = eq_flags(I_YFU, c.CT, c.TurbType, cs.cfg.ProblemType);
@@ -84,6 +93,7 @@ bool mech_species_cauchy(const Case& cs) {
 }
 
 bool lean_single_gas(const Case& cs) {
+  if (!cs.J.whole() && cs.facts.valid) return cs.facts.single_gas;
   static const real zero = 0.0;
   for (const CellRecord& c : cs.J.c)
     for (int k = 4; k < 4 + NCOMP; k++)
@@ -92,6 +102,7 @@ bool lean_single_gas(const Case& cs) {
 }
 
 bool lean_any_cauchy_x(const Case& cs) {
+  if (!cs.J.whole() && cs.facts.valid) return cs.facts.any_cauchy_x;
   for (const CellRecord& c : cs.J.c) {
     if (!is_active(c.CT)) continue;
     for (int k = 0; k < NEQ; k++)

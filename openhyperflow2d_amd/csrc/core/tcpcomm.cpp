@@ -245,6 +245,16 @@ std::vector<std::string> TcpComm::allgather_bytes(const std::string& mine) {
   return all;
 }
 
+void TcpComm::send_to(int rank, const std::string& s) {
+  if (r_ != 0 || rank <= 0 || rank >= n_) throw std::runtime_error("TcpComm::send_to: rank 0 to a rank >= 1 only");
+  send_blob(ctrl_[rank], s);
+}
+
+std::string TcpComm::recv_from_root() {
+  if (r_ == 0) throw std::runtime_error("TcpComm::recv_from_root on rank 0");
+  return recv_blob(ctrl_[0]);
+}
+
 std::string TcpComm::broadcast(const std::string& s, int root) {
   const auto all = allgather_bytes(r_ == root ? s : std::string());
   return all[root];

@@ -39,6 +39,9 @@ class TcpComm : public Comm {
   void allreduce_residual(ResidualPack& p) override;
   std::vector<std::string> allgather_bytes(const std::string& mine) override;
   std::string broadcast(const std::string& s, int root = 0);
+  // point-to-point with rank 0 over the control connection (strip scatter)
+  void send_to(int rank, const std::string& s);   // rank 0 only
+  std::string recv_from_root();                    // ranks >= 1
 
   // Full-duplex exchange with the strip neighbours (either side may be
   // absent: pass nbytes 0).  Sends and receives proceed together, so
