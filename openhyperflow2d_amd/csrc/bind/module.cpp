@@ -716,6 +716,13 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("sk_mode", &DeviceSolver::sk_mode)
       .def_readonly("lean_sg_ok", &DeviceSolver::lean_sg_ok)
       .def_readonly("lean_has_cauchy_x", &DeviceSolver::lean_has_cauchy_x)
+      .def_readwrite("halo_compact", &DeviceSolver::halo_compact)
+      .def_readonly("any_cauchy_x", &DeviceSolver::any_cauchy_x)
+      .def("halo_field_count", [](const DeviceSolver& d, int group, bool full) {
+        std::vector<real*> f;
+        d.halo_fields(group, f, full);
+        return (int)f.size();
+      }, py::arg("group"), py::arg("full") = false)
       .def_property("lean_plain", [](const DeviceSolver& d) { return d.lean_plain; },
                     [](DeviceSolver& d, bool on) { d.set_lean_plain(on); })
       .def_readonly("lean_ok", &DeviceSolver::lean_ok)

@@ -1605,7 +1605,9 @@ void DeviceSolver::upload() {
     cbuf = 0;
   }
   lean_sg_ok = lean_ok && lean_single_gas(cs);
-  lean_has_cauchy_x = lean_ok && lean_any_cauchy_x(cs);
+  any_cauchy_x = lean_any_cauchy_x(cs);
+  lean_has_cauchy_x = lean_ok && any_cauchy_x;
+  ghost_mode = -1;
   if (lean_ok) {
     lean_bytes = lean_flags(h, cs.cfg.ProblemType);
     if (!lean_plain)
@@ -2099,10 +2101,16 @@ int DeviceSolver::comm_size() const { return impl->nranks; }
 // and unpack folds the MIN in -- one grouped p2p launch per step instead of a
 // send/recv group plus an all-reduce.
 // device columns of the fields a halo group carries (pack order)
-void DeviceSolver::halo_fields(int group, std::vector<real*>& f) const {
+int DeviceSolver::split_mode() const {
+  return impl->mech ? SK_MECH : (cs.cfg.ProblemType == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+}
+
+void DeviceSolver::halo_fields(int group, std::vector<real*>& f, bool full) const {
   const Impl& m = *impl;
   const long N = h.N;
   f.clear();
+  full = full || !halo_compact;
+  const int mode = split_mode();
   auto add_eq = [&](real* base) {
     for (int k = 0; k < NEQ; k++) f.push_back(base + (long)k * N);
   };
@@ -2118,15 +2126,30 @@ void DeviceSolver::halo_fields(int group, std::vector<real*>& f) const {
     f.push_back(m.P2[pbuf]);
     if (lean_has_cauchy_x) add_eq(m.dSdx[dsbuf]);
   } else if (group == CpuSolver::HALO_MID) {
-    add_eq(m.S[1 - sbuf]);
+    // the predicted state as the N-S fill reads it of an x neighbour
+    // (stepkern.hpp fill_compute: Sn of rho, the species slots, k and eps);
+    // mechanism strips also react their ghost columns, which reads rho, rhoU,
+    // rhoV and rhoE (chem_fast_dev.hpp chem_cell)
+    for (int k = 0; k < NEQ; k++)
+      if (full || k == 0 || (mode == SK_MECH && k < 4) || (k >= 4 && sk_live(mode, k)))
+        f.push_back(m.S[1 - sbuf] + (long)k * N);
     for (int q = 0; q < m.nsp; q++) f.push_back(m.Ys[1 - sbuf] + (long)q * N);
   } else if (group == CpuSolver::HALO_QDIR) {
     for (int d = 0; d < 4; d++) f.push_back(m.qdir + (long)d * N);
   } else {
-    add_eq(m.S[sbuf]);
-    add_eq(m.A[abuf]);
-    add_eq(m.B[abuf]);
-    add_eq(m.dSdx[dsbuf]);
+    // what the next split step reads of a ghost column: the predictor's S
+    // and x flux A of the live equations (stepkern.hpp predict_core: SL/SR,
+    // AL/AR; the y flux B only along the own column), dS/dx only where a node
+    // applies d2/dx2 = 0, the fill's previous U/V/T and the wall heat flux's
+    // conductivities; the mechanism species block likewise
+    for (int k = 0; k < NEQ; k++)
+      if (full || sk_live(mode, k)) f.push_back(m.S[sbuf] + (long)k * N);
+    for (int k = 0; k < NEQ; k++)
+      if (full || sk_live(mode, k)) f.push_back(m.A[abuf] + (long)k * N);
+    if (full) add_eq(m.B[abuf]);
+    if (full || any_cauchy_x)
+      for (int k = 0; k < NEQ; k++)
+        if (full || sk_live(mode, k)) f.push_back(m.dSdx[dsbuf] + (long)k * N);
     f.push_back(m.U[pbuf]);
     f.push_back(m.V[pbuf]);
     f.push_back(m.Tg[pbuf]);
@@ -2135,19 +2158,20 @@ void DeviceSolver::halo_fields(int group, std::vector<real*>& f) const {
     for (int q = 0; q < m.nsp; q++) {
       f.push_back(m.Ys[sbuf] + (long)q * N);
       f.push_back(m.As + (long)q * N);
-      f.push_back(m.Bs + (long)q * N);
-      if (m.dSdxs[0]) f.push_back(m.dSdxs[dsbuf] + (long)q * N);
+      if (full) f.push_back(m.Bs + (long)q * N);
+      if (m.dSdxs[0] && (full || any_cauchy_x)) f.push_back(m.dSdxs[dsbuf] + (long)q * N);
     }
   }
 }
 
-void DeviceSolver::exchange(int group, int dt_slot, void* on_stream) {
+void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) {
   Impl& m = *impl;
   p2p_complete();
   if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
   const int ny = h.ny;
   std::vector<real*> fl;
-  halo_fields(group, fl);
+  halo_fields(group, fl, full);
+  if (group == CpuSolver::HALO_STATE) ghost_mode = (full || !halo_compact) ? -1 : split_mode();
   if (fl.size() > (size_t)MAX_HALO_FIELDS) throw std::runtime_error("halo: too many exchanged fields");
   ColList L;
   L.nf = (int)fl.size();
@@ -2548,6 +2572,10 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
     // mechanism mode: SK_MECH (Euler and N-S)
     const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+    // the ghost columns were last exchanged for a single-gas specialisation
+    // and this step is generic (sgl switched off): refresh them in full first
+    if (ghost_mode >= 0 && ghost_mode != SK_GENERIC && mode == SK_GENERIC)
+      exchange(CpuSolver::HALO_STATE, -1, nullptr, true);
     // XCD-aware order: split Step 63.8 -> 59.2 us, resonator 117.7 -> 107.8 us
     // on 1x MI355X; the mechanism pair is 2 % slower with it (1.767 vs 1.800 ms)
     P.xcd = (split_xcd && (mode != SK_MECH || split_xcd_mech)) ? 1 : 0;

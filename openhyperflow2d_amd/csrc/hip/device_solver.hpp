@@ -100,14 +100,20 @@ class DeviceSolver : public SolverBase {
   void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import
   int comm_rank() const;
   int comm_size() const;
-  void exchange(int group, int dt_slot = -1, void* on_stream = nullptr);
+  void exchange(int group, int dt_slot = -1, void* on_stream = nullptr, bool full = false);
   void exchange_dt(int dt_slot);
+  // split-path halos carry only what the next kernels read of a ghost column
+  // (halo_fields); false: every field of the group (the A/B of the layouts)
+  bool halo_compact = true;
+  int ghost_mode = -1;    // SK_* mode the ghost columns were last exchanged for (-1: complete)
+  int split_mode() const; // SK_* mode of the split stepper (step_split)
+  bool any_cauchy_x = true;   // some node applies d2/dx2 = 0 (reads dS/dx of an x neighbour)
   // RCCL / in-process transports: halo of the edge tiles on a comm stream while
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
   long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
-  void halo_fields(int group, std::vector<real*>& f) const;
+  void halo_fields(int group, std::vector<real*>& f, bool full = false) const;
   // p2p self-validation (collective over the strip ranks, before the first
   // step): poisons the ghost columns, runs one mailbox exchange of the full
   // state group with a rank-tagged dt, restores the device scalars and

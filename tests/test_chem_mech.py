@@ -148,7 +148,9 @@ def test_cli_chem_runs_file_mechanism(gpu, tmp_path, capsys):
 def test_solver_uses_mfma_kernel_for_file_mechanism(gpu, tmp_path):
     """A mechanism read from a file at run time (here the built-in set with one
     rate constant changed, so no compiled kernel matches) runs the MFMA kernel
-    inside the time step and agrees with the host stepper."""
+    inside the time step (with the hiprtc-specialised kernels switched off;
+    they are the default, tests/test_gpu_mechanism.py) and agrees with the
+    host stepper."""
     from openhyperflow2d_amd.models import decks
 
     m = M.h2_air_li2004()
@@ -159,6 +161,7 @@ def test_solver_uses_mfma_kernel_for_file_mechanism(gpu, tmp_path):
     text = decks.with_mechanism(decks.reactor0d(8, 8, T=1200.0, p=101325.0), mechanism=str(path), substeps=2)
     g = gpu.Simulation(text, "gpu")
     assert not g.solver.chem_fast_ok
+    g.solver.chem_rtc = False
     c = gpu.Simulation(text, "cpu")
     g.step(300)
     c.step(300)

@@ -121,7 +121,7 @@ def test_lean_bitwise_with_switches(gpu):
 
 
 def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False, corrupt=False,
-                   stats=None):
+                   stats=None, setup=None, chunk_hook=None, fields=FIELDS):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
     host thread each, halos through the in-process LocalGroup transport (or,
     p2p=True, the device-side mailbox transport: one exchange kernel per step,
@@ -138,6 +138,8 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
     for r, (a, b) in enumerate(parts):
         s = nat.DeviceSolver(cases[r], 0, a, b)
         s.lean = lean
+        if setup is not None:
+            setup(s)
         s.init_local(group, r)
         solvers.append(s)
     if p2p:
@@ -187,6 +189,8 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
         if toggle:   # alternate fused / separate-kernel exchange between chunks
             for s in solvers:
                 s.p2p_fuse = (k % 2 == 0)
+        if chunk_hook is not None:
+            chunk_hook(k, solvers)
         th = [threading.Thread(target=run, args=(s, n, res), daemon=True) for s in solvers]
         for t in th:
             t.start()
@@ -199,7 +203,7 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
     if stats is not None:
         stats["overlap_steps"] = [s.overlap_steps for s in solvers]
     out = {}
-    for f in FIELDS:
+    for f in fields:
         full = None
         for r, (a, b) in enumerate(parts):
             solvers[r].download()
@@ -223,6 +227,62 @@ def test_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean):
         ref.step(n, residual=res)
     assert summ["dt"] == ref.summary()["dt"]
     for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def _gas_source_ns():
+    import os
+
+    d = os.path.join(os.path.dirname(__file__), "fixtures", "ref", "gas_source")
+    with open(os.path.join(d, "deck.dat")) as fh:
+        return decks.set_key(fh.read(), "ProblemType", 1)
+
+
+@pytest.mark.parametrize("deck,p2p", [("mech", False), ("mech", True), ("generic", False), ("generic", True),
+                                      ("sgt_toggle", False), ("sgt_toggle", True)])
+def test_compact_state_halo_matches_single_gpu(gpu, deck, p2p):
+    """Split-path halos carry only what the next kernels read of a ghost
+    column (S and the x flux A of the live equations, dS/dx only with Cauchy-x
+    nodes, no y flux B; mid-step only rho, the species, k/eps -- plus rhoU,
+    rhoV, rhoE where mechanism strips react their ghosts).  The strips still
+    equal one GPU bit for bit: mechanism (SK_MECH), generic species N-S
+    (gas sources) and single-gas k-eps (SK_SGT) switching to the generic
+    stepper mid-run, which refreshes the ghost columns in full first."""
+    nat = gpu.native()
+    fields = list(FIELDS) + ["k", "mu_t"]
+    if deck == "mech":
+        text = decks.scramjet(150, 50, nmax=10 ** 6, nout=10 ** 5)
+        fields += ["Y:H2", "Y:O2", "Y:OH", "Y:H2O"]
+        nranks = 3
+    elif deck == "generic":
+        text = _gas_source_ns()
+        fields += ["S4", "S5", "S6"]
+        nranks = 3
+    else:
+        text = decks.wedge15(240, 60, navier_stokes=True, turbulence=4, nmax=10 ** 6, nout=10 ** 5)
+        nranks = 3
+    schedule = [(5, True), (14, False), (5, True), (12, False)]
+    counts = {}
+
+    def setup(s):
+        counts["compact"] = s.halo_field_count(1, False)
+        counts["full"] = s.halo_field_count(1, True)
+
+    def hook(k, solvers):   # single-gas specialisation off for the second half
+        if deck == "sgt_toggle" and k == 2:
+            for s in solvers:
+                s.sgl = False
+
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=False, p2p=p2p, fuse=False, setup=setup,
+                               chunk_hook=hook, fields=fields)
+    assert counts["compact"] < counts["full"], counts
+    ref = gpu.Simulation(text, "gpu", lean=False)
+    for k, (n, res) in enumerate(schedule):
+        if deck == "sgt_toggle" and k == 2:
+            ref.solver.sgl = False
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
+    for f in fields:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
 
