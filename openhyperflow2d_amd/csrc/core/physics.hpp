@@ -360,51 +360,38 @@ struct RefMix {
   HF_HD void heat_flux(const N&, real&, real&) const {}
 };
 
-// TURB = 0: the caller guarantees that no node carries a turbulence-model
-// bit (SK_SGL, lean.cpp sk_eligible), so turb_model() is a no-op and is not
-// compiled in (its Spalart-Allmaras branch alone put the node in scratch);
-// TURB = 2: k-eps is the only model bit present (lean N-S kernel).
-template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every model, 2 k-eps only
-HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
+// fill_node() in three pieces, so that the mechanism-mode lean step
+// (hip/lean_mech.hpp) can run the part of a node that decides its thermodynamic
+// state -- skip tests, velocity recovery, wall conditions, T by Newton -- once
+// per cell (mech_state_node) and the flux part per tile and ring cell with that
+// state loaded.  fill_node() calls them in this order, so both are the same
+// arithmetic.
+//   fill_node_pre   skip tests and U, V from the conserved momentum
+//   (turbulence model)
+//   fill_node_wall  wall-law / no-slip velocity and wall sources
+template <class N>
+HF_HD inline bool fill_node_pre(N& n) {
   if (has_all(n.CT, CT_SOLID)) return false;
   if (n.S[I_RHO] == 0) return false;
   if (n.k < 1) return false;
-  real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
-  if (!MX::MECH) n.k = n.CP / (n.CP - n.R);
-  {
-    // every branch writes both members (same values as "if U const: rho*U,
-    // else U = rhoU/rho"): two stores to different members under a branch
-    // are merged by the compiler into one store through a selected address,
-    // which puts the whole node struct in scratch memory on the GPU
-    const bool uc = has_all(n.CT, CT_U_CONST), vc = has_all(n.CT, CT_V_CONST);
-    const real r = n.S[I_RHO], su = n.S[I_RHOU], sv = n.S[I_RHOV];
-    const real u = uc ? n.U : su / r, v = vc ? n.V : sv / r;
-    n.S[I_RHOU] = uc ? u * r : su;
-    n.S[I_RHOV] = vc ? v * r : sv;
-    n.U = u;
-    n.V = v;
-  }
+  // every branch writes both members (same values as "if U const: rho*U,
+  // else U = rhoU/rho"): two stores to different members under a branch
+  // are merged by the compiler into one store through a selected address,
+  // which puts the whole node struct in scratch memory on the GPU
+  const bool uc = has_all(n.CT, CT_U_CONST), vc = has_all(n.CT, CT_V_CONST);
+  const real r = n.S[I_RHO], su = n.S[I_RHOU], sv = n.S[I_RHOV];
+  const real u = uc ? n.U : su / r, v = vc ? n.V : sv / r;
+  n.S[I_RHOU] = uc ? u * r : su;
+  n.S[I_RHOV] = vc ? v * r : sv;
+  n.U = u;
+  n.V = v;
+  return true;
+}
 
-  if (P.sm == SM_NS) {
-    if (P.is_init && n.TurbType > 0) {
-      n.mu_t = 5.0 * n.mu;
-    } else if (P.is_init) {
-      n.mu_t = n.lam_t = 0.;
-    }
-    if (TURB != 0 && n.TurbType > 0) turb_model<N, TURB == 2>(n, P, P.is_mu_t, P.is_init);
-  }
-
-  if (!MX::MECH) {
-    Tmp1 = n.S[I_RHO];
-    for (int i = 0; i < NCOMP; i++) {
-      Tmp3 += P.Hu[i] * n.S[i + 4];
-      Tmp1 -= n.S[i + 4];
-    }
-    Tmp3 += P.Hu[NCOMP] * Tmp1;
-  }
-
+template <class N>
+HF_HD inline void fill_node_wall(N& n, const FillParams& P) {
   if (has_all(n.CT, CT_WALL_LAW)) {
-    Tmp1 = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
+    const real Tmp1 = std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
     n.S[I_RHOU] = Tmp1 * n.BGX;
     n.S[I_RHOV] = Tmp1 * n.BGY;
     n.U = n.S[I_RHOU] / n.S[I_RHO];
@@ -428,6 +415,42 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   } else {
     for (int i = 0; i < NEQ; i++) n.SrcAdd[i] = 0.;
   }
+}
+
+// TURB = 0: the caller guarantees that no node carries a turbulence-model
+// bit (SK_SGL, lean.cpp sk_eligible), so turb_model() is a no-op and is not
+// compiled in (its Spalart-Allmaras branch alone put the node in scratch);
+// TURB = 2: k-eps is the only model bit present (lean N-S kernel);
+// TURB = 3: k-omega SST is the only one (mechanism-mode lean step).
+template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every model, 2 k-eps only, 3 SST only
+HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
+  if (!fill_node_pre(n)) return false;
+  real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
+  if (!MX::MECH) n.k = n.CP / (n.CP - n.R);   // (k is not read by fill_node_pre's velocity part)
+
+  if (P.sm == SM_NS) {
+    if (P.is_init && n.TurbType > 0) {
+      n.mu_t = 5.0 * n.mu;
+    } else if (P.is_init) {
+      n.mu_t = n.lam_t = 0.;
+    }
+    if (TURB == 3) {
+      if (has_all(n.TurbType, TCT_k_omega_SST_Model)) turb_sst(n, P, P.is_mu_t, P.is_init);
+    } else if (TURB != 0 && n.TurbType > 0) {
+      turb_model<N, TURB == 2>(n, P, P.is_mu_t, P.is_init);
+    }
+  }
+
+  if (!MX::MECH) {
+    Tmp1 = n.S[I_RHO];
+    for (int i = 0; i < NCOMP; i++) {
+      Tmp3 += P.Hu[i] * n.S[i + 4];
+      Tmp1 -= n.S[i + 4];
+    }
+    Tmp3 += P.Hu[NCOMP] * Tmp1;
+  }
+
+  fill_node_wall(n, P);
 
   if (MX::MECH) {
     mx.state(n);   // T by Newton on the thermally perfect e(T); R, Cp, k, p at T

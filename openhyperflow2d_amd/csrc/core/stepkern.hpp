@@ -15,6 +15,8 @@
 //                  owner-computes form (no scatter races).
 #pragma once
 
+#include <type_traits>
+
 #include "physics.hpp"
 #include "mechanism.hpp"
 #include "mechanism_io.hpp"
@@ -660,6 +662,16 @@ struct MechMixLazy {
 // did not skip the node.  `inplace`: the fluxes are updated in place, so
 // those of the flow and species equations need not be loaded (fill_node
 // rewrites them on every node it does not skip).
+// An accessor that declares TILE_TURB is a lean tile's (hip/lean_mech.hpp): it
+// supplies the node's thermodynamic state and the mixture closure (IO::mixer),
+// names the turbulence-model set of fill_node (TILE_TURB), and fill_compute
+// stops after fill_node (no dt, transport or slot fractions: its caller forms
+// those once per cell).
+template <class IO, class = void>
+struct io_is_tile : std::false_type {};
+template <class IO>
+struct io_is_tile<IO, std::void_t<decltype(IO::TILE_TURB)>> : std::true_type {};
+
 template <int MODE, int NSB, class IO, bool KEPS_ONLY = false>
 HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* mY, real* mgx, real* mgy,
                                const MechData* mech, int nsp, int i, int j, bool inplace, int* neg_T,
@@ -758,7 +770,8 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
   // lazy mechanism gradients (sout): formed in MechMixLazy::heat_flux
   real lz_dx = 0, lz_dy = 0;
   bool lz_nx0 = false, lz_ny0 = false;
-  const bool lazy = MECH && sout != nullptr && P.sm == SM_NS;
+  constexpr bool TILE = io_is_tile<IO>::value;
+  const bool lazy = MECH && (sout != nullptr || TILE) && P.sm == SM_NS;
   if (active && P.sm == SM_NS) {
     const uint8_t nbm = io.nb();
     const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
@@ -844,7 +857,10 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     fp.is_init = P.ffc.is_init;
   }
   bool filled;
-  if constexpr (MECH) {
+  if constexpr (MECH && TILE) {
+    filled = fill_node<CellLocal, typename IO::Mix, IO::TILE_TURB>(
+        c, fp, io.mixer(mY, lz_dx, lz_dy, active, lz_nx0, lz_ny0));
+  } else if constexpr (MECH) {
     if (lazy) {
       MechMixLazy<NSB, IO> mx{mech, mY, &io, sout, io.N, io.idx, lz_dx, lz_dy, (real)P.fpa.FT, nsp, mech->bath,
                               active, lz_nx0, lz_ny0, P.fpa.FT != 0};
@@ -857,6 +873,7 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     filled = fill_node<CellLocal, RefMix, MODE == SK_SGL ? 0 : (KEPS_ONLY ? 2 : 1)>(c, fp);
   }
   *filled_out = filled;
+  if constexpr (TILE) return 1.0;
 
   real dt_local = 1.0;
   if (active) {

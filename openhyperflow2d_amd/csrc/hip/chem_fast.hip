@@ -67,12 +67,16 @@ ChemArgs chem_args(const SoA& mid, const SoA& out, const real* Tprev, long c0, l
 
 bool chem_fast_launch(const std::string& mech, const StepParams& P, const SoA& mid, const SoA& out, const real* Tprev,
                       long c0, long c1, DevScalars* sc, int slot, double Tchem, int nsub, hipStream_t st, int* list,
-                      unsigned* count) {
+                      unsigned* count, bool list_ready) {
   (void)P;
   if (mech != "h2_air_li2004" || mid.nsp != Mech_h2_air_li2004::NS) return false;
   const unsigned nb = (unsigned)((c1 - c0 + 255) / 256);
   if (nb == 0) return true;
   const ChemArgs a = chem_args(mid, out, Tprev, c0, c1, sc, slot, Tchem, nsub, list, count);
+  if (list && count && list_ready) {
+    hipLaunchKernelGGL(hf2d_chem_fast_list<Mech_h2_air_li2004>, dim3(std::min(nb, 4096u)), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess;
+  }
   if (list && count) {   // compacted: frozen cells copied, reacting cells integrated densely
     if (hipMemsetAsync(count, 0, sizeof(unsigned), st) != hipSuccess) return false;
     hipLaunchKernelGGL(hf2d_chem_fast_mark<Mech_h2_air_li2004>, dim3(nb), dim3(256), 0, st, a);

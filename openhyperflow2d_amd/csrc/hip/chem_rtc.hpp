@@ -26,9 +26,12 @@ std::string chem_rtc_program(const MechData& m);
 // *why) when hiprtc fails; the caller falls back to the runtime-data kernel.
 bool chem_rtc_prepare(const MechData& m, std::string* why);
 // mechanism-mode kinetics of cells [c0, c1) with the prepared kernels
-// (compacted form when list / count are given)
+// (compacted form when list / count are given; list_ready: the list and its
+// count are already built on the device, only the listed cells are integrated
+// in place -- the lean mechanism step, hip/lean_mech.hpp)
 bool chem_rtc_launch(const MechData& m, const SoA& mid, const SoA& out, const double* Tprev, long c0, long c1,
-                     DevScalars* sc, int slot, double Tchem, int nsub, ihipStream_t* st, int* list, unsigned* count);
+                     DevScalars* sc, int slot, double Tchem, int nsub, ihipStream_t* st, int* list, unsigned* count,
+                     bool list_ready = false);
 // standalone operator on n cells (rhoY [ns][n] and T in place); mean kernel ms
 double chem_rtc_run_host(const MechData& m, double* rhoY, const double* rho, const double* e, double* T, long n,
                          double dt, int nsub, int repeats);

@@ -15,6 +15,10 @@ struct DevScalars {
   double time_part;                // accumulated dt since the cycle start
   int neg_T;
   int pad;
+  double dt_val[3];                // dt of the step that used the slot (the lean
+                                   // mechanism step's fill belongs to the previous one)
+  unsigned hot_cnt[3];             // lean mechanism step: reacting cells listed by the step using the slot
+  unsigned pad2;
 };
 
 __device__ inline double bits_to_d(unsigned long long b) { return __longlong_as_double((long long)b); }

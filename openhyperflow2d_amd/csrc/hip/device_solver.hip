@@ -42,6 +42,7 @@
 #include "chem_rtc.hpp"
 #include "chem_mech.hpp"
 #include "lean_ns.hpp"
+#include "lean_mech.hpp"
 
 #define HIP_CHECK(x)                                                                             \
   do {                                                                                           \
@@ -122,6 +123,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
     // writing) and accumulate physical time.
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    sc->dt_val[slot] = P.dt;
+    sc->hot_cnt[slot_next] = 0;
     scenario_next(P, sc, slot, slot_next);
   }
   const long c = c0 + g;
@@ -828,6 +831,296 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) vo
   lns_step_body<RES, MODE>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 
+// ---------------------------------------------------------------------------
+// Lean mechanism-mode step (lean_mech.hpp): hf2d_lnm_step per 16 x 16 tile,
+// then the kinetics of the listed cells and hf2d_lnm_hot.
+// ---------------------------------------------------------------------------
+// G_m of global cell (gi, gj) at tile coordinates (ii, jj): flow S / A / B
+// and species A / B into the LDS planes that cell feeds.  dt_fill: the dt of
+// the step the split fill F_m belongs to (SST's point-implicit destruction).
+template <int TURB>
+__device__ __forceinline__ void lnm_fill(StepParams& P, const LnmArrays& a, const LnmLayout& L, real* lds, int gi,
+                                         int gj, int ii, int jj, CellLocal& c, real* mY, bool* early, bool* filled) {
+  LnmFillIO<TURB> io(a, gi, gj, P.nx, P.ny);
+  io.lds = lds;
+  io.L = &L;
+  io.aoff = L.a_at(ii, jj);
+  io.boff = L.b_at(ii, jj);
+  real mgx[1], mgy[1];
+  int dummy = 0;
+  (void)fill_compute<SK_MECH, LNM_NSB, LnmFillIO<TURB>, true>(P, io, c, mY, mgx, mgy, a.mech, a.nsp, gi, gj, true,
+                                                               &dummy, early, filled);
+  const int sC = L.s_at(ii, jj), aC = io.aoff, bC = io.boff;
+  const bool zero = *early || !*filled;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    const int k = Lns<SK_SGT>::eqk(q);
+    lds[L.oS + q * L.NC + sC] = c.S[k];
+    if (aC >= 0) lds[L.oA + q * L.NA + aC] = zero ? 0.0 : c.A[k];
+    if (bC >= 0) lds[L.oB + q * L.NB + bC] = zero ? 0.0 : c.B[k];
+  }
+  if (zero)   // (a skipped node stops the lean path; a solid one is never a neighbour)
+    for (int t = 0; t < L.nspt; t++) {
+      if (aC >= 0) lds[L.osA + t * L.NA + aC] = 0.0;
+      if (bC >= 0) lds[L.osB + t * L.NB + bC] = 0.0;
+    }
+}
+
+template <bool RES, int TURB>
+__device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a, const LeanTile& T, DevScalars* sc,
+                                              int slot, int slot_next, int serial, ResidualPack* partials) {
+  extern __shared__ real lds[];
+  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  const LnmLayout L(T.TI, T.TJ, a.nsp - 1);
+  // G_m runs with the dt of the step the split fill F_m belongs to
+  P.dt = sc->dt_val[slot_reset(slot)];
+  const real dt_step = bits_to_d(sc->dt_bits[slot]);
+  if (b == 0 && threadIdx.x == 0) {
+    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    sc->time_part += dt_step;
+    sc->dt_val[slot] = dt_step;
+    sc->hot_cnt[slot_next] = 0;
+    scenario_next(P, sc, slot, slot_next);
+  }
+  int i, j, c, i0, j0;
+  const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
+  const int ii = (int)threadIdx.x / T.TJ, jj = (int)threadIdx.x - ii * T.TJ;
+  int skip = 0;
+  // 1a. ring cells (wavefront 0): S, A or B only
+  if ((int)threadIdx.x < 2 * (T.TI + T.TJ) && !(a.dbg & 1)) {
+    int ri, rj;
+    lns_ring_cell(T, (int)threadIdx.x, &ri, &rj);
+    const int gi = i0 + ri, gj = j0 + rj;
+    if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
+      CellLocal rc;
+      real mY[LNM_NSB];
+      bool early, filled;
+      lnm_fill<TURB>(P, a, L, lds, gi, gj, ri, rj, rc, mY, &early, &filled);
+    }
+  }
+  // 1b. own cell: G_m, its level-m outputs, kept values for 2. and 3.
+  LnmLevel lv;
+  u64 CT = 0;
+  uint8_t gf = 0, nbm = 0;
+  bool early = true;
+  const long N = a.N;
+  const long idx = (long)i * P.ny + j;
+  real bpre[6];
+  if (mine) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) bpre[q] = a.beta[Lns<SK_SGT>::eqk(q) * N + idx];
+    CellLocal oc;
+    real mY[LNM_NSB];
+    bool filled = false;
+    lnm_fill<TURB>(P, a, L, lds, i, j, ii, jj, oc, mY, &early, &filled);
+    CT = oc.CT;
+    gf = a.gf[idx];
+    nbm = a.nb[idx];
+    if (!early) {
+      if (!filled) skip = 1;
+      // mixture transport at T^m (fill_compute's tail: active nodes with a valid T)
+      real mu = oc.mu, lam = oc.lam;
+      if (is_active(CT) && !(oc.Tg < 0. || !(oc.Tg > MECH_TMIN))) mech_transport<LNM_NSB>(*a.mech, mY, oc.Tg, &mu, &lam);
+      a.Uo[idx] = oc.U;
+      a.Vo[idx] = oc.V;
+      a.To[idx] = oc.Tg;
+      a.muo[idx] = mu;
+      a.lamo[idx] = lam;
+      a.mu_to[idx] = oc.mu_t;
+      if (TURB) {
+        a.Src[(long)I_K * N + idx] = oc.Src[I_K];
+        a.Src[(long)I_EPS * N + idx] = oc.Src[I_EPS];
+      }
+      if (gf & GF_SRCADD)
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+          const int k = Lns<SK_SGT>::eqk(q);
+          a.SrcAdd[k * N + idx] = oc.SrcAdd[k];
+        }
+      lv.U = oc.U;
+      lv.V = oc.V;
+      lv.Tg = oc.Tg;
+      lv.k = oc.k;
+      lv.BGX = oc.BGX;
+      lv.BGY = oc.BGY;
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const int k = Lns<SK_SGT>::eqk(q);
+        lv.SrcAdd[q] = oc.SrcAdd[k];
+        lv.F[q] = oc.F[k];
+        lv.Src[q] = oc.Src[k];
+      }
+    }
+  }
+  apply_dt(P, sc, slot);   // this step's dt for the predictor and E_{m+1}
+  __syncthreads();
+  // 2. predict_m, flow and turbulence equations
+  ResidualPack r;
+  if (RES) {
+    residual_reset(r);
+#pragma unroll
+    for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
+  }
+  double dtl = 1.0;
+  int neg = 0;
+  const int nsp = a.nsp, bath = a.bath;
+  if (mine) {
+    const int sC = L.s_at(ii, jj), aC = L.a_at(ii, jj), bC = L.b_at(ii, jj);
+    LnmPredictIO io{a, lds, L, lv, bpre, N, idx, idx, idx, idx, idx, sC, sC, sC, sC, sC, aC, aC, bC, bC, gf, {}};
+    const bool act = is_active(CT);
+    const u64 TT = a.TT[idx];
+    const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+    const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+    const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j, iU = idx + n3, iD = idx - n4;
+    if (!act) {
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        const int k = Lns<SK_SGT>::eqk(q);
+        io.sn[k] = io.S(k);
+        io.keep_dS(k);
+      }
+    } else {
+      io.iL = iL;
+      io.iR = iR;
+      io.iU = iU;
+      io.iD = iD;
+      io.sL = sC - n1 * (T.TJ + 2);
+      io.sR = sC + n2 * (T.TJ + 2);
+      io.sU = sC + n3;
+      io.sD = sC - n4;
+      io.aL = aC - n1 * T.TJ;
+      io.aR = aC + n2 * T.TJ;
+      io.bU = bC + n3;
+      io.bD = bC - n4;
+      predict_core<RES>(P, io, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, r);
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const int k = Lns<SK_SGT>::eqk(q);
+      a.Sp_out[k * N + idx] = io.sn[k];
+    }
+    // 3. species: transported ones by the predictor, the bath gas as the
+    // remainder of the new rho (predict_cell_t order)
+    real ysn[LNM_NSB];
+    real sum = 0.0;
+    const real rho_c = io.S(I_RHO);
+#pragma unroll
+    for (int s = 0; s < LNM_NSB; s++) {
+      ysn[s] = 0.0;
+      if (s < nsp && (s != bath || !act) && !(a.dbg & 4)) {
+        const long o = (long)s * N;
+        LnmSpeciesIO sio{a, lds, L, N, idx, iL, iR, iU, iD, o, s < bath ? s : s - 1,
+                         io.aL, io.aR, io.bU, io.bD, bC, gf, a.Ys[o + idx], lv.SrcAdd[0], rho_c, 0.0};
+        if (!act) {
+          sio.out = sio.ys;
+          a.Ys_out[o + idx] = sio.ys;
+          sio.keep_dS(0);
+        } else {
+          predict_core<RES>(P, sio, CT, TT, n1, n2, n3, n4, P.gx0 + i, j, r);
+          sum += sio.out;
+        }
+        ysn[s] = sio.out;
+      }
+    }
+    if (act)
+#pragma unroll
+      for (int s = 0; s < LNM_NSB; s++)
+        if (s == bath) {
+          ysn[s] = io.sn[I_RHO] - sum;
+          a.Ys_out[(long)s * N + idx] = ysn[s];
+        }
+    // 4. E_{m+1} of the new state, unless the kinetics change it (then hf2d_lnm_hot)
+    if (!early) {
+      const bool hot = act && io.sn[I_RHO] > 0.0 && lv.Tg >= a.mech->Tchem && P.dt > 0.0;
+      const unsigned long long ball = __ballot(hot);
+      if (ball) {
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int leader = __ffsll((long long)ball) - 1;
+        unsigned base = 0;
+        if (lane == leader) base = atomicAdd(&sc->hot_cnt[slot], (unsigned)__popcll(ball));
+        base = __shfl(base, leader, WAVE);
+        if (hot) a.hot[base + __popcll(ball & ((1ull << lane) - 1ull))] = (int)idx;
+      }
+      if (!hot && !(a.dbg & 2)) {
+        const real S4[4] = {io.sn[0], io.sn[1], io.sn[2], io.sn[3]};
+        LnmState st;
+        if (!mech_state_node(P, *a.mech, nsp, S4, ysn, lv.U, lv.V, lv.Tg, lv.k, CT, lv.BGX, lv.BGY, &st, &dtl, &neg))
+          skip = 1;
+        a.Tso[idx] = st.T;
+        a.pso[idx] = st.p;
+        a.CPso[idx] = st.CP;
+        a.kso[idx] = st.k;
+      }
+    }
+  }
+  if (RES) {
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  if (skip) atomicOr(&sc->neg_T, LNS_SKIP_ERR);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mn = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) mn = fmin(mn, sdt[q]);
+    if (serial) mn = fmin(mn, P.dt);
+    atomicMin(&sc->dt_bits[slot_next], d_to_bits(mn));
+  }
+}
+
+// (two workgroups per CU: the LDS of a 16 x 16 tile is ~80 KB, so a budget
+// of 2 waves per SIMD costs no occupancy)
+template <bool RES, int TURB>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void hf2d_lnm_step(
+    StepParams P, LnmArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
+    ResidualPack* partials) {
+  lnm_step_body<RES, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
+}
+
+// E_{m+1} of the cells the kinetics changed (after them): state and dt.
+__global__ __launch_bounds__(BLOCK) void hf2d_lnm_hot(StepParams P, LnmArrays a, DevScalars* sc, int slot,
+                                                       int slot_next, int serial) {
+  apply_dt(P, sc, slot);
+  const unsigned n = sc->hot_cnt[slot];
+  const long N = a.N;
+  double dtl = 1.0;
+  int neg = 0, skip = 0;
+  for (unsigned q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
+    const long idx = a.hot[q];
+    real S4[4], ys[LNM_NSB];
+#pragma unroll
+    for (int k = 0; k < 4; k++) S4[k] = a.Sp_out[k * N + idx];
+#pragma unroll
+    for (int s = 0; s < LNM_NSB; s++) ys[s] = a.Ys_out[(long)(s < a.nsp ? s : a.nsp - 1) * N + idx];
+    LnmState st;
+    double d = 1.0;
+    if (!mech_state_node(P, *a.mech, a.nsp, S4, ys, a.Uo[idx], a.Vo[idx], a.To[idx], a.ksi[idx], a.CT[idx],
+                         a.BGX[idx], a.BGY[idx], &st, &d, &neg))
+      skip = 1;
+    dtl = fmin(dtl, d);
+    a.Tso[idx] = st.T;
+    a.pso[idx] = st.p;
+    a.CPso[idx] = st.CP;
+    a.kso[idx] = st.k;
+  }
+  for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
+  __shared__ double sdt[BLOCK / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
+  if (neg) atomicOr(&sc->neg_T, 1);
+  if (skip) atomicOr(&sc->neg_T, LNS_SKIP_ERR);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mn = sdt[0];
+    for (int q = 1; q < BLOCK / WAVE; q++) mn = fmin(mn, sdt[q]);
+    if (serial) mn = fmin(mn, P.dt);
+    if (mn < 1.0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(mn));
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void hf2d_wall_solid(StepParams P, SoA s, real* qdir, long c0, long c1) {
   const long c = c0 + (long)blockIdx.x * BLOCK + threadIdx.x;
   if (c >= c1) return;
@@ -1168,6 +1461,9 @@ struct DeviceSolver::Impl {
   real *Spre[2], *P2[2];
   // lean N-S: second level of CP / mu / lam / k (the first is the generic array)
   real *CP2 = nullptr, *mu2 = nullptr, *lam2 = nullptr, *kk2 = nullptr, *mu_t2 = nullptr;
+  // lean mechanism step: second level of p and both levels of the stored T
+  // (the thermodynamic state T, p, Cp, k of lean_mech.hpp; Cp / k share CP2 / kk2)
+  real *p2 = nullptr, *Tst[2] = {nullptr, nullptr};
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   int32_t* wslot;
@@ -1297,6 +1593,73 @@ struct DeviceSolver::Impl {
     a.TT = TT;
     a.nb = nb;
     a.gf = gf;
+    return a;
+  }
+
+  // lean mechanism step arguments (lean_mech.hpp): Sp^m in S[1-sb], its
+  // post-kinetics species in Ys[sb]; every two-level array is read at
+  // [1 - cb] and written at [cb] (transport m-1 -> m, state m -> m+1)
+  LnmArrays lnm_arrays(const HostArrays& h, int sb, int pb, int cb, int db, int ab) const {
+    LnmArrays a;
+    a.N = h.N;
+    a.mech = mech;
+    a.nsp = nsp;
+    a.bath = h.mech ? h.mech->bath : 0;
+    a.Sp = S[1 - sb];
+    a.Sp_out = S[sb];
+    a.Ys = Ys[sb];
+    a.Ys_out = Ys[1 - sb];
+    a.beta = beta;
+    a.betas = betas;
+    a.Ui = U[1 - pb];
+    a.Vi = V[1 - pb];
+    a.Ti = Tg[1 - pb];
+    a.Uo = U[pb];
+    a.Vo = V[pb];
+    a.To = Tg[pb];
+    real* const mux[2] = {mu, mu2};
+    real* const lamx[2] = {lam, lam2};
+    real* const mutx[2] = {mu_t, mu_t2};
+    real* const cpx[2] = {CP, CP2};
+    real* const kkx[2] = {kk, kk2};
+    real* const px[2] = {p, p2};
+    a.mui = mux[1 - cb];
+    a.lami = lamx[1 - cb];
+    a.mu_ti = mutx[1 - cb];
+    a.muo = mux[cb];
+    a.lamo = lamx[cb];
+    a.mu_to = mutx[cb];
+    a.Tsi = Tst[1 - cb];
+    a.psi = px[1 - cb];
+    a.CPsi = cpx[1 - cb];
+    a.ksi = kkx[1 - cb];
+    a.Tso = Tst[cb];
+    a.pso = px[cb];
+    a.CPso = cpx[cb];
+    a.kso = kkx[cb];
+    a.l_min = l_min;
+    a.y_plus = y_plus;
+    a.BGX = BGX;
+    a.BGY = BGY;
+    a.grad = grad;
+    a.Src = Src;
+    a.SrcAdd = SrcAdd;
+    a.gA = A[ab];
+    a.gB = B[ab];
+    a.gF = F;
+    a.dSdx_in = dSdx[db];
+    a.dSdy_in = dSdy[db];
+    a.dSdx_out = dSdx[1 - db];
+    a.dSdy_out = dSdy[1 - db];
+    a.dSdxs_in = dSdxs[db];
+    a.dSdys_in = dSdys[db];
+    a.dSdxs_out = dSdxs[1 - db];
+    a.dSdys_out = dSdys[1 - db];
+    a.CT = CT;
+    a.TT = TT;
+    a.nb = nb;
+    a.gf = gf;
+    a.hot = chem_list;
     return a;
   }
 
@@ -1604,6 +1967,55 @@ void DeviceSolver::upload() {
     lns_state = 0;
     cbuf = 0;
   }
+  {
+    // lean mechanism step (lean_mech.hpp): N-S, laminar or k-omega SST only
+    // (SA / k-eps read values of the previous level before the state), no
+    // eddy-viscosity or viscous CFL term in the dt (the state part has no
+    // gradients), adiabatic walls, no volume sources, every non-solid node
+    // set, one strip, <= LNM_NSB species
+    auto no = [&](const char* w) {
+      lnm_ok = false;
+      lnm_why = w;
+    };
+    lnm_ok = true;
+    lnm_why.clear();
+    lnm_turb = 0;
+    const u64 other_models = TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
+                             TCT_k_omega_Model | TCT_k_eps_Model | TCT_Baldwin_Lomax_Model | TCT_nut_92_Model |
+                             TCT_Smagorinsky_Model;
+    if (!h.mech) no("not mechanism mode");
+    else if (cs.cfg.ProblemType != SM_NS) no("not Navier-Stokes");
+    else if (m.nsp > LNM_NSB || m.nsp < 2) no("species count outside the kernel's block");
+    else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
+    else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
+    else if (cs.cfg.ViscousCFL > 0) no("viscous CFL");
+    else if (h.ny < LNM_TILE) no("grid lower than one tile");
+    else
+      for (long q = 0; q < N && lnm_ok; q++) {
+        if (h.gf[q] & GF_SRC) no("volume sources");
+        else if (!has_all(h.CT[q], CT_SOLID) && !has_all(h.CT[q], CT_NODE_IS_SET)) no("unset non-solid node");
+        else if (h.TT[q] & other_models) no("turbulence model other than k-omega SST");
+        else if (has_all(h.TT[q], TCT_k_omega_SST_Model)) lnm_turb = 3;
+      }
+    if (lnm_ok) {
+      if (!m.CP2) {
+        m.CP2 = m.mem.alloc<real>(N);
+        m.mu2 = m.mem.alloc<real>(N);
+        m.lam2 = m.mem.alloc<real>(N);
+        m.kk2 = m.mem.alloc<real>(N);
+        m.mu_t2 = m.mem.alloc<real>(N);
+      }
+      if (!m.p2) {
+        m.p2 = m.mem.alloc<real>(N);
+        m.Tst[0] = m.mem.alloc<real>(N);
+        m.Tst[1] = m.mem.alloc<real>(N);
+      }
+      if (!m.chem_list) {
+        m.chem_list = m.mem.alloc<int>(N);
+        m.chem_count = m.mem.alloc<unsigned>(1);
+      }
+    }
+  }
   lean_sg_ok = lean_ok && lean_single_gas(cs);
   any_cauchy_x = lean_any_cauchy_x(cs);
   lean_has_cauchy_x = lean_ok && any_cauchy_x;
@@ -1704,6 +2116,36 @@ void DeviceSolver::lns_materialize() {
   P.gx0 = gi0 - l_off;
   P.species = m.species;
   P.scen = m.scen;
+  if (m.mech) {
+    // lean mechanism path: the split (lazy) fill F_{m+1} from Sp^{m+1}, its
+    // post-kinetics species and the level-m primitives / transport; the
+    // lagged k of its skip test is the state of level m
+    SoA sin = m.view(h, 1 - sbuf, abuf, dsbuf, 1 - pbuf);
+    m.mech_view(sin, sbuf, dsbuf);
+    real* const mux[2] = {m.mu, m.mu2};
+    real* const lamx[2] = {m.lam, m.lam2};
+    real* const mutx[2] = {m.mu_t, m.mu_t2};
+    real* const cpx[2] = {m.CP, m.CP2};
+    real* const kkx[2] = {m.kk, m.kk2};
+    real* const px[2] = {m.p, m.p2};
+    sin.mu = mux[1 - cbuf];
+    sin.lam = lamx[1 - cbuf];
+    sin.mu_t = mutx[1 - cbuf];
+    sin.CP = cpx[cbuf];
+    sin.kk = kkx[cbuf];
+    sin.p = px[cbuf];
+    SoA out = m.view(h, sbuf, abuf, dsbuf, pbuf);
+    const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
+    const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+    // (the split fill F_{m+1} belongs to step m: its dt is slot m % 3, which
+    // step m+1 has not reset yet; SST's point-implicit destruction reads it)
+    hipLaunchKernelGGL((hf2d_fill_occ<SK_MECH, 9, 2, true>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0,
+                       c1, m.sc, (int)((nstep + 2) % 3), -1, 0, 1);
+    HIP_CHECK(hipGetLastError());
+    lns_state = 0;
+    cbuf = 0;
+    return;
+  }
   SoA sin = m.view(h, 1 - sbuf, abuf, dsbuf, 1 - pbuf);
   real* const cpx[2] = {m.CP, m.CP2};
   real* const mux[2] = {m.mu, m.mu2};
@@ -2476,7 +2918,7 @@ void DeviceSolver::flush_pending() {
 uint64_t DeviceSolver::mode_signature() const {
   const int fields[] = {lean_state, (int)lean, (int)fused, (int)lean_tile, (int)(lean_sg && lean_sg_ok), lean_cpt,
                         lean_tj, lean_wgcu, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok), lns_state,
-                        (int)lean_ns};
+                        (int)lean_ns, (int)lean_mech};
   uint64_t h = 0;
   for (int f : fields) h = h * 1000003ull + (uint64_t)(f + 1);
   return h;
@@ -2586,7 +3028,14 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     if (P.sm == SM_NS) exchange(CpuSolver::HALO_MID);
     SoA sin = m.view(h, 1 - sbuf, abuf, 1 - dsbuf, pbuf);
     SoA out = m.view(h, sbuf, abuf, 1 - dsbuf, 1 - pbuf);
-    if (to_lns) {   // entering the lean N-S path: level n+1 into the second buffers
+    if (to_lns && mode == SK_MECH) {
+      // entering the lean mechanism path: transport of level n+1 into the
+      // second buffers (level n stays for G_{n+1}); the state (T, p, Cp, k)
+      // of level n+1 is read from the generic arrays (T copied to Tst[0])
+      out.mu = m.mu2;
+      out.lam = m.lam2;
+      out.mu_t = m.mu_t2;
+    } else if (to_lns) {   // entering the lean N-S path: level n+1 into the second buffers
       out.CP = m.CP2;
       out.mu = m.mu2;
       out.lam = m.lam2;
@@ -2631,10 +3080,78 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
 }
 
 bool DeviceSolver::lns_entry(const StepParams& P0) const {
-  if (!lean_ns || !lns_ok) return false;
   StepParams P = P0;
   P.ny = h.ny;
-  return lns_step_ok(P);
+  return (lean_ns && lns_ok && lns_step_ok(P)) || (lean_mech && lnm_ok && lnm_step_ok(P));
+}
+
+// The lean mechanism step applies (lean_mech.hpp; eligibility lnm_ok) with a
+// list-building kinetics kernel (compiled or hiprtc-specialised)
+bool DeviceSolver::lnm_step_ok(const StepParams& P) const {
+  const Impl& m = *impl;
+  const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : (chem_rtc && chem_rtc_ok) ? 4 : 2);
+  return lean_mech && lnm_ok && m.mech && P.sm == SM_NS && m.nranks == 1 && !m.p2p.on && chem_compact &&
+         ((kind == 1 && chem_fast_ok) || (kind == 4 && chem_rtc_ok)) && !P.fpa.is_init && !P.ffc.is_init &&
+         P.fpa.is_mu_t == lns_prev_mu_t && P.ny >= LNM_TILE;
+}
+
+using LnmK = void (*)(StepParams, LnmArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*);
+// [residual][SST]
+static const LnmK kLnm[2][2] = {{hf2d_lnm_step<false, 0>, hf2d_lnm_step<false, 3>},
+                                {hf2d_lnm_step<true, 0>, hf2d_lnm_step<true, 3>}};
+
+// One lean mechanism step (lean_mech.hpp): tile kernel, kinetics of the
+// listed cells in place on the new species, their state kernel.
+void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int slot_next, int serial) {
+  Impl& m = *impl;
+  hipStream_t st = m.stream;
+  LnmArrays a = m.lnm_arrays(h, sbuf, pbuf, cbuf, dsbuf, abuf);
+  if (const char* e = std::getenv("HF2D_LNM_DBG")) a.dbg = std::atoi(e);
+  const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, LNM_TILE, 1);
+  const LnmLayout L(T.TI, T.TJ, m.nsp - 1);
+  const size_t shmem = (size_t)L.total() * sizeof(real);
+  const LnmK k = kLnm[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0];
+  static bool attr_set[2][2] = {{false, false}, {false, false}};
+  if (!attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0]) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+    (void)hipGetLastError();
+    attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0] = true;
+  }
+  hipLaunchKernelGGL(k, dim3(T.nbi * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
+                     m.partials);
+  HIP_CHECK(hipGetLastError());
+  // kinetics of the listed cells (T^m >= Tchem), in place on the new species
+  const MechData& md = *cs.cfg.mech->data_ptr();
+  SoA mid;
+  mid.nx = h.nx;
+  mid.ny = h.ny;
+  mid.N = h.N;
+  mid.S = a.Sp_out;
+  mid.Ys = a.Ys_out;
+  mid.CT = m.CT;
+  mid.mech = m.mech;
+  mid.nsp = m.nsp;
+  const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
+  unsigned* cnt = &m.sc->hot_cnt[slot];
+  const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : 4);
+  if (kind == 1) {
+    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st,
+                          m.chem_list, cnt, true))
+      throw std::runtime_error("hf2d_chem_fast list launch failed");
+    chem_kernel_used = "hf2d_chem_fast";
+  } else {
+    if (!chem_rtc_launch(md, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st, m.chem_list, cnt, true))
+      throw std::runtime_error("hf2d_rtc_chem list launch failed");
+    chem_kernel_used = "hf2d_rtc_chem";
+  }
+  const unsigned nb = (unsigned)std::min<long>((c1 - c0 + BLOCK - 1) / BLOCK, 1024);
+  hipLaunchKernelGGL(hf2d_lnm_hot, dim3(nb), dim3(BLOCK), 0, st, P, a, m.sc, slot, slot_next, serial);
+  HIP_CHECK(hipGetLastError());
+  sbuf = 1 - sbuf;
+  pbuf = 1 - pbuf;
+  cbuf = 1 - cbuf;
+  dsbuf = 1 - dsbuf;
+  lnm_steps++;
 }
 
 // The lean N-S kernel applies to this step (lean_ns.hpp; eligibility lns_ok)
@@ -2782,6 +3299,19 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     abuf = 1 - abuf;
     dsbuf = 1 - dsbuf;
     sbuf = 1 - sbuf;
+  } else if (lnm_step_ok(P)) {
+    if (lean_state) lean_materialize();
+    if (lns_state == 0) {
+      // first lean mechanism step: the split step, then T^{n+1} as the stored state
+      step_split(P, want_res, slot, slot_next, serial, nblk, true);
+      HIP_CHECK(hipMemcpyAsync(m.Tst[0], m.Tg[pbuf], h.N * sizeof(real), hipMemcpyDeviceToDevice, st));
+      lns_state = 1;
+      cbuf = 1;
+    } else {
+      lnm_step(P, want_res, slot, slot_next, serial);
+      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, LNM_TILE, 1);
+      nres = (unsigned)(T.nbi * T.nbj);
+    }
   } else if (lns_step_ok(P)) {
     if (lean_state) lean_materialize();
     if (lns_state == 0) {

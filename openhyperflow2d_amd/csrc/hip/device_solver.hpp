@@ -181,6 +181,14 @@ class DeviceSolver : public SolverBase {
   int lns_occ = 0;
   int lns_prev_mu_t = -1;  // is_mu_t of the previous step (the split fill F_m ran with it)        // 0: compiler register budget; 5 / 6: waves-per-SIMD budget
   void lns_materialize();
+  // Mechanism mode (SK_MECH N-S, laminar or k-omega SST): the lean step of
+  // hip/lean_mech.hpp (tile kernel + kinetics + reacting-cell state kernel)
+  // when eligible (lnm_ok); it shares lns_state / cbuf with the lean N-S path
+  bool lean_mech = true;
+  bool lnm_ok = false;
+  std::string lnm_why;
+  int lnm_turb = 0;       // fill_node turbulence set of the kernel: 0 none, 3 SST
+  long lnm_steps = 0;
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
   void lean_materialize();
@@ -201,6 +209,8 @@ class DeviceSolver : public SolverBase {
   void step_split(const StepParams& P, bool want_res, int slot, int slot_next, int serial, unsigned nblk, bool to_lns);
   bool lns_step_ok(const StepParams& P) const;
   bool lns_entry(const StepParams& P0) const;
+  bool lnm_step_ok(const StepParams& P) const;
+  void lnm_step(const StepParams& P, bool want_res, int slot, int slot_next, int serial);
   // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
   void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };

@@ -144,3 +144,47 @@ def test_file_mechanism_runs_the_rtc_kernel_and_matches_cpu(gpu, tmp_path):
     for f in ("rho", "U", "V", "p", "T", "Y:H2", "Y:O2", "Y:OH"):
         a, b = g.field(f), c.field(f)
         assert np.abs(a - b).max() <= 1e-9 * max(np.abs(b).max(), 1e-30), f
+
+
+@pytest.mark.parametrize("deck", ["sst", "sst_graphs", "laminar", "hot"])
+def test_lean_mech_equals_split(gpu, deck):
+    """Lean mechanism step (hip/lean_mech.hpp: flow, turbulence and species
+    fluxes recomputed in the LDS tile, the Newton T once per cell and step,
+    kinetics and the state of the reacting cells over a list) == the split
+    predict + kinetics + fill kernels on every field, dt and time, across
+    entry / materialize / re-entry transitions (residual steps, downloads
+    between windows, graph windows).  'hot': ChemTmin 200 K, so every active
+    cell goes through the kinetics list and hf2d_lnm_hot."""
+    if deck == "laminar":
+        text = decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5, turbulence=0)
+    elif deck == "hot":
+        text = decks.with_mechanism(decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5), tmin=200.0)
+    else:
+        text = decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    b.solver.lean_mech = False
+    graphs = deck.endswith("_graphs")
+    if not graphs:
+        a.solver.use_graph = b.solver.use_graph = False
+    assert a.solver.lnm_ok, a.solver.lnm_why
+    assert a.solver.lnm_turb == (0 if deck == "laminar" else 3)
+    sched = [(4, True), (30, False), (6, True), (19, False)] if not graphs else [(40, False), (13, True), (61, False)]
+    for n, res in sched:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+        assert a.summary()["dt"] == b.summary()["dt"]
+    assert a.solver.lnm_steps > 0
+    assert b.solver.lnm_steps == 0
+    assert a.solver.chem_kernel_used == b.solver.chem_kernel_used
+    assert a.summary()["time"] == b.summary()["time"]
+    np.testing.assert_allclose(a.summary()["rms"], b.summary()["rms"], rtol=1e-12, atol=0)
+    for f in ("rho", "U", "V", "p", "T", "k", "R", "CP", "mu", "lam", "mu_t", "S7", "S8", "Y:H2", "Y:O2", "Y:OH",
+              "Y:H2O", "Y:N2"):
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+    ra = np.frombuffer(a.records(), dtype=np.float64).reshape(-1, 156).copy()
+    rb = np.frombuffer(b.records(), dtype=np.float64).reshape(-1, 156).copy()
+    assert (np.isnan(ra) == np.isnan(rb)).all()
+    ra[np.isnan(ra)] = 0
+    rb[np.isnan(rb)] = 0
+    np.testing.assert_array_equal(ra.view(np.uint64), rb.view(np.uint64))
