@@ -685,11 +685,14 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("lns_why", &DeviceSolver::lns_why)
       .def_readonly("lns_state", &DeviceSolver::lns_state)
       .def_readonly("lns_steps", &DeviceSolver::lns_steps)
+      .def_readonly("lns_turb", &DeviceSolver::lns_turb)
       .def_readwrite("lean_mech", &DeviceSolver::lean_mech)
       .def_readonly("lnm_ok", &DeviceSolver::lnm_ok)
       .def_readonly("lnm_why", &DeviceSolver::lnm_why)
       .def_readonly("lnm_turb", &DeviceSolver::lnm_turb)
       .def_readonly("lnm_steps", &DeviceSolver::lnm_steps)
+      .def_readwrite("lnm_ti", &DeviceSolver::lnm_ti)
+      .def("lnm_trace_fetch", &DeviceSolver::lnm_trace_fetch, py::call_guard<py::gil_scoped_release>())
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)

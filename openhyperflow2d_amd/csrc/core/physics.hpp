@@ -182,6 +182,56 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   n.F[I_OMEGA] = FT * (n.mu + mut * so) * n.depsdy;
 }
 
+// Spalart-Allmaras branch of TurbModRANS2D (hyper_flow_node.hpp:822-918):
+// nu~ in the k slot.
+template <class N>
+HF_HD inline void turb_sa(N& n, const FillParams& P, int is_mu_t, int is_init) {
+  const u64 TT = n.TurbType;
+  real fv1 = 1.0;
+  if (is_init) {
+    n.S[I_NUT] = n.mu / n.S[I_RHO] / 100.0;
+  } else if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW) ||
+             has_all(TT, TCT_nu_t_CONST)) {
+    n.S[I_NUT] = 0.;
+  } else if (has_all(n.CT, NT_FC)) {
+    n.S[I_NUT] = n.mu / n.S[I_RHO] * P.turb_I;
+  } else {
+    const real Cb1 = 0.1355, Cb2 = 0.622, sig = 2.0 / 3.0, _k = 0.41;
+    const real Cw1 = Cb1 / (_k * _k) + (1 + Cb2) / sig;
+    const real Cw2 = 0.3, Cw3 = 2.0, Cv1 = 7.1, Ct2 = 2.0, Ct4 = 0.5, C5 = 3.5;
+    const real a_sound2 = n.k * n.R * n.Tg;
+    const real nu = n.mu / n.S[I_RHO];
+    const real ksi = n.S[I_NUT] / nu;
+    fv1 = ksi * ksi * ksi / (ksi * ksi * ksi + Cv1 * Cv1 * Cv1);
+    const real nu_hat = n.mu_t / n.S[I_RHO] / fv1;
+    const real fv2 = 1.0 - ksi / (1.0 + ksi * fv1);
+    const real Wxy = 0.5 * (n.dVdx - n.dUdy);
+    const real Omega = std::sqrt(2.0 * Wxy * Wxy);
+    real S_hat = Omega + n.S[I_NUT] / (_k * _k * n.l_min * n.l_min) * fv2;
+    if (S_hat < 0.3 * Omega) S_hat = 0.3 * Omega;
+    const real r = hf_min((n.S[I_NUT] / (S_hat * _k * _k * n.l_min * n.l_min)), 10.0);
+    const real g = r + Cw2 * (std::pow(r, 6.0) - r);
+    const real fw = g * std::pow((1.0 + std::pow(Cw3, 6.0)) / (std::pow(g, 6.0) + std::pow(Cw3, 6.0)),
+                                 1.0 / 6.0);
+    const real ft2 = Ct2 * std::exp(-Ct4 * ksi * ksi);
+    n.A[I_NUT] = n.S[I_NUT] * n.U;
+    n.B[I_NUT] = n.S[I_NUT] * n.V;
+    const real Div_nu = (n.dkdx + n.dkdy);
+    n.RX[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdx) / sig;
+    n.RY[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdy) / sig;
+    n.A[I_NUT] = n.A[I_NUT] - n.RX[I_NUT];
+    n.B[I_NUT] = n.B[I_NUT] - n.RY[I_NUT];
+    n.Src[I_NUT] = Cb1 * (1.0 - ft2) * S_hat * n.S[I_NUT] -
+                   (Cw1 * fw - Cb1 / (_k * _k) * ft2) * (n.S[I_NUT] / n.l_min) * (n.S[I_NUT] / n.l_min) +
+                   (Cb2 * Div_nu * Div_nu) / sig - C5 * nu_hat * nu_hat / a_sound2 * n.dUdy * n.dVdx;
+  }
+  turb_axisym_addon(n, P, is_init);
+  if (is_mu_t) {
+    n.mu_t = hf_max(0.0, (n.S[I_RHO] * n.S[I_NUT] * fv1));
+    n.lam_t = n.mu_t * n.CP;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Turbulence closures.
 // ---------------------------------------------------------------------------
@@ -285,49 +335,7 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
       turb_axisym_addon(n, P, is_init);
     }
   } else if (!KEPS_ONLY && has_all(TT, TCT_Spalart_Allmaras_Model)) {
-    real fv1 = 1.0;
-    if (is_init) {
-      n.S[I_NUT] = n.mu / n.S[I_RHO] / 100.0;
-    } else if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW) ||
-               has_all(TT, TCT_nu_t_CONST)) {
-      n.S[I_NUT] = 0.;
-    } else if (has_all(n.CT, NT_FC)) {
-      n.S[I_NUT] = n.mu / n.S[I_RHO] * P.turb_I;
-    } else {
-      const real Cb1 = 0.1355, Cb2 = 0.622, sig = 2.0 / 3.0, _k = 0.41;
-      const real Cw1 = Cb1 / (_k * _k) + (1 + Cb2) / sig;
-      const real Cw2 = 0.3, Cw3 = 2.0, Cv1 = 7.1, Ct2 = 2.0, Ct4 = 0.5, C5 = 3.5;
-      const real a_sound2 = n.k * n.R * n.Tg;
-      const real nu = n.mu / n.S[I_RHO];
-      const real ksi = n.S[I_NUT] / nu;
-      fv1 = ksi * ksi * ksi / (ksi * ksi * ksi + Cv1 * Cv1 * Cv1);
-      const real nu_hat = n.mu_t / n.S[I_RHO] / fv1;
-      const real fv2 = 1.0 - ksi / (1.0 + ksi * fv1);
-      const real Wxy = 0.5 * (n.dVdx - n.dUdy);
-      const real Omega = std::sqrt(2.0 * Wxy * Wxy);
-      real S_hat = Omega + n.S[I_NUT] / (_k * _k * n.l_min * n.l_min) * fv2;
-      if (S_hat < 0.3 * Omega) S_hat = 0.3 * Omega;
-      const real r = hf_min((n.S[I_NUT] / (S_hat * _k * _k * n.l_min * n.l_min)), 10.0);
-      const real g = r + Cw2 * (std::pow(r, 6.0) - r);
-      const real fw = g * std::pow((1.0 + std::pow(Cw3, 6.0)) / (std::pow(g, 6.0) + std::pow(Cw3, 6.0)),
-                                   1.0 / 6.0);
-      const real ft2 = Ct2 * std::exp(-Ct4 * ksi * ksi);
-      n.A[I_NUT] = n.S[I_NUT] * n.U;
-      n.B[I_NUT] = n.S[I_NUT] * n.V;
-      const real Div_nu = (n.dkdx + n.dkdy);
-      n.RX[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdx) / sig;
-      n.RY[I_NUT] = ((n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdy) / sig;
-      n.A[I_NUT] = n.A[I_NUT] - n.RX[I_NUT];
-      n.B[I_NUT] = n.B[I_NUT] - n.RY[I_NUT];
-      n.Src[I_NUT] = Cb1 * (1.0 - ft2) * S_hat * n.S[I_NUT] -
-                     (Cw1 * fw - Cb1 / (_k * _k) * ft2) * (n.S[I_NUT] / n.l_min) * (n.S[I_NUT] / n.l_min) +
-                     (Cb2 * Div_nu * Div_nu) / sig - C5 * nu_hat * nu_hat / a_sound2 * n.dUdy * n.dVdx;
-    }
-    turb_axisym_addon(n, P, is_init);
-    if (is_mu_t) {
-      n.mu_t = hf_max(0.0, (n.S[I_RHO] * n.S[I_NUT] * fv1));
-      n.lam_t = n.mu_t * n.CP;
-    }
+    turb_sa(n, P, is_mu_t, is_init);
   } else if (!KEPS_ONLY && has_all(TT, TCT_k_omega_SST_Model)) {
     turb_sst(n, P, is_mu_t, is_init);
   } else if (!KEPS_ONLY && has_all(TT, TCT_Integral_Model) && n.mu != 0.0) {
@@ -421,8 +429,8 @@ HF_HD inline void fill_node_wall(N& n, const FillParams& P) {
 // bit (SK_SGL, lean.cpp sk_eligible), so turb_model() is a no-op and is not
 // compiled in (its Spalart-Allmaras branch alone put the node in scratch);
 // TURB = 2: k-eps is the only model bit present (lean N-S kernel);
-// TURB = 3: k-omega SST is the only one (mechanism-mode lean step).
-template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every model, 2 k-eps only, 3 SST only
+// TURB = 3 / 4: k-omega SST / Spalart-Allmaras is the only one (lean steps).
+template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every model, 2 k-eps, 3 SST, 4 SA only
 HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (!fill_node_pre(n)) return false;
   real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
@@ -436,6 +444,8 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
     }
     if (TURB == 3) {
       if (has_all(n.TurbType, TCT_k_omega_SST_Model)) turb_sst(n, P, P.is_mu_t, P.is_init);
+    } else if (TURB == 4) {
+      if (has_all(n.TurbType, TCT_Spalart_Allmaras_Model)) turb_sa(n, P, P.is_mu_t, P.is_init);
     } else if (TURB != 0 && n.TurbType > 0) {
       turb_model<N, TURB == 2>(n, P, P.is_mu_t, P.is_init);
     }

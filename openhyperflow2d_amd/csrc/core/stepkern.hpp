@@ -671,6 +671,12 @@ template <class IO, class = void>
 struct io_is_tile : std::false_type {};
 template <class IO>
 struct io_is_tile<IO, std::void_t<decltype(IO::TILE_TURB)>> : std::true_type {};
+// An accessor that declares TURB_SET names fill_node's turbulence-model set
+// (physics.hpp; the lean N-S kernel's k-eps / SST / SA variants).
+template <class IO, int DEF, class = void>
+struct io_turb_set : std::integral_constant<int, DEF> {};
+template <class IO, int DEF>
+struct io_turb_set<IO, DEF, std::void_t<decltype(IO::TURB_SET)>> : std::integral_constant<int, IO::TURB_SET> {};
 
 template <int MODE, int NSB, class IO, bool KEPS_ONLY = false>
 HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* mY, real* mgx, real* mgy,
@@ -870,7 +876,7 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
       filled = fill_node(c, fp, mx);
     }
   } else {
-    filled = fill_node<CellLocal, RefMix, MODE == SK_SGL ? 0 : (KEPS_ONLY ? 2 : 1)>(c, fp);
+    filled = fill_node<CellLocal, RefMix, MODE == SK_SGL ? 0 : io_turb_set<IO, KEPS_ONLY ? 2 : 1>::value>(c, fp);
   }
   *filled_out = filled;
   if constexpr (TILE) return 1.0;

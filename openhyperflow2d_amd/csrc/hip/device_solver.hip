@@ -664,7 +664,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
 // ---------------------------------------------------------------------------
 constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
 
-template <bool RES, int MODE>
+template <bool RES, int MODE, int TURB>
 __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
@@ -674,8 +674,12 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   if (b == 0 && threadIdx.x == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
     sc->time_part += P.dt;
+    sc->dt_val[slot] = P.dt;
     scenario_next(P, sc, slot, slot_next);
   }
+  // F_m runs with the dt of the step the split fill F_m belongs to (SST's
+  // point-implicit destruction reads it); the predictor with this step's
+  P.dt = sc->dt_val[slot_reset(slot)];
   const int NC = T.NC;
   int i, j, c, i0, j0;
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
@@ -689,7 +693,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
       CellLocal rc;
       bool early, filled;
-      lns_fill_to_lds<MODE>(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
+      lns_fill_to_lds<MODE, TURB>(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
     }
   }
   // 1b. own cell: F_m, its level-m outputs, kept values for 2./3.
@@ -704,7 +708,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
 #pragma unroll
     for (int q = 0; q < NL; q++) bpre[q] = a.beta[Lns<MODE>::eqk(q) * N + idx];
     CellLocal oc;
-    lns_fill_to_lds<MODE>(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
+    lns_fill_to_lds<MODE, TURB>(P, a, i, j, lds, NC, c, oc, &early, &filled, &dummy);
     CT = oc.CT;
     gf = a.gf[idx];
     nbm = a.nb[idx];
@@ -752,6 +756,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       }
     }
   }
+  apply_dt(P, sc, slot);
   __syncthreads();
   // 2. predict_m
   ResidualPack r;
@@ -818,17 +823,17 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   }
 }
 
-template <bool RES, int MODE>
+template <bool RES, int MODE, int TURB = 2>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
                                                         int slot, int slot_next, int serial, ResidualPack* partials) {
-  lns_step_body<RES, MODE>(P, a, T, sc, slot, slot_next, serial, partials);
+  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 // register budget of OCC waves per SIMD (DeviceSolver::lns_occ, measured)
-template <bool RES, int MODE, int OCC>
+template <bool RES, int MODE, int OCC, int TURB = 2>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_lns_step_occ(
     StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
     ResidualPack* partials) {
-  lns_step_body<RES, MODE>(P, a, T, sc, slot, slot_next, serial, partials);
+  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 
 // ---------------------------------------------------------------------------
@@ -872,6 +877,10 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   extern __shared__ real lds[];
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   const LnmLayout L(T.TI, T.TJ, a.nsp - 1);
+  // phase trace: wavefront 0 (slots 0..8) and the last wavefront (9, 10) of the workgroup
+  unsigned long long* tr = a.tr ? a.tr + (long)b * 12 : nullptr;
+  const bool tr0 = tr && threadIdx.x == 0, trl = tr && threadIdx.x == BLOCK - WAVE;
+  if (tr0) tr[0] = rt_clock();
   // G_m runs with the dt of the step the split fill F_m belongs to
   P.dt = sc->dt_val[slot_reset(slot)];
   const real dt_step = bits_to_d(sc->dt_bits[slot]);
@@ -886,10 +895,14 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
   const int ii = (int)threadIdx.x / T.TJ, jj = (int)threadIdx.x - ii * T.TJ;
   int skip = 0;
-  // 1a. ring cells (wavefront 0): S, A or B only
-  if ((int)threadIdx.x < 2 * (T.TI + T.TJ) && !(a.dbg & 1)) {
+  // 1a. ring cells: S, A or B only (on the threads after the tile's cells when
+  // they fit in the workgroup, else on the first ones as a second fill)
+  const int nring = 2 * (T.TI + T.TJ), own = T.TI * T.TJ;
+  const int rbase = own + nring <= BLOCK ? own : 0;
+  const int rt = (int)threadIdx.x - rbase;
+  if (rt >= 0 && rt < nring) {
     int ri, rj;
-    lns_ring_cell(T, (int)threadIdx.x, &ri, &rj);
+    lns_ring_cell(T, rt, &ri, &rj);
     const int gi = i0 + ri, gj = j0 + rj;
     if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
       CellLocal rc;
@@ -898,6 +911,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
       lnm_fill<TURB>(P, a, L, lds, gi, gj, ri, rj, rc, mY, &early, &filled);
     }
   }
+  if (tr0) tr[1] = rt_clock();
   // 1b. own cell: G_m, its level-m outputs, kept values for 2. and 3.
   LnmLevel lv;
   u64 CT = 0;
@@ -952,8 +966,29 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
       }
     }
   }
+  if (tr0) tr[2] = rt_clock();
+  if (trl) tr[9] = rt_clock();
+  // species inputs of the predictor, loaded before the barrier (in flight
+  // while the other wavefronts finish their fills)
+  const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
+  const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
+  const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j, iU = idx + n3, iD = idx - n4;
+  real ys0[LNM_NSB], ysL[LNM_NSB], ysR[LNM_NSB], ysU[LNM_NSB], ysD[LNM_NSB], bts[LNM_NSB];
+  if (mine) {
+#pragma unroll
+    for (int s = 0; s < LNM_NSB; s++) {
+      const long o = (long)(s < a.nsp ? s : a.nsp - 1) * N;
+      ys0[s] = a.Ys[o + idx];
+      ysL[s] = a.Ys[o + iL];
+      ysR[s] = a.Ys[o + iR];
+      ysU[s] = a.Ys[o + iU];
+      ysD[s] = a.Ys[o + iD];
+      bts[s] = a.betas[o + idx];
+    }
+  }
   apply_dt(P, sc, slot);   // this step's dt for the predictor and E_{m+1}
   __syncthreads();
+  if (tr0) tr[3] = rt_clock();
   // 2. predict_m, flow and turbulence equations
   ResidualPack r;
   if (RES) {
@@ -969,9 +1004,6 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
     LnmPredictIO io{a, lds, L, lv, bpre, N, idx, idx, idx, idx, idx, sC, sC, sC, sC, sC, aC, aC, bC, bC, gf, {}};
     const bool act = is_active(CT);
     const u64 TT = a.TT[idx];
-    const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
-    const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
-    const long iL = (long)(i - n1) * P.ny + j, iR = (long)(i + n2) * P.ny + j, iU = idx + n3, iD = idx - n4;
     if (!act) {
 #pragma unroll
       for (int q = 0; q < 6; q++) {
@@ -999,6 +1031,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
       const int k = Lns<SK_SGT>::eqk(q);
       a.Sp_out[k * N + idx] = io.sn[k];
     }
+    if (tr0) tr[4] = rt_clock();
     // 3. species: transported ones by the predictor, the bath gas as the
     // remainder of the new rho (predict_cell_t order)
     real ysn[LNM_NSB];
@@ -1007,10 +1040,10 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
 #pragma unroll
     for (int s = 0; s < LNM_NSB; s++) {
       ysn[s] = 0.0;
-      if (s < nsp && (s != bath || !act) && !(a.dbg & 4)) {
+      if (s < nsp && (s != bath || !act)) {
         const long o = (long)s * N;
-        LnmSpeciesIO sio{a, lds, L, N, idx, iL, iR, iU, iD, o, s < bath ? s : s - 1,
-                         io.aL, io.aR, io.bU, io.bD, bC, gf, a.Ys[o + idx], lv.SrcAdd[0], rho_c, 0.0};
+        LnmSpeciesIO sio{a, lds, L, N, idx, iL, iR, iU, iD, o, s < bath ? s : s - 1, io.aL, io.aR, io.bU, io.bD, bC,
+                         gf, ys0[s], ysL[s], ysR[s], ysU[s], ysD[s], bts[s], lv.SrcAdd[0], rho_c, 0.0};
         if (!act) {
           sio.out = sio.ys;
           a.Ys_out[o + idx] = sio.ys;
@@ -1029,6 +1062,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
           ysn[s] = io.sn[I_RHO] - sum;
           a.Ys_out[(long)s * N + idx] = ysn[s];
         }
+    if (tr0) tr[5] = rt_clock();
     // 4. E_{m+1} of the new state, unless the kinetics change it (then hf2d_lnm_hot)
     if (!early) {
       const bool hot = act && io.sn[I_RHO] > 0.0 && lv.Tg >= a.mech->Tchem && P.dt > 0.0;
@@ -1041,7 +1075,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
         base = __shfl(base, leader, WAVE);
         if (hot) a.hot[base + __popcll(ball & ((1ull << lane) - 1ull))] = (int)idx;
       }
-      if (!hot && !(a.dbg & 2)) {
+      if (!hot) {
         const real S4[4] = {io.sn[0], io.sn[1], io.sn[2], io.sn[3]};
         LnmState st;
         if (!mech_state_node(P, *a.mech, nsp, S4, ysn, lv.U, lv.V, lv.Tg, lv.k, CT, lv.BGX, lv.BGY, &st, &dtl, &neg))
@@ -1053,6 +1087,8 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
       }
     }
   }
+  if (tr0) tr[6] = rt_clock();
+  if (trl) tr[10] = rt_clock();
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
@@ -1069,6 +1105,11 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
     for (int q = 1; q < BLOCK / WAVE; q++) mn = fmin(mn, sdt[q]);
     if (serial) mn = fmin(mn, P.dt);
     atomicMin(&sc->dt_bits[slot_next], d_to_bits(mn));
+  }
+  if (tr0) {
+    tr[7] = rt_clock();
+    tr[8] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID: wave/SIMD/CU/SE
+    tr[11] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 }
 
@@ -1393,12 +1434,16 @@ static const LeanEulerK kLeanEuler[2][2] = {{hf2d_lean_euler<false, false>, hf2d
                                             {hf2d_lean_euler<true, false>, hf2d_lean_euler<true, true>}};
 
 using LnsK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*);
-// [k-eps][residual][register budget: default, 3, 5 waves per SIMD]
-static const LnsK kLns[2][2][3] = {
+// [laminar, k-eps, SST, SA][residual][register budget: default, 3, 5 waves per SIMD]
+static const LnsK kLns[4][2][3] = {
     {{hf2d_lns_step<false, SK_SGL>, hf2d_lns_step_occ<false, SK_SGL, 3>, hf2d_lns_step_occ<false, SK_SGL, 5>},
      {hf2d_lns_step<true, SK_SGL>, hf2d_lns_step<true, SK_SGL>, hf2d_lns_step<true, SK_SGL>}},
     {{hf2d_lns_step<false, SK_SGT>, hf2d_lns_step_occ<false, SK_SGT, 3>, hf2d_lns_step_occ<false, SK_SGT, 5>},
-     {hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>}}};
+     {hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>, hf2d_lns_step<true, SK_SGT>}},
+    {{hf2d_lns_step<false, SK_SGT, 3>, hf2d_lns_step_occ<false, SK_SGT, 3, 3>, hf2d_lns_step_occ<false, SK_SGT, 5, 3>},
+     {hf2d_lns_step<true, SK_SGT, 3>, hf2d_lns_step<true, SK_SGT, 3>, hf2d_lns_step<true, SK_SGT, 3>}},
+    {{hf2d_lns_step<false, SK_SGT, 4>, hf2d_lns_step_occ<false, SK_SGT, 3, 4>, hf2d_lns_step_occ<false, SK_SGT, 5, 4>},
+     {hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>}}};
 
 struct DevBuf {
   std::vector<void*> ptrs;
@@ -1464,6 +1509,8 @@ struct DeviceSolver::Impl {
   // lean mechanism step: second level of p and both levels of the stored T
   // (the thermodynamic state T, p, Cp, k of lean_mech.hpp; Cp / k share CP2 / kk2)
   real *p2 = nullptr, *Tst[2] = {nullptr, nullptr};
+  unsigned long long* lnm_trace = nullptr;   // HF2D_LNM_TRACE phase clocks
+  long lnm_trace_n = 0;
   uint8_t* lb;
   uint8_t* gf;   // generic-stepper GF_* traffic flags
   int32_t* wslot;
@@ -1746,6 +1793,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_MECH_LAZY")) mech_lazy = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_CHEM_KERNEL")) chem_kernel = std::atoi(e);   // 1 compiled 2 MFMA 3 generic 4 hiprtc
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
@@ -1932,23 +1980,29 @@ void DeviceSolver::upload() {
     };
     lns_ok = true;
     lns_why.clear();
-    // turbulence: the k-eps family without Chien's model (it reads the
-    // previous p) and no eddy-viscosity term in the dt (the own-cell part of
-    // the next fill has no gradients)
-    const u64 other_models = TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
-                             TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model |
+    // turbulence: one of k-eps (without Chien's model: it reads the previous
+    // p), k-omega SST or Spalart-Allmaras, and no eddy-viscosity term in the
+    // dt (the own-cell part of the next fill has no gradients)
+    const u64 other_models = TCT_Prandtl_Model | TCT_Integral_Model | TCT_k_omega_Model | TCT_Baldwin_Lomax_Model |
                              TCT_nut_92_Model | TCT_Smagorinsky_Model;
+    lns_turb = 2;
+    u64 models = 0;
     if (sk_mode != SK_SGL && sk_mode != SK_SGT) no("not single-gas N-S");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
     else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
-    else if (sk_mode == SK_SGT && cs.cfg.TurbExtModel == TEM_k_eps_Chien) no("Chien k-eps");
     else if (sk_mode == SK_SGT && cs.cfg.ViscousCFL > 0) no("viscous CFL with eddy viscosity");
     else
       for (long q = 0; q < N && lns_ok; q++) {
         if (h.gf[q] & GF_SRC) no("volume sources");
         else if (!has_all(h.CT[q], CT_SOLID) && !has_all(h.CT[q], CT_NODE_IS_SET)) no("unset non-solid node");
-        else if (h.TT[q] & other_models) no("turbulence model other than k-eps");
+        else if (h.TT[q] & other_models) no("turbulence model other than k-eps, SST or SA");
+        else models |= h.TT[q] & (TCT_k_eps_Model | TCT_k_omega_SST_Model | TCT_Spalart_Allmaras_Model);
       }
+    // one model per kernel (fill_node's turbulence set)
+    if (lns_ok && models == TCT_k_omega_SST_Model) lns_turb = 3;
+    else if (lns_ok && models == TCT_Spalart_Allmaras_Model) lns_turb = 4;
+    else if (lns_ok && models != 0 && models != TCT_k_eps_Model) no("more than one turbulence model");
+    else if (lns_ok && models == TCT_k_eps_Model && cs.cfg.TurbExtModel == TEM_k_eps_Chien) no("Chien k-eps");
     if (lns_ok && !m.CP2) {
       m.CP2 = m.mem.alloc<real>(N);
       m.mu2 = m.mem.alloc<real>(N);
@@ -2160,9 +2214,11 @@ void DeviceSolver::lns_materialize() {
   SoA out = m.view(h, sbuf, abuf, dsbuf, pbuf);
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
   const unsigned nb = (unsigned)((c1 - c0 + BLOCK - 1) / BLOCK);
+  // (the split fill F_{m+1} belongs to step m: its dt is slot m % 3, which
+  // step m+1 has not reset yet; SST's point-implicit destruction reads it)
   if (sk_mode == SK_SGT)
     hipLaunchKernelGGL((hf2d_fill<SK_SGT, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
-                       (int)(nstep % 3), -1, 0, 1);
+                       (int)((nstep + 2) % 3), -1, 0, 1);
   else
     hipLaunchKernelGGL((hf2d_fill<SK_SGL, 1>), dim3(nb), dim3(BLOCK), 0, m.stream, P, sin, sin, out, c0, c1, m.sc,
                        (int)(nstep % 3), -1, 0, 1);
@@ -3102,12 +3158,28 @@ static const LnmK kLnm[2][2] = {{hf2d_lnm_step<false, 0>, hf2d_lnm_step<false, 3
 
 // One lean mechanism step (lean_mech.hpp): tile kernel, kinetics of the
 // listed cells in place on the new species, their state kernel.
+std::vector<unsigned long long> DeviceSolver::lnm_trace_fetch() {
+  synchronize();
+  Impl& m = *impl;
+  std::vector<unsigned long long> v((size_t)m.lnm_trace_n * 12);
+  if (!v.empty()) HIP_CHECK(hipMemcpy(v.data(), m.lnm_trace, v.size() * 8, hipMemcpyDeviceToHost));
+  return v;
+}
+
 void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int slot_next, int serial) {
   Impl& m = *impl;
   hipStream_t st = m.stream;
   LnmArrays a = m.lnm_arrays(h, sbuf, pbuf, cbuf, dsbuf, abuf);
-  if (const char* e = std::getenv("HF2D_LNM_DBG")) a.dbg = std::atoi(e);
-  const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, LNM_TILE, 1);
+  if (std::getenv("HF2D_LNM_TRACE")) {   // phase trace of every step (the last one is kept)
+    const long nwg = (long)((P.i1 - P.i0 + lnm_ti - 1) / lnm_ti) * ((P.ny + LNM_TILE - 1) / LNM_TILE);
+    if (!m.lnm_trace || m.lnm_trace_n < nwg) {
+      m.lnm_trace = m.mem.alloc<unsigned long long>(nwg * 12);
+      m.lnm_trace_n = nwg;
+    }
+    a.tr = m.lnm_trace;
+  }
+  if (lnm_ti < 1 || lnm_ti > BLOCK / LNM_TILE) lnm_ti = BLOCK / LNM_TILE;
+  const LeanTile T = lnm_tile(P.i1 - P.i0, P.ny, lnm_ti);
   const LnmLayout L(T.TI, T.TJ, m.nsp - 1);
   const size_t shmem = (size_t)L.total() * sizeof(real);
   const LnmK k = kLnm[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0];
@@ -3309,7 +3381,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       cbuf = 1;
     } else {
       lnm_step(P, want_res, slot, slot_next, serial);
-      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, LNM_TILE, 1);
+      const LeanTile T = lnm_tile(P.i1 - P.i0, P.ny, lnm_ti);
       nres = (unsigned)(T.nbi * T.nbj);
     }
   } else if (lns_step_ok(P)) {
@@ -3331,7 +3403,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // 2000x200: 110.7 -> 98.8 us/step); the laminar one is best unbounded
       const int occ = lns_occ > 0 ? lns_occ : (t2 ? 3 : 0);
       // (a residual step runs the compiler's register budget)
-      const LnsK lk = kLns[t2][want_res][want_res ? 0 : (occ == 5 ? 2 : occ == 3 ? 1 : 0)];
+      const int tv = !t2 ? 0 : lns_turb == 3 ? 2 : lns_turb == 4 ? 3 : 1;
+      const LnsK lk = kLns[tv][want_res][want_res ? 0 : (occ == 5 ? 2 : occ == 3 ? 1 : 0)];
       hipLaunchKernelGGL(lk, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial, m.partials);
       HIP_CHECK(hipGetLastError());
       nres = (unsigned)ntile;

@@ -179,6 +179,7 @@ class DeviceSolver : public SolverBase {
   int cbuf = 0;           // lean N-S: CP/mu/lam/k level ping-pong (0: the generic arrays)
   long lns_steps = 0;
   int lns_occ = 0;
+  int lns_turb = 2;       // turbulence set of the SGT kernel: 2 k-eps, 3 SST, 4 Spalart-Allmaras
   int lns_prev_mu_t = -1;  // is_mu_t of the previous step (the split fill F_m ran with it)        // 0: compiler register budget; 5 / 6: waves-per-SIMD budget
   void lns_materialize();
   // Mechanism mode (SK_MECH N-S, laminar or k-omega SST): the lean step of
@@ -189,6 +190,8 @@ class DeviceSolver : public SolverBase {
   std::string lnm_why;
   int lnm_turb = 0;       // fill_node turbulence set of the kernel: 0 none, 3 SST
   long lnm_steps = 0;
+  int lnm_ti = 16;
+  std::vector<unsigned long long> lnm_trace_fetch();   // HF2D_LNM_TRACE: 12 clocks / ids per workgroup        // tile columns (16 rows): 16 or 12 (lean_mech.hpp lnm_tile)
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
   void lean_materialize();

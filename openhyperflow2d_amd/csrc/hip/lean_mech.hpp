@@ -76,8 +76,23 @@ struct LnmArrays {
   const uint8_t* nb = nullptr;
   const uint8_t* gf = nullptr;
   int* hot = nullptr;   // reacting cells of the step (kinetics list)
-  int dbg = 0;          // timing experiments only (HF2D_LNM_DBG): 1 no ring fill, 2 no state, 4 no species
+  unsigned long long* tr = nullptr;   // phase trace (HF2D_LNM_TRACE): 12 clocks per workgroup
 };
+
+// Tile of the lean mechanism step: TI columns x LNM_TILE rows, one cell per
+// thread.  TI = 16: the 64 ring cells take a second fill on wavefront 0;
+// TI = 12: 192 own + 56 ring cells, every thread one fill.
+inline LeanTile lnm_tile(int ncols, int ny, int ti) {
+  LeanTile T;
+  T.TJ = LNM_TILE;
+  T.TI = T.TIh = ti;
+  T.CPT = 1;
+  T.W = T.TJ + 2;
+  T.NC = (T.TI + 2) * T.W;
+  T.nbi = (ncols + T.TI - 1) / T.TI;
+  T.nbj = (ny + T.TJ - 1) / T.TJ;
+  return T;
+}
 
 // LDS planes of a TI x TJ tile.  Flow / turbulence equation q (Lns<SK_SGT>::q):
 // S over the tile + cross ring, A over the tile + left/right ring, B over the
@@ -348,7 +363,10 @@ struct LnmPredictIO {
 };
 
 // predict_core() accessor of species s (SpeciesPredictIO with the fluxes in
-// the LDS planes).  F_s of the axisymmetric predictor equals B_s (FT = 1).
+// the LDS planes and the species' own / neighbour values and blending factor
+// loaded before the workgroup barrier: a load after a store of the previous
+// species cannot be hoisted, so per-species loads were one memory latency
+// each).  F_s of the axisymmetric predictor equals B_s (FT = 1).
 struct LnmSpeciesIO {
   static constexpr int NE = 1;
   static constexpr bool skip(int) { return false; }
@@ -359,12 +377,12 @@ struct LnmSpeciesIO {
   long N, idx, iL, iR, iU, iD, o;
   int t, aL, aR, bU, bD, bC;
   uint8_t gf;
-  real ys, srcadd_rho, rho_c, out;
+  real ys, yl, yr, yu, yd, bt, srcadd_rho, rho_c, out;
   HF_HD real S(int) const { return ys; }
-  HF_HD real SL(int) const { return a.Ys[o + iL]; }
-  HF_HD real SR(int) const { return a.Ys[o + iR]; }
-  HF_HD real SU(int) const { return a.Ys[o + iU]; }
-  HF_HD real SD(int) const { return a.Ys[o + iD]; }
+  HF_HD real SL(int) const { return yl; }
+  HF_HD real SR(int) const { return yr; }
+  HF_HD real SU(int) const { return yu; }
+  HF_HD real SD(int) const { return yd; }
   HF_HD real AL(int) const { return lds[L.osA + t * L.NA + aL]; }
   HF_HD real AR(int) const { return lds[L.osA + t * L.NA + aR]; }
   HF_HD real BU(int) const { return lds[L.osB + t * L.NB + bU]; }
@@ -373,7 +391,7 @@ struct LnmSpeciesIO {
   HF_HD real dxR(int) const { return a.dSdxs_in ? a.dSdxs_in[o + iR] : 0.0; }
   HF_HD real dyU(int) const { return a.dSdys_in ? a.dSdys_in[o + iU] : 0.0; }
   HF_HD real dyD(int) const { return a.dSdys_in ? a.dSdys_in[o + iD] : 0.0; }
-  HF_HD real beta(int) const { return a.betas[o + idx]; }
+  HF_HD real beta(int) const { return bt; }
   HF_HD real F(int) const { return lds[L.osB + t * L.NB + bC]; }
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int) const { return (gf & GF_SRCADD) ? srcadd_rho * (ys / rho_c) : 0.0; }

@@ -77,8 +77,11 @@ constexpr int LNS_NL = 4;
 // one memory latency instead of a chain of dependent ones.  Inputs the fill
 // rewrites before any use (p, Diff, lam_t; k-eps: the k/eps fluxes) return
 // +0; wall / inactive-only fields load on demand.
-template <int MODE>
+// TURB: fill_node's turbulence-model set of the SGT kernel (2 k-eps, 3 SST, 4
+// Spalart-Allmaras; physics.hpp)
+template <int MODE, int TURB = 2>
 struct LnsFillIO {
+  static constexpr int TURB_SET = TURB;
   static constexpr bool T2 = MODE == SK_SGT;
   static constexpr int NL = Lns<MODE>::NL;
   const LnsArrays& a;
@@ -131,7 +134,11 @@ struct LnsFillIO {
     nbit[ND_U] = n3;
     nbit[ND_D] = n4;
   }
-  HF_HD bool keps() const { return has_all(tt, TCT_k_eps_Model); }
+  // the turbulence fluxes fill_node rewrites on every node of the model (SA
+  // leaves them on walls / NT_FC nodes: loaded)
+  HF_HD bool keps() const {
+    return (TURB == 2 && has_all(tt, TCT_k_eps_Model)) || (TURB == 3 && has_all(tt, TCT_k_omega_SST_Model));
+  }
   HF_HD u64 CT() const { return ct; }
   HF_HD u64 TT() const { return tt; }
   HF_HD uint8_t gf() const { return g; }
@@ -193,6 +200,7 @@ struct LnsLevel {
 // with an eddy viscosity).
 template <int MODE>
 struct LnsOwnIO {
+  static constexpr int TURB_SET = 0;   // dt does not depend on the turbulence model
   const real* sn;   // Sp^{m+1} by equation index
   const LnsLevel<MODE>& v;
   u64 ct, tt;
@@ -327,14 +335,14 @@ HF_HD inline void lns_ring_cell(const LeanTile& T, int r, int* ii, int* jj) {
 
 // F_m of global cell (gi, gj) into LDS cell cc (committed S, A, B of the
 // live equations); *early / *filled as fill_compute's.
-template <int MODE>
+template <int MODE, int TURB = 2>
 HF_HD inline void lns_fill_to_lds(const StepParams& P, const LnsArrays& a, int gi, int gj, real* lds, int NC, int cc,
                                   CellLocal& c, bool* early, bool* filled, int* neg_dummy) {
   constexpr int NL = Lns<MODE>::NL;
-  LnsFillIO<MODE> io(a, gi, gj, P.nx, P.ny);
+  LnsFillIO<MODE, TURB> io(a, gi, gj, P.nx, P.ny);
   real mY[1], mgx[1], mgy[1];
-  (void)fill_compute<MODE, 1, LnsFillIO<MODE>, true>(P, io, c, mY, mgx, mgy, nullptr, 0, gi, gj, true, neg_dummy,
-                                                       early, filled);
+  (void)fill_compute<MODE, 1, LnsFillIO<MODE, TURB>, true>(P, io, c, mY, mgx, mgy, nullptr, 0, gi, gj, true,
+                                                             neg_dummy, early, filled);
 #pragma unroll
   for (int q = 0; q < NL; q++) {
     const int k = Lns<MODE>::eqk(q);

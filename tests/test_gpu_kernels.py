@@ -446,7 +446,8 @@ def test_rccl_single_rank_comm(gpu, tmp_path):
     assert any(p.suffix == ".plt" for p in tmp_path.iterdir())
 
 
-@pytest.mark.parametrize("deck", ["step", "step_ref_ns", "step_graphs", "resonator", "resonator_graphs"])
+@pytest.mark.parametrize("deck", ["step", "step_ref_ns", "step_graphs", "resonator", "resonator_graphs", "sst_plate",
+                                  "sst_plate_graphs", "sa_plate"])
 def test_lean_ns_equals_split(gpu, deck):
     """Lean laminar N-S kernel (hip/lean_ns.hpp: fluxes recomputed in the LDS
     tile, one kernel per step) == the split predict + fill kernels on every
@@ -460,6 +461,10 @@ def test_lean_ns_equals_split(gpu, deck):
         text = decks.set_key(read_deck("Step.dat"), "ProblemType", 1)   # reference deck, laminar N-S
     elif deck.startswith("resonator"):   # axisymmetric k-eps, no-slip tube walls (turbulent lean kernel)
         text = decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
+    elif deck.startswith("sst_plate") or deck == "sa_plate":   # k-omega SST / Spalart-Allmaras kernels
+        # (no solid cells: the wall heat kernels have nothing to do)
+        text = decks.set_key(decks.flat_plate(200, 60, turbulence=6 if deck.startswith("sst") else 3, nmax=10 ** 6,
+                                              nout=10 ** 5), "isAdiabaticWall", 1)
     else:
         text = decks.wedge15(200, 60, navier_stokes=True, turbulence=4, nmax=10 ** 6, nout=10 ** 5)
     a = gpu.Simulation(text, "gpu")
@@ -469,6 +474,8 @@ def test_lean_ns_equals_split(gpu, deck):
     if not graphs:
         a.solver.use_graph = b.solver.use_graph = False
     assert a.solver.lns_ok, a.solver.lns_why
+    if deck.startswith("sst") or deck.startswith("sa"):
+        assert a.solver.lns_turb == (3 if deck.startswith("sst") else 4)
     sched = [(4, True), (30, False), (6, True), (19, False)] if not graphs else [(40, False), (13, True), (61, False)]
     for n, res in sched:
         a.step(n, residual=res)

@@ -146,7 +146,7 @@ def test_file_mechanism_runs_the_rtc_kernel_and_matches_cpu(gpu, tmp_path):
         assert np.abs(a - b).max() <= 1e-9 * max(np.abs(b).max(), 1e-30), f
 
 
-@pytest.mark.parametrize("deck", ["sst", "sst_graphs", "laminar", "hot"])
+@pytest.mark.parametrize("deck", ["sst", "sst_graphs", "laminar", "hot", "sst_ti12"])
 def test_lean_mech_equals_split(gpu, deck):
     """Lean mechanism step (hip/lean_mech.hpp: flow, turbulence and species
     fluxes recomputed in the LDS tile, the Newton T once per cell and step,
@@ -164,6 +164,8 @@ def test_lean_mech_equals_split(gpu, deck):
     a = gpu.Simulation(text, "gpu")
     b = gpu.Simulation(text, "gpu")
     b.solver.lean_mech = False
+    if deck.endswith("_ti12"):   # 12 x 16 tiles: ring cells on their own threads
+        a.solver.lnm_ti = 12
     graphs = deck.endswith("_graphs")
     if not graphs:
         a.solver.use_graph = b.solver.use_graph = False
