@@ -25,6 +25,7 @@ void Config::load_globals(InputDeck& d) {
   CFL = d.get_float("CFL");
   CFL_Scenario = d.get_table("CFL_Scenario");
   ViscousCFL = d.get_float_or("ViscousCFL", 0.0);
+  SSTWallDistance = d.get_float_or("SSTWallDistance", 0.5);
   ThreadBlockSize = d.get_int_or("ThreadBlockSize", 0);
   NSaveStep = d.get_int("NSaveStep");
   Nmax = d.get_int("Nmax");
@@ -100,6 +101,7 @@ FillParams Config::fill_params() const {
   P.dx = dx;
   P.dy = dy;
   for (int i = 0; i < NSPEC; i++) P.Hu[i] = Hu[i];
+  P.sst_d1 = SSTWallDistance;
   return P;
 }
 

@@ -33,6 +33,7 @@ struct FillParams {
   int isSrcAdd = 0;
   real turb_I = 0.005;    // FlowNodeTurbulence2D::I
   int sst_version = 2003; // new model (not in reference)
+  real sst_d1 = 0.5;      // SST wall omega distance / min(dx, dy) (Config::SSTWallDistance)
   real dt = 0.0;          // time step of the fill's step (SST point-implicit destruction)
 };
 
@@ -101,7 +102,7 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   }
   if (has_all(n.CT, CT_WALL_NO_SLIP) || has_all(n.CT, CT_WALL_LAW)) {
     // Menter wall BC: k = 0, omega = 60 nu / (beta1 d^2)
-    const real d1 = hf_min(P.dx, P.dy) * 0.5;
+    const real d1 = hf_min(P.dx, P.dy) * P.sst_d1;
     n.S[I_K] = 0.0;
     n.S[I_OMEGA] = rho * 60.0 * (n.mu / rho) / (b1 * d1 * d1);
   }
