@@ -80,6 +80,7 @@ py::array_t<double> field_scalar(const Field& J, const std::string& name) {
       const CellRecord& c = J.at(i, j);
       double v = 0;
       if (name.size() == 2 && name[0] == 'S') v = c.S[name[1] - '0'];
+      else if (name.size() == 5 && name.compare(0, 4, "beta") == 0) v = c.beta[name[4] - '0'];   // blending factor
       else if (name == "rho") v = c.S[0];
       else if (name == "U") v = c.U;
       else if (name == "V") v = c.V;

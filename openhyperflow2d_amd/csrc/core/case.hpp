@@ -54,9 +54,8 @@ struct Config {
   // dt <= ViscousCFL * rho / ((mu + mu_t) (1/dx^2 + 1/dy^2)); 0 = off (reference)
   real ViscousCFL = 0;
   // new key: k-omega SST wall omega = 60 nu / (beta1 d1^2) with d1 = SSTWallDistance *
-  // min(dx, dy); 0.5 (default) places it half a cell off the wall node, 1.0 is Menter's
-  // first-cell distance
-  real SSTWallDistance = 0.5;
+  // min(dx, dy): 1.0 (default) is Menter's distance of the first cell off the wall node
+  real SSTWallDistance = 1.0;
   // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
   // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
   int ThreadBlockSize = 0;

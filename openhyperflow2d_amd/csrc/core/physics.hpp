@@ -33,7 +33,7 @@ struct FillParams {
   int isSrcAdd = 0;
   real turb_I = 0.005;    // FlowNodeTurbulence2D::I
   int sst_version = 2003; // new model (not in reference)
-  real sst_d1 = 0.5;      // SST wall omega distance / min(dx, dy) (Config::SSTWallDistance)
+  real sst_d1 = 1.0;      // SST wall omega distance / min(dx, dy) (Config::SSTWallDistance)
   real dt = 0.0;          // time step of the fill's step (SST point-implicit destruction)
 };
 

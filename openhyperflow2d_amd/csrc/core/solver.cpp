@@ -49,7 +49,9 @@ void HostArrays::allocate(int X, int Yn) {
 
 void HostArrays::from_field(const Field& J, int gi0) {
   for (int li = 0; li < nx; li++) {
-    const int gi = gi0 + li;
+    // (a second ghost column outside the resident ones -- device N-S strips --
+    // starts as a copy of the nearest; the first lean exchange refreshes it)
+    const int gi = std::min(std::max(gi0 + li, J.i0), J.i0 + J.nxl - 1);
     for (int j = 0; j < ny; j++) {
       const long idx = (long)li * ny + j;
       const CellRecord& c = J.at(gi, j);
@@ -194,7 +196,7 @@ void HostArrays::mech_from_case(const Case& cs, int gi0) {
   if (!mech) return;
   const real FT = (real)cs.cfg.FT;
   for (int li = 0; li < nx; li++) {
-    const int gi = gi0 + li;
+    const int gi = std::min(std::max(gi0 + li, cs.J.i0), cs.J.i0 + cs.J.nxl - 1);   // (see from_field)
     for (int j = 0; j < ny; j++) {
       const long idx = (long)li * ny + j;
       const CellRecord& c = cs.J.at(gi, j);

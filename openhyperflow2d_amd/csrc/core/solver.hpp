@@ -202,7 +202,7 @@ class CpuSolver : public SolverBase {
   // groups: 0 = predicted state (N-S gradients), 1 = post-fill state,
   // 2 = wall-heat per-direction fluxes
   // 3 = lean inviscid state (lean_euler.hpp)
-  enum { HALO_MID = 0, HALO_STATE = 1, HALO_QDIR = 2, HALO_LEAN = 3 };
+  enum { HALO_MID = 0, HALO_STATE = 1, HALO_QDIR = 2, HALO_LEAN = 3, HALO_LNS = 4 };   // HALO_LNS: lean N-S / mechanism (device)
   int halo_doubles(int group) const;
   void pack_column(int group, int local_i, real* buf) const;
   void unpack_column(int group, int local_i, const real* buf);

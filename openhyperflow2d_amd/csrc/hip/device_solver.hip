@@ -314,8 +314,13 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
 
 // Halo pack: nf field columns (each ny contiguous doubles at src[f] + col*ny)
 constexpr int MAX_HALO_FIELDS = 128;   // 4*NEQ + 5 state fields + up to 16 species x 4
+// Halo field list: entry f is column (first + o[f]) / (last - o[f]) of
+// field f on the sending side and ghost column (ghostL - o[f]) / (ghostR +
+// o[f]) on the receiving side: o = 1 carries the second column of a
+// two-column halo (the lean N-S / mechanism kernels on strips).
 struct ColList {
   real* f[MAX_HALO_FIELDS];
+  unsigned char o[MAX_HALO_FIELDS] = {};
   int nf;
 };
 constexpr long P2P_SPIN_LIMIT = 1L << 26;   // ~3 s of s_sleep polling, then give up (neg_T bit 2)
@@ -696,6 +701,13 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       lns_fill_to_lds<MODE, TURB>(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
     }
   }
+  // 1a'. a strip's first ghost column inside a partial last tile: its fill
+  // is a neighbour's (the ring covers it when the tile is full)
+  if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
+    CellLocal gc;
+    bool ge, gfl;
+    lns_fill_to_lds<MODE, TURB>(P, a, i, j, lds, NC, c, gc, &ge, &gfl, &dummy);
+  }
   // 1b. own cell: F_m, its level-m outputs, kept values for 2./3.
   LnsLevel<MODE> lv;
   u64 CT = 0, TT = 0;
@@ -912,6 +924,13 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
     }
   }
   if (tr0) tr[1] = rt_clock();
+  // 1a'. a strip's first ghost column inside a partial last tile (see lns)
+  if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
+    CellLocal gc;
+    real mY[LNM_NSB];
+    bool ge, gfl;
+    lnm_fill<TURB>(P, a, L, lds, i, j, ii, jj, gc, mY, &ge, &gfl);
+  }
   // 1b. own cell: G_m, its level-m outputs, kept values for 2. and 3.
   LnmLevel lv;
   u64 CT = 0;
@@ -1224,7 +1243,7 @@ __global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, re
   if (right) t -= cnt;
   if (t >= cnt || !(sides & (right ? 2 : 1))) return;
   const int f = t / ny, j = t - f * ny;
-  (right ? bufR : bufL)[t] = L.f[f][(long)(right ? colR : colL) * ny + j];
+  (right ? bufR : bufL)[t] = L.f[f][(long)(right ? colR - L.o[f] : colL + L.o[f]) * ny + j];
 }
 // Also folds the dt gathered from the other ranks (ndt > 0: dtr[q], q != self)
 // into the next dt slot: MIN of positive doubles, exact in any order.
@@ -1242,7 +1261,7 @@ __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* 
   if (right) t -= cnt;
   if (t >= cnt || !(sides & (right ? 2 : 1))) return;
   const int f = t / ny, j = t - f * ny;
-  L.f[f][(long)(right ? colR : colL) * ny + j] = (right ? bufR : bufL)[t];
+  L.f[f][(long)(right ? colR + L.o[f] : colL - L.o[f]) * ny + j] = (right ? bufR : bufL)[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1299,14 +1318,14 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
     real* dst = a.peer_recv_l + ((long)par * 2 + 1) * a.cap;   // left neighbour receives "from right"
     for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
       const int f = t / ny, j = t - f * ny;
-      p2p_store(dst + t, a.L.f[f][(long)a.first * ny + j]);
+      p2p_store(dst + t, a.L.f[f][(long)(a.first + a.L.o[f]) * ny + j]);
     }
   }
   if (a.sides & 2) {
     real* dst = a.peer_recv_r + ((long)par * 2) * a.cap;       // right neighbour receives "from left"
     for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
       const int f = t / ny, j = t - f * ny;
-      p2p_store(dst + t, a.L.f[f][(long)a.last * ny + j]);
+      p2p_store(dst + t, a.L.f[f][(long)(a.last - a.L.o[f]) * ny + j]);
     }
   }
   const double mydt = bits_to_d(a.sc->dt_bits[a.dslot]);
@@ -1362,7 +1381,7 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
         const bool right = !(a.sides & 1) || t >= a.cnt;
         const int tt = (a.sides & 1) && right ? t - a.cnt : t;
         const int f = tt / ny, j = tt - f * ny;
-        a.L.f[f][(long)(right ? a.ghostR : a.ghostL) * ny + j] = v[u];
+        a.L.f[f][(long)(right ? a.ghostR + a.L.o[f] : a.ghostL - a.L.o[f]) * ny + j] = v[u];
       }
     }
   }
@@ -1796,7 +1815,11 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
-  const int lh = gi0 > 0 ? 1 : 0, rh = gi1 < c.J.nx ? 1 : 0;
+  // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
+  // evaluate the fill of the first ghost column, which reads the second);
+  // the split kernels read one, the inviscid ones one
+  const int G = c.cfg.ProblemType == SM_NS ? 2 : 1;
+  const int lh = gi0 > 0 ? G : 0, rh = gi1 < c.J.nx ? G : 0;
   l_off = lh;
   h.allocate((gi1 - gi0) + lh + rh, c.J.ny);
   const long N = h.N;
@@ -1989,7 +2012,7 @@ void DeviceSolver::upload() {
     u64 models = 0;
     if (sk_mode != SK_SGL && sk_mode != SK_SGT) no("not single-gas N-S");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
-    else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
+    else if ((gi0 > 0 && l_off < 2) || (gi1 < cs.J.nx && h.nx - l_off - (gi1 - gi0) < 2)) no("one ghost column");
     else if (sk_mode == SK_SGT && cs.cfg.ViscousCFL > 0) no("viscous CFL with eddy viscosity");
     else
       for (long q = 0; q < N && lns_ok; q++) {
@@ -2041,7 +2064,7 @@ void DeviceSolver::upload() {
     else if (cs.cfg.ProblemType != SM_NS) no("not Navier-Stokes");
     else if (m.nsp > LNM_NSB || m.nsp < 2) no("species count outside the kernel's block");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
-    else if (gi0 != 0 || gi1 != cs.J.nx) no("strip decomposition");
+    else if ((gi0 > 0 && l_off < 2) || (gi1 < cs.J.nx && h.nx - l_off - (gi1 - gi0) < 2)) no("one ghost column");
     else if (cs.cfg.ViscousCFL > 0) no("viscous CFL");
     else if (h.ny < LNM_TILE) no("grid lower than one tile");
     else
@@ -2604,9 +2627,61 @@ int DeviceSolver::split_mode() const {
 }
 
 void DeviceSolver::halo_fields(int group, std::vector<real*>& f, bool full) const {
+  std::vector<unsigned char> o;
+  halo_fields(group, f, o, full);
+}
+
+void DeviceSolver::halo_fields(int group, std::vector<real*>& f, std::vector<unsigned char>& o, bool full) const {
   const Impl& m = *impl;
   const long N = h.N;
   f.clear();
+  o.clear();
+  if (group == CpuSolver::HALO_LNS) {
+    // lean N-S / mechanism strips (two ghost columns): what the next lean step
+    // reads of them -- the inner ghost column is a ring cell (its fill reads
+    // its predicted state, lagged primitives, transport and thermodynamic
+    // state), the outer one only the neighbour values of that fill (state,
+    // species, lagged U, V, T)
+    const int cb = cbuf;
+    auto two = [&](real* p) {
+      f.push_back(p);
+      o.push_back(0);
+      f.push_back(p);
+      o.push_back(1);
+    };
+    auto one = [&](real* p) {
+      f.push_back(p);
+      o.push_back(0);
+    };
+    for (int k = 0; k < NEQ; k++)
+      if (sk_live(m.mech ? SK_MECH : sk_mode, k)) two(m.S[1 - sbuf] + (long)k * N);
+    two(m.U[1 - pbuf]);
+    two(m.V[1 - pbuf]);
+    two(m.Tg[1 - pbuf]);
+    real* const mux[2] = {m.mu, m.mu2};
+    real* const lamx[2] = {m.lam, m.lam2};
+    real* const mutx[2] = {m.mu_t, m.mu_t2};
+    real* const cpx[2] = {m.CP, m.CP2};
+    real* const kkx[2] = {m.kk, m.kk2};
+    one(mux[1 - cb]);
+    one(lamx[1 - cb]);
+    one(mutx[1 - cb]);
+    one(cpx[1 - cb]);
+    one(kkx[1 - cb]);
+    if (m.mech) {
+      real* const px[2] = {m.p, m.p2};
+      one(px[1 - cb]);
+      one(m.Tst[1 - cb]);
+      for (int q = 0; q < m.nsp; q++) two(m.Ys[sbuf] + (long)q * N);
+    }
+    if (any_cauchy_x) {   // dS/dx of the ghost column (Cauchy neighbours of the edge cells)
+      for (int k = 0; k < NEQ; k++)
+        if (sk_live(m.mech ? SK_MECH : sk_mode, k)) one(m.dSdx[dsbuf] + (long)k * N);
+      if (m.dSdxs[0])
+        for (int q = 0; q < m.nsp; q++) one(m.dSdxs[dsbuf] + (long)q * N);
+    }
+    return;
+  }
   full = full || !halo_compact;
   const int mode = split_mode();
   auto add_eq = [&](real* base) {
@@ -2668,12 +2743,18 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
   if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
   const int ny = h.ny;
   std::vector<real*> fl;
-  halo_fields(group, fl, full);
+  std::vector<unsigned char> fo;
+  halo_fields(group, fl, fo, full);
   if (group == CpuSolver::HALO_STATE) ghost_mode = (full || !halo_compact) ? -1 : split_mode();
+  if (group == CpuSolver::HALO_LNS) ghost_stale = true;   // lean representation in the ghosts
+  else if (group == CpuSolver::HALO_STATE) ghost_stale = false;
   if (fl.size() > (size_t)MAX_HALO_FIELDS) throw std::runtime_error("halo: too many exchanged fields");
   ColList L;
   L.nf = (int)fl.size();
-  for (int k = 0; k < L.nf; k++) L.f[k] = fl[k];
+  for (int k = 0; k < L.nf; k++) {
+    L.f[k] = fl[k];
+    L.o[k] = k < (int)fo.size() ? fo[k] : 0;
+  }
   const int cnt = L.nf * ny;
   const unsigned nb2 = (unsigned)((2 * cnt + BLOCK - 1) / BLOCK);
   const int first = l_off, last = l_off + (gi1 - gi0) - 1;
@@ -2687,8 +2768,8 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     a.L = L;
     a.first = first;
     a.last = last;
-    a.ghostL = 0;
-    a.ghostR = h.nx - 1;
+    a.ghostL = l_off - 1;
+    a.ghostR = l_off + (gi1 - gi0);
     a.ny = ny;
     a.cnt = cnt;
     a.sides = sides;
@@ -2751,7 +2832,7 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
       }
   NCCL_CHECK(ncclGroupEnd());
   }
-  hipLaunchKernelGGL(hf2d_unpack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, st, L, 0, h.nx - 1, ny,
+  hipLaunchKernelGGL(hf2d_unpack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, st, L, l_off - 1, l_off + (gi1 - gi0), ny,
                      m.halo_recv[0], m.halo_recv[1], sides, m.sc, gather_dt ? dt_slot : 0, m.dt_recv,
                      gather_dt ? m.nranks : 0, m.rank);
   HIP_CHECK(hipGetLastError());
@@ -2780,7 +2861,7 @@ std::string DeviceSolver::p2p_probe() {
   if (!m.p2p.on) throw std::runtime_error("p2p_probe: p2p transport not active");
   hipStream_t st = m.stream;
   const int ny = h.ny;
-  const int first = l_off, last = l_off + (gi1 - gi0) - 1, gl = 0, gr = h.nx - 1;
+  const int first = l_off, last = l_off + (gi1 - gi0) - 1, gl = l_off - 1, gr = l_off + (gi1 - gi0);
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   std::vector<real*> fl;
   halo_fields(CpuSolver::HALO_STATE, fl);
@@ -2927,7 +3008,8 @@ void DeviceSolver::p2p_complete() {
   L.f[L.nf++] = m.U[pbuf];
   L.f[L.nf++] = m.V[pbuf];
   L.f[L.nf++] = m.P2[pbuf];
-  hipLaunchKernelGGL(hf2d_p2p_complete, dim3(1), dim3(P2P_THREADS), 0, m.stream, L, 0, h.nx - 1, h.ny, L.nf * h.ny,
+  hipLaunchKernelGGL(hf2d_p2p_complete, dim3(1), dim3(P2P_THREADS), 0, m.stream, L, l_off - 1, l_off + (gi1 - gi0), h.ny,
+                     L.nf * h.ny,
                      fused_args(), m.sc, (int)(nstep % 3));
   HIP_CHECK(hipGetLastError());
 }
@@ -3070,6 +3152,9 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
     // single-gas N-S: only the live equations and fields move (SK_SGL/SK_SGT);
     // mechanism mode: SK_MECH (Euler and N-S)
     const int mode = m.mech ? SK_MECH : (P.sm == SM_NS && sgl) ? sk_mode : SK_GENERIC;
+    // the ghost columns hold the lean N-S / mechanism representation (the
+    // record was materialised): the split step's halo first
+    if (ghost_stale) exchange(CpuSolver::HALO_STATE);
     // the ghost columns were last exchanged for a single-gas specialisation
     // and this step is generic (sgl switched off): refresh them in full first
     if (ghost_mode >= 0 && ghost_mode != SK_GENERIC && mode == SK_GENERIC)
@@ -3102,7 +3187,8 @@ void DeviceSolver::step_split(const StepParams& P0, bool want_res, int slot, int
       // operator-split kinetics: Ys[1-sbuf] -> Ys[sbuf]; N-S strips also react
       // their ghost columns (exchanged above; same inputs as on the owner)
       const bool ghosts = multi && P.sm == SM_NS;
-      const long k0 = ghosts ? 0 : c0, k1 = ghosts ? h.N : c1;
+      const long k0 = ghosts ? c0 - (c0 > 0 ? h.ny : 0) : c0;
+      const long k1 = ghosts ? c1 + (c1 < h.N ? h.ny : 0) : c1;
       const unsigned nbk = (unsigned)((k1 - k0 + BLOCK - 1) / BLOCK);
       launch_chem(P, sin, out, k0, k1, nbk, slot);
       m.mech_view(sin, sbuf, 1 - dsbuf);   // the fill reads the post-chemistry species
@@ -3146,7 +3232,7 @@ bool DeviceSolver::lns_entry(const StepParams& P0) const {
 bool DeviceSolver::lnm_step_ok(const StepParams& P) const {
   const Impl& m = *impl;
   const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : (chem_rtc && chem_rtc_ok) ? 4 : 2);
-  return lean_mech && lnm_ok && m.mech && P.sm == SM_NS && m.nranks == 1 && !m.p2p.on && chem_compact &&
+  return lean_mech && lnm_ok && m.mech && P.sm == SM_NS && chem_compact &&
          ((kind == 1 && chem_fast_ok) || (kind == 4 && chem_rtc_ok)) && !P.fpa.is_init && !P.ffc.is_init &&
          P.fpa.is_mu_t == lns_prev_mu_t && P.ny >= LNM_TILE;
 }
@@ -3232,7 +3318,7 @@ bool DeviceSolver::lns_step_ok(const StepParams& P) const {
   // (the fill F_m runs in step m here but in step m-1 in the split stepper:
   // the step parameters it reads must agree, i.e. is_mu_t must not change)
   return lean_ns && lns_ok && P.sm == SM_NS && sgl && sgl_ok && (sk_mode == SK_SGL || sk_mode == SK_SGT) &&
-         !m.mech && m.nranks == 1 && !m.p2p.on && !P.fpa.is_init && !P.ffc.is_init &&
+         !m.mech && !P.fpa.is_init && !P.ffc.is_init &&
          P.fpa.is_mu_t == lns_prev_mu_t && P.ny >= LEAN_TILE_MIN_TJ;
 }
 
@@ -3423,7 +3509,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   if (fx_step) {
     fx_pending = true;   // exchanged inside the tile kernel
   } else if ((m.comm || m.local || m.p2p.on) && m.nranks > 1) {
-    exchange(lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
+    exchange(lns_state ? CpuSolver::HALO_LNS : lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
   }
   if (!cs.cfg.isAdiabaticWall) {
     SoA s = m.view(h, sbuf, abuf, dsbuf, pbuf);

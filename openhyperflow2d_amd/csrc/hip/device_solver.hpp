@@ -114,6 +114,9 @@ class DeviceSolver : public SolverBase {
   long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
   void halo_fields(int group, std::vector<real*>& f, bool full = false) const;
+  // (o: column offset of each entry, 1 = the second column of a two-column halo)
+  void halo_fields(int group, std::vector<real*>& f, std::vector<unsigned char>& o, bool full) const;
+  bool ghost_stale = false;   // the ghost columns hold another stepper's representation (refresh before a split step)
   // p2p self-validation (collective over the strip ranks, before the first
   // step): poisons the ghost columns, runs one mailbox exchange of the full
   // state group with a rank-tagged dt, restores the device scalars and

@@ -202,6 +202,8 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
         assert all(s.graph_launches > 0 for s in solvers) or max(n for n, _ in schedule) < 12
     if stats is not None:
         stats["overlap_steps"] = [s.overlap_steps for s in solvers]
+        stats["lns_steps"] = [s.lns_steps for s in solvers]
+        stats["lnm_steps"] = [s.lnm_steps for s in solvers]
     out = {}
     for f in fields:
         full = None
@@ -282,6 +284,43 @@ def test_compact_state_halo_matches_single_gpu(gpu, deck, p2p):
             ref.solver.sgl = False
         ref.step(n, residual=res)
     assert summ["dt"] == ref.summary()["dt"]
+    for f in fields:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("deck,nranks,p2p", [("step", 3, False), ("resonator", 4, False), ("sst_plate", 3, False),
+                                            ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True)])
+def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
+    """Lean N-S / mechanism tiles on strips (two ghost columns: the tile
+    evaluates the fill of the first one, which reads the second; HALO_LNS
+    carries the next lean step's inputs of both, the second column only what
+    a neighbour's fill reads) == one GPU bit for bit, across residual steps,
+    downloads (materialize) and re-entry, over the in-process and the xGMI
+    mailbox transports."""
+    fields = list(FIELDS) + ["k", "mu", "mu_t"]
+    if deck == "step":
+        text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5)
+    elif deck == "resonator":
+        text = decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
+        fields += ["S7", "S8"]
+    elif deck == "sst_plate":
+        text = decks.set_key(decks.flat_plate(200, 60, turbulence=6, nmax=10 ** 6, nout=10 ** 5), "isAdiabaticWall", 1)
+        fields += ["S7", "S8"]
+    else:
+        text = decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5)
+        fields += ["S7", "S8", "Y:H2", "Y:O2", "Y:OH", "Y:H2O"]
+    schedule = [(4, True), (17, False), (5, True), (14, False)]
+    stats = {}
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=p2p, fuse=False, stats=stats,
+                               fields=fields)
+    lean_steps = stats["lnm_steps"] if deck == "scramjet" else stats["lns_steps"]
+    assert min(lean_steps) > 0, stats
+    ref = gpu.Simulation(text, "gpu")
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert (ref.solver.lnm_steps if deck == "scramjet" else ref.solver.lns_steps) > 0
+    assert summ["dt"] == ref.summary()["dt"]
+    assert summ["time"] == ref.summary()["time"]
     for f in fields:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 

@@ -10,10 +10,11 @@ from openhyperflow2d_amd.models import decks, validation
 pytestmark = pytest.mark.gpu
 
 
-def _run(gpu, model, nx, ny, dx, dy, p, flow_throughs):
+def _run(gpu, model, nx, ny, dx, dy, p, flow_throughs, cfl=None):
     text = decks.flat_plate(nx, ny, dx=dx, dy=dy, x_le=0.2, mach=2.5, p=p, turbulence=model,
-                            nmax=10 ** 9, nout=10 ** 8)
-    sim = gpu.Simulation(text, "gpu")
+                            nmax=10 ** 9, nout=10 ** 8, cfl=cfl)
+    # the plate is the domain edge (no solid cells): adiabatic, lean N-S kernels
+    sim = gpu.Simulation(decks.set_key(text, "isAdiabaticWall", 1), "gpu")
     t_end = flow_throughs * nx * dx / (2.5 * 341.0)
     while sim.summary()["time"] < t_end:
         sim.step(2000)
@@ -21,12 +22,13 @@ def _run(gpu, model, nx, ny, dx, dy, p, flow_throughs):
 
 
 def test_laminar_plate_follows_blasius(gpu):
-    """Cf ~ Re_x^-1/2 (Blasius) within 20 %; measured 0.85 +- 0.02 of the
-    correlation on this 30-cells-per-thickness grid (0.70 on half of it)."""
-    r = _run(gpu, 0, 250, 100, 1e-3, 1e-4, 1e3, 3.0)
+    """Cf ~ Re_x^-1/2 (Blasius): 0.90-0.92 of the correlation at CFL 0.4 on
+    this 30-cells-per-thickness grid (0.85 at the deck's CFL 0.1: the DEEPS
+    blend's diffusion scales with dy^2 / dt, profiles/flat_plate_validation.md)."""
+    r = _run(gpu, 0, 250, 100, 1e-3, 1e-4, 1e3, 3.0, cfl=0.4)
     sel = (r["Re_x"] > 1.5e4) & (r["Re_x"] < 1.0e5)
     ratio = r["Cf"][sel] / r["Cf_lam"][sel]
-    assert 0.8 < ratio.mean() < 1.05, ratio.mean()
+    assert 0.87 < ratio.mean() < 1.05, ratio.mean()
     assert ratio.std() < 0.05, ratio.std()
     slope = np.polyfit(np.log(r["Re_x"][sel]), np.log(r["Cf"][sel]), 1)[0]
     assert -0.56 < slope < -0.44, slope
@@ -38,19 +40,28 @@ def turbulent_runs(request):
 
     if not hf.gpu_available():
         pytest.fail("GPU test requires a HIP device")
-    return {m: _run(hf, m, 312, 750, 2e-3, 4e-5, 1e4, 2.0) for m in (6, 4)}
+    return {6: _run(hf, 6, 312, 750, 1e-3, 4e-5, 1e4, 5.0, cfl=0.4), 4: _run(hf, 4, 312, 750, 2e-3, 4e-5, 1e4, 2.0)}
 
 
-def test_sst_plate_transitions_above_laminar(turbulent_runs):
-    """k-omega SST builds a turbulent layer: Cf departs from the laminar law
-    and rises above it by Re_x > 1e6.  It stays below the fully turbulent
-    correlation (0.32 of it at Re_x = 2.5e6: eddy-viscosity ratio 18 -> 73
-    along the plate, still developing) -- the bounds pin today's behaviour."""
+def test_sst_plate_matches_the_turbulent_correlation(turbulent_runs):
+    """k-omega SST (Menter's wall omega at the first cell) on a developed
+    turbulent layer, Re_x 0.7-1.3e6, CFL 0.4: the wall stress the discrete
+    momentum balance carries -- the largest modelled stress (mu + mu_t) dU/dy
+    within y+ < 150, where a zero-pressure-gradient layer holds ~tau_w --
+    is 0.8-0.85 of Schlichting's turbulent law with Eckert's reference
+    temperature, the same on grids of dy = 40 and 20 um (0.83 / 0.84).  The
+    molecular mu_w dU/dy alone is lower (0.53 / 0.65 of the law, converging
+    as dy -> 0): across the viscous sublayer the DEEPS blend's own diffusion
+    (1 - beta) dyy/2 dy^2/dt, ~0.5 nu_w here, carries the rest
+    (profiles/flat_plate_validation.md).  The layer is turbulent: Cf is 2x
+    the laminar law."""
     r = turbulent_runs[6]
-    hi = r["Re_x"] > 1.4e6
-    assert (r["Cf"][hi] / r["Cf_lam"][hi]).min() > 1.3
-    ratio = r["Cf"][hi] / r["Cf_turb"][hi]
-    assert 0.2 < ratio.mean() < 1.2, ratio.mean()
+    hi = r["Re_x"] > 7e5
+    assert (r["Cf"][hi] / r["Cf_lam"][hi]).min() > 1.6
+    eff = r["Cf_eff"][hi] / r["Cf_turb"][hi]
+    assert 0.75 < eff.mean() < 1.15, eff.mean()
+    mol = r["Cf"][hi] / r["Cf_turb"][hi]
+    assert 0.4 < mol.mean() < eff.mean(), (mol.mean(), eff.mean())
 
 
 def test_keps_plate_keeps_the_reference_eddy_viscosity_cap(turbulent_runs):
