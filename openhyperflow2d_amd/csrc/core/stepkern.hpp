@@ -124,6 +124,10 @@ struct StepParams {
   const SpeciesProps* species;  // host or device pointer
   const ScenarioTables* scen = nullptr;   // device: evaluate beta_min / CFL_min per step
   int xcd = 0;       // device split kernels: XCD-aware workgroup order (speed only; host ignores it)
+  // device tile kernels: workgroup w waits (w / stagger_wgs) * stagger ticks
+  // of the 100 MHz clock before staging, so the dispatch rounds of a
+  // co-resident grid load their tiles one after another (speed only)
+  int stagger = 0, stagger_wgs = 256;
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

@@ -420,6 +420,19 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   extern __shared__ real lds[];
   unsigned long long tr[5];
   if (TR) tr[0] = rt_clock();
+  if (!FX && P.stagger > 0) {
+    // staggered start: every workgroup of a step is resident at once, so
+    // without it they all stage together (HBM saturated, VALUs idle) and
+    // then all compute (HBM idle); later dispatch rounds start loading while
+    // the earlier ones compute
+    // (rounds beyond the 4th are dispatched as earlier workgroups retire:
+    // no wait for them)
+    const unsigned r = blockIdx.x / (unsigned)P.stagger_wgs;
+    if (r > 0 && r < 4) {
+      const unsigned long long t0 = rt_clock(), d = (unsigned long long)r * (unsigned)P.stagger;
+      while (rt_clock() - t0 < d) __builtin_amdgcn_s_sleep(2);
+    }
+  }
   const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
@@ -684,29 +697,40 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   }
   // F_m runs with the dt of the step the split fill F_m belongs to (SST's
   // point-implicit destruction reads it); the predictor with this step's
-  P.dt = sc->dt_val[slot_reset(slot)];
+  // (both read here: a second read of the device scalars after the fills
+  // made the whole kernel 2x slower)
+  const real dt_now = P.dt;
+  if (MODE == SK_SGT && TURB == 3) P.dt = sc->dt_val[slot_reset(slot)];
   const int NC = T.NC;
   int i, j, c, i0, j0;
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
   int dummy = 0, skip = 0;
   // 1a. ring cells first (only their S, A, B are kept)
   const int nring = 2 * (T.TI + T.TJ);
-  if ((int)threadIdx.x < nring) {
-    int ii, jj;
-    lns_ring_cell(T, (int)threadIdx.x, &ii, &jj);
-    const int gi = i0 + ii, gj = j0 + jj;
+  // 1a'. a strip's first ghost column inside a partial last tile: its fill
+  // is a neighbour's (the ring covers it when the tile is full).  One call
+  // site for both (an inlined second copy of the fill costs registers).
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    int gi = -1, gj = 0, cc = 0;
+    if (pass == 0) {
+      if ((int)threadIdx.x < nring) {
+        int ii, jj;
+        lns_ring_cell(T, (int)threadIdx.x, &ii, &jj);
+        gi = i0 + ii;
+        gj = j0 + jj;
+        cc = (ii + 1) * T.W + jj + 1;
+      }
+    } else if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
+      gi = i;
+      gj = j;
+      cc = c;
+    }
     if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
       CellLocal rc;
       bool early, filled;
-      lns_fill_to_lds<MODE, TURB>(P, a, gi, gj, lds, NC, (ii + 1) * T.W + jj + 1, rc, &early, &filled, &dummy);
+      lns_fill_to_lds<MODE, TURB>(P, a, gi, gj, lds, NC, cc, rc, &early, &filled, &dummy);
     }
-  }
-  // 1a'. a strip's first ghost column inside a partial last tile: its fill
-  // is a neighbour's (the ring covers it when the tile is full)
-  if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
-    CellLocal gc;
-    bool ge, gfl;
-    lns_fill_to_lds<MODE, TURB>(P, a, i, j, lds, NC, c, gc, &ge, &gfl, &dummy);
   }
   // 1b. own cell: F_m, its level-m outputs, kept values for 2./3.
   LnsLevel<MODE> lv;
@@ -768,7 +792,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
       }
     }
   }
-  apply_dt(P, sc, slot);
+  P.dt = dt_now;   // this step's dt for the predictor
   __syncthreads();
   // 2. predict_m
   ResidualPack r;
@@ -893,7 +917,12 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   unsigned long long* tr = a.tr ? a.tr + (long)b * 12 : nullptr;
   const bool tr0 = tr && threadIdx.x == 0, trl = tr && threadIdx.x == BLOCK - WAVE;
   if (tr0) tr[0] = rt_clock();
-  // G_m runs with the dt of the step the split fill F_m belongs to
+  // G_m runs with the dt of the step the split fill F_m belongs to; this
+  // step's dt, scenario values and dt/dx, dt/dy are read up front as well (a
+  // second read of the device scalars after the fills doubled the lean N-S
+  // kernel's time)
+  apply_dt(P, sc, slot);
+  const real dt_now = P.dt;
   P.dt = sc->dt_val[slot_reset(slot)];
   const real dt_step = bits_to_d(sc->dt_bits[slot]);
   if (b == 0 && threadIdx.x == 0) {
@@ -912,24 +941,31 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   const int nring = 2 * (T.TI + T.TJ), own = T.TI * T.TJ;
   const int rbase = own + nring <= BLOCK ? own : 0;
   const int rt = (int)threadIdx.x - rbase;
-  if (rt >= 0 && rt < nring) {
-    int ri, rj;
-    lns_ring_cell(T, rt, &ri, &rj);
-    const int gi = i0 + ri, gj = j0 + rj;
+  // 1a'. a strip's first ghost column inside a partial last tile (see lns).
+  // Both fills go through one call site: a second inlined copy of the fill
+  // pushed the SST kernel from 56 to 784 B/lane of scratch (2x slower).
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    int gi = -1, gj = 0, ri = 0, rj = 0;
+    if (pass == 0) {
+      if (rt >= 0 && rt < nring) {
+        lns_ring_cell(T, rt, &ri, &rj);
+        gi = i0 + ri;
+        gj = j0 + rj;
+      }
+    } else if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
+      gi = i;
+      gj = j;
+      ri = ii;
+      rj = jj;
+    }
     if (gi >= 0 && gi < P.nx && gj >= 0 && gj < P.ny) {
       CellLocal rc;
       real mY[LNM_NSB];
       bool early, filled;
       lnm_fill<TURB>(P, a, L, lds, gi, gj, ri, rj, rc, mY, &early, &filled);
     }
-  }
-  if (tr0) tr[1] = rt_clock();
-  // 1a'. a strip's first ghost column inside a partial last tile (see lns)
-  if (!mine && (int)threadIdx.x < T.TIh * T.TJ && i == P.i1 && i < P.nx && j < P.ny) {
-    CellLocal gc;
-    real mY[LNM_NSB];
-    bool ge, gfl;
-    lnm_fill<TURB>(P, a, L, lds, i, j, ii, jj, gc, mY, &ge, &gfl);
+    if (pass == 0 && tr0) tr[1] = rt_clock();
   }
   // 1b. own cell: G_m, its level-m outputs, kept values for 2. and 3.
   LnmLevel lv;
@@ -1005,7 +1041,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
       bts[s] = a.betas[o + idx];
     }
   }
-  apply_dt(P, sc, slot);   // this step's dt for the predictor and E_{m+1}
+  P.dt = dt_now;   // this step's dt for the predictor and E_{m+1}
   __syncthreads();
   if (tr0) tr[3] = rt_clock();
   // 2. predict_m, flow and turbulence equations
@@ -1813,6 +1849,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_CHEM_KERNEL")) chem_kernel = std::atoi(e);   // 1 compiled 2 MFMA 3 generic 4 hiprtc
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
+  if (const char* e = std::getenv("HF2D_STAGGER")) tile_stagger = std::atoi(e);
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
@@ -3361,6 +3398,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (lean_wgcu > 0)   // cap the resident workgroups per CU through the LDS request (160 KB per CU)
       shmem = std::max(shmem, (size_t)((LDS_PER_CU / lean_wgcu - 1024) & ~255));
     const bool out = step_outputs || want_res;
+    P.stagger = tile_stagger;
+    P.stagger_wgs = cu_count > 0 ? cu_count : 256;
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
