@@ -206,6 +206,51 @@ static_assert(offsetof(CellRecord, droYdx) == 1120, "layout");
 static_assert(offsetof(CellRecord, dUdx) == 1184, "layout");
 static_assert(offsetof(CellRecord, BGX) == 1232, "layout");
 
+// ---------------------------------------------------------------------------
+// Correctly rounded FP64 division and square root for operands of ordinary
+// magnitude.  The compiler's IEEE expansion on gfx950 wraps the Newton-
+// Raphson / Markstein sequence in v_div_scale (operand scaling near the
+// exponent limits) and v_div_fixup (inf / nan / zero cases), 11 VALU
+// instructions per division; for operands whose exponents are far from the
+// limits the scaling is the identity and the fixup returns the quotient
+// unchanged, so the bare sequence (8 instructions) yields the same correctly
+// rounded result, bit for bit -- the host computes a / b.  Callers use these
+// only where the divisor is a nonzero physical quantity (density, pressure,
+// temperature, sound speed + |u|, 1 + |residual| ...).  hf_sqrt keeps the
+// zero / +inf case (a steady cell has a zero residual) and drops the tiny-
+// argument scaling (inputs >= 2^-767 or exactly 0).
+// ---------------------------------------------------------------------------
+HF_HD inline double hf_div(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(b);
+  double t = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, t, r);
+  t = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, t, r);
+  const double q = a * r;
+  const double e = __builtin_fma(-b, q, a);
+  return __builtin_fma(e, r, q);
+#else
+  return a / b;
+#endif
+}
+HF_HD inline double hf_sqrt(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  g = __builtin_fma(d, h, g);
+  return (x == 0.0 || x == __builtin_inf()) ? x : g;
+#else
+  return __builtin_sqrt(x);
+#endif
+}
+
 // Piecewise-linear property table with the reference's rule: linear
 // interpolation inside, linear *extrapolation* from the end segment outside
 // (obj_data/obj_data.cpp:1822-1859).  Plain-old-data so it can live in device
@@ -230,7 +275,7 @@ HF_HD inline real table_eval(const TableData& t, real xv) {
     for (i = 1; i < n; i++)
       if (xv >= t.x[i - 1] && xv < t.x[i]) break;
   }
-  return t.y[i] + (t.y[i - 1] - t.y[i]) * (xv - t.x[i]) / (t.x[i - 1] - t.x[i]);
+  return t.y[i] + hf_div((t.y[i - 1] - t.y[i]) * (xv - t.x[i]), t.x[i - 1] - t.x[i]);
 }
 
 // Species property pack: R, formation enthalpy and Cp/lam/mu(T) tables for

@@ -316,19 +316,19 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
     io.out_UVP(u_old, v_old, io.P0());
     return 1.0;
   }
-  const real kk = c.CP / (c.CP - c.R);
+  const real kk = hf_div(c.CP, c.CP - c.R);
   real U, V;
   if (has_all(CT, CT_U_CONST)) {
     U = u_old;
     s[I_RHOU] = U * s[I_RHO];
   } else {
-    U = s[I_RHOU] / s[I_RHO];
+    U = hf_div(s[I_RHOU], s[I_RHO]);
   }
   if (has_all(CT, CT_V_CONST)) {
     V = v_old;
     s[I_RHOV] = V * s[I_RHO];
   } else {
-    V = s[I_RHOV] / s[I_RHO];
+    V = hf_div(s[I_RHOV], s[I_RHO]);
   }
   real Tmp1 = s[I_RHO], Tmp3 = 0.;
   for (int q = 0; q < NCOMP; q++) {
@@ -364,7 +364,7 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
     s[I_RHOV] = V * s[I_RHO];
   }
   const real p = (kk - 1.) * (s[I_RHOE] - s[I_RHO] * (U * U + V * V) * 0.5 - Tmp3);
-  const real Tg = p / c.R / s[I_RHO];
+  const real Tg = hf_div(hf_div(p, c.R), s[I_RHO]);
   // fluxes of this fill are built from the pre-chemistry species
   if (!SG)
     for (int k = 0; k < NCOMP; k++) io.out_Ps(k, s[4 + k]);
@@ -373,8 +373,8 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
     if (Tg < 0.) {
       if (neg_T) *neg_T = 1;
     } else {
-      const real AAA = std::sqrt(kk * c.R * Tg);
-      dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(U)), P.dy / (AAA + std::fabs(V)));
+      const real AAA = hf_sqrt(kk * c.R * Tg);
+      dt_local = P.CFL_min * hf_min(hf_div(P.dx, AAA + std::fabs(U)), hf_div(P.dy, AAA + std::fabs(V)));
       if (P.chem_model != NO_REACTIONS) {
         c.Tg = Tg;
         c.Tf = L.Tf[idx];

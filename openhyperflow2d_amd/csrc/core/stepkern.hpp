@@ -200,12 +200,12 @@ HF_HD inline bool is_active(u64 CT) {
 HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, real sqrt_res) {
   const real b2 = beta_min * beta_min;
   switch (bff) {
-    case BFF_L: return hf_min(beta_min, b2 / (beta_min + DD));
-    case BFF_LR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + DD));
-    case BFF_S: return hf_min(beta_min, b2 / (beta_min + DD * DD));
-    case BFF_SR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + DD * DD));
-    case BFF_SQR: return hf_min(beta_min, b2 / (beta_min + sqrt_res));
-    case BFF_SQRR: return hf_min((beta_min + beta_old) * 0.5, b2 / (beta_min + sqrt_res));
+    case BFF_L: return hf_min(beta_min, hf_div(b2, beta_min + DD));
+    case BFF_LR: return hf_min((beta_min + beta_old) * 0.5, hf_div(b2, beta_min + DD));
+    case BFF_S: return hf_min(beta_min, hf_div(b2, beta_min + DD * DD));
+    case BFF_SR: return hf_min((beta_min + beta_old) * 0.5, hf_div(b2, beta_min + DD * DD));
+    case BFF_SQR: return hf_min(beta_min, hf_div(b2, beta_min + sqrt_res));
+    case BFF_SQRR: return hf_min((beta_min + beta_old) * 0.5, hf_div(b2, beta_min + sqrt_res));
     default: return beta_old;   // declared but unimplemented variants (Q22)
   }
 }
@@ -314,9 +314,9 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
       const real absDD = snew - s;
       real DD, sqrt_res = 0;
       if (std::fabs(s) > 1.e-15) {
-        DD = std::fabs(absDD / s);
+        DD = std::fabs(hf_div(absDD, s));
         // only the square-root blending variants read it (uniform branch)
-        if (P.bff == BFF_SQR || P.bff == BFF_SQRR) sqrt_res = std::sqrt(DD);
+        if (P.bff == BFF_SQR || P.bff == BFF_SQRR) sqrt_res = hf_sqrt(DD);
       } else {
         DD = 1.0;
       }

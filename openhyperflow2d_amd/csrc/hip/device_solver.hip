@@ -3398,8 +3398,11 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (lean_wgcu > 0)   // cap the resident workgroups per CU through the LDS request (160 KB per CU)
       shmem = std::max(shmem, (size_t)((LDS_PER_CU / lean_wgcu - 1024) & ~255));
     const bool out = step_outputs || want_res;
-    P.stagger = tile_stagger;
+    // staggered start only for a grid that is resident at once (<= 4 dispatch
+    // rounds: measured 1.5 us faster on the headline grid; the 4000x1000 triple
+    // point, dispatched in ~15 waves, ran 350 -> 550 us with it)
     P.stagger_wgs = cu_count > 0 ? cu_count : 256;
+    P.stagger = ntile <= 4u * (unsigned)P.stagger_wgs ? tile_stagger : 0;
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
