@@ -214,9 +214,10 @@ static_assert(offsetof(CellRecord, BGX) == 1232, "layout");
 // instructions per division; for operands whose exponents are far from the
 // limits the scaling is the identity and the fixup returns the quotient
 // unchanged, so the bare sequence (8 instructions) yields the same correctly
-// rounded result, bit for bit -- the host computes a / b.  Callers use these
-// only where the divisor is a nonzero physical quantity (density, pressure,
-// temperature, sound speed + |u|, 1 + |residual| ...).  hf_sqrt keeps the
+// rounded result, bit for bit -- the host computes a / b.  v_div_fixup is
+// kept (9 instructions), so zero, infinite and NaN operands still give the
+// IEEE result; only operands within ~2^100 of the exponent limits, where the
+// scaling would engage, can differ.  hf_sqrt keeps the
 // zero / +inf case (a steady cell has a zero residual) and drops the tiny-
 // argument scaling (inputs >= 2^-767 or exactly 0).
 // ---------------------------------------------------------------------------
@@ -229,7 +230,8 @@ HF_HD inline double hf_div(double a, double b) {
   r = __builtin_fma(r, t, r);
   const double q = a * r;
   const double e = __builtin_fma(-b, q, a);
-  return __builtin_fma(e, r, q);
+  // v_div_fixup: zero / inf / nan operands give the IEEE result
+  return __builtin_amdgcn_div_fixup(__builtin_fma(e, r, q), b, a);
 #else
   return a / b;
 #endif

@@ -61,7 +61,7 @@ HF_HD inline void turb_axisym_addon(N& n, const FillParams& P, int is_init) {
   const real FT = (real)P.FT;
   if (has_all(n.TurbType, TCT_k_eps_Model) && !is_init) {
     n.F[I_K] = FT * (n.mu + n.mu_t) * n.dkdy;
-    n.F[I_EPS] = FT * (n.mu + n.mu_t / 1.3) * n.depsdy;
+    n.F[I_EPS] = FT * (n.mu + hf_div(n.mu_t, 1.3)) * n.depsdy;
   } else if (has_all(n.TurbType, TCT_Spalart_Allmaras_Model) && !is_init) {
     n.F[I_NUT] = FT * (n.mu / n.S[I_RHO] + n.S[I_NUT]) * n.dkdy;
   } else if (is_init) {
@@ -110,31 +110,31 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
     const real TmpI = P.turb_I * std::sqrt(n.U * n.U + n.V * n.V + 1.e-30);
     n.S[I_K] = 1.5 * TmpI * TmpI * rho;
   }
-  const real kk = hf_max(n.S[I_K] / rho, 0.0);
-  const real nu = n.mu / rho;
+  const real kk = hf_max(hf_div(n.S[I_K], rho), 0.0);
+  const real nu = hf_div(n.mu, rho);
   // omega floor: eddy-viscosity ratio nu_t / nu <= 1e5 (keeps the explicit
   // cross-diffusion and production terms bounded where k ~ 0, e.g. fluid at
   // rest next to an impulsively started free stream)
-  const real om_floor = hf_max(kk / (1.0e5 * nu + 1e-300), 1e-6);
-  const real om = hf_max(n.S[I_OMEGA] / rho, om_floor);
+  const real om_floor = hf_max(hf_div(kk, 1.0e5 * nu + 1e-300), 1e-6);
+  const real om = hf_max(hf_div(n.S[I_OMEGA], rho), om_floor);
   if (has_all(n.TurbType, TCT_eps_CONST)) {
     const real l = hf_max(n.l_min, hf_min(P.dx, P.dy)) * 0.41;
     n.S[I_OMEGA] = rho * hf_max(omega_inflow(kk, l), om_floor);
   }
   // dkdx.. hold d(k)/dx and d(omega)/dx (already divided by rho, like the k-eps path)
   const real cross = n.dkdx * n.depsdx + n.dkdy * n.depsdy;
-  const real CDkw = hf_max(2.0 * rho * so2 / om * cross, 1e-10);
-  const real arg1a = std::sqrt(kk) / (bstar * om * dmin);
-  const real arg1b = 500.0 * nu / (dmin * dmin * om);
-  const real arg1 = hf_min(hf_max(arg1a, arg1b), 4.0 * rho * so2 * kk / (CDkw * dmin * dmin));
+  const real CDkw = hf_max(hf_div(2.0 * rho * so2, om) * cross, 1e-10);
+  const real arg1a = hf_div(hf_sqrt(kk), bstar * om * dmin);
+  const real arg1b = hf_div(500.0 * nu, dmin * dmin * om);
+  const real arg1 = hf_min(hf_max(arg1a, arg1b), hf_div(4.0 * rho * so2 * kk, CDkw * dmin * dmin));
   const real F1 = std::tanh(arg1 * arg1 * arg1 * arg1);
   const real arg2 = hf_max(2.0 * arg1a, arg1b);
   const real F2 = std::tanh(arg2 * arg2);
   const real Sxy = 0.5 * (n.dUdy + n.dVdx);
   real Smag2 = 2.0 * (n.dUdx * n.dUdx + n.dVdy * n.dVdy) + 4.0 * Sxy * Sxy;
-  if (P.FT) Smag2 += 2.0 * (n.V / n.y) * (n.V / n.y);
-  const real Smag = std::sqrt(Smag2);
-  const real mut = rho * a1 * kk / hf_max(a1 * om, Smag * F2);
+  if (P.FT) Smag2 += 2.0 * hf_div(n.V, n.y) * hf_div(n.V, n.y);
+  const real Smag = hf_sqrt(Smag2);
+  const real mut = hf_div(rho * a1 * kk, hf_max(a1 * om, Smag * F2));
   const real sk = F1 * sk1 + (1.0 - F1) * sk2;
   const real so = F1 * so1 + (1.0 - F1) * so2;
   const real beta = F1 * b1 + (1.0 - F1) * b2;
@@ -166,16 +166,16 @@ HF_HD inline void turb_sst(N& n, const FillParams& P, int is_mu_t, int is_init) 
   // which can never drive k or omega negative however large omega gets next to
   // a no-slip wall (omega_w = 60 nu / (beta1 d^2)) on fine grids.
   const real rk = bstar * om, rw = beta * om;
-  const real ik = P.dt > 0 ? 1.0 / (1.0 + P.dt * rk) : 1.0;
-  const real iw = P.dt > 0 ? 1.0 / (1.0 + P.dt * rw) : 1.0;
+  const real ik = P.dt > 0 ? hf_div(1.0, 1.0 + P.dt * rk) : 1.0;
+  const real iw = P.dt > 0 ? hf_div(1.0, 1.0 + P.dt * rw) : 1.0;
   if (!has_all(n.TurbType, TCT_k_CONST)) n.Src[I_K] = Pk - rho * kk * rk * ik;
   if (!has_all(n.TurbType, TCT_eps_CONST)) {
     // production gamma * rho * S^2 (the Pk limiter applied through nu_t) and
     // the cross-diffusion term, each bounded by the destruction scale
     // beta* rho omega^2 * 10 for the explicit DEEPS update
     const real cap = 10.0 * bstar * rho * om * om;
-    const real Pw = hf_min(gam * rho / hf_max(mut, 1e-30) * Pk, cap);
-    const real CD = hf_max(hf_min(2.0 * (1.0 - F1) * rho * so2 / om * cross, cap), -cap);
+    const real Pw = hf_min(hf_div(gam * rho, hf_max(mut, 1e-30)) * Pk, cap);
+    const real CD = hf_max(hf_min(hf_div(2.0 * (1.0 - F1) * rho * so2, om) * cross, cap), -cap);
     n.Src[I_OMEGA] = Pw - rho * om * rw * iw + CD;
   }
   const real FT = (real)P.FT;
@@ -264,11 +264,11 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
     const real Tmp1 = n.dUdy + n.dVdx;
     const real Tmp2 = n.S[I_RHO] * l;
     real Tmp3 = n.dUdx * n.dUdx + n.dVdy * n.dVdy;
-    if (P.FT) Tmp3 += n.U / n.y;
+    if (P.FT) Tmp3 += hf_div(n.U, n.y);
     if (n.mu_t == 0) n.mu_t = n.S[I_RHO] * l * l * hf_max(std::fabs(n.dUdy), std::fabs(n.dVdx));
     G = n.mu_t * (Tmp1 * Tmp1 + 2 * Tmp3);
     if (n.S[I_EPS] != 0.0 && n.mu != 0.0)
-      Rt = n.S[I_K] * n.S[I_K] / n.S[I_EPS] / n.mu;
+      Rt = hf_div(hf_div(n.S[I_K] * n.S[I_K], n.S[I_EPS]), n.mu);
     else
       Rt = 0;
     if (P.tem == TEM_k_eps_Chien) {
@@ -309,7 +309,7 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
     if (has_all(TT, TCT_eps_Cmk2kXn_WALL))
       n.S[I_EPS] = std::pow(C_mu, 3. / 4.) * std::pow(n.S[I_K] / n.S[I_RHO], 3. / 2.) / l;
     if (is_mu_t && n.S[I_EPS] != 0) {
-      const real nu_t = std::fabs(C_mu * f_mu * n.S[I_K] * n.S[I_K] / n.S[I_EPS]);
+      const real nu_t = std::fabs(hf_div(C_mu * f_mu * n.S[I_K] * n.S[I_K], n.S[I_EPS]));
       n.mu_t = hf_min(nu_t, n.mu_t);
     }
     if (!is_init) {
@@ -317,10 +317,10 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
       n.A[I_EPS] = n.S[I_EPS] * n.U;
       n.B[I_K] = n.S[I_K] * n.V;
       n.B[I_EPS] = n.S[I_EPS] * n.V;
-      n.RX[I_K] = (n.mu + n.mu_t / sig_k) * (n.dkdx);
-      n.RX[I_EPS] = (n.mu + n.mu_t / sig_eps) * (n.depsdx);
-      n.RY[I_K] = (n.mu + n.mu_t / sig_k) * (n.dkdy);
-      n.RY[I_EPS] = (n.mu + n.mu_t / sig_eps) * (n.depsdy);
+      n.RX[I_K] = (n.mu + hf_div(n.mu_t, sig_k)) * (n.dkdx);
+      n.RX[I_EPS] = (n.mu + hf_div(n.mu_t, sig_eps)) * (n.depsdx);
+      n.RY[I_K] = (n.mu + hf_div(n.mu_t, sig_k)) * (n.dkdy);
+      n.RY[I_EPS] = (n.mu + hf_div(n.mu_t, sig_eps)) * (n.depsdy);
       n.A[I_K] = n.A[I_K] - n.RX[I_K];
       n.A[I_EPS] = n.A[I_EPS] - n.RX[I_EPS];
       n.B[I_K] = n.B[I_K] - n.RY[I_K];
@@ -330,8 +330,8 @@ HF_HD inline void turb_model(N& n, const FillParams& P, int is_mu_t, int is_init
         if (!has_all(TT, TCT_k_CONST))
           n.Src[I_K] = (G - n.S[I_EPS] * (1 + Mt) + L_k * n.S[I_RHO]);
         if (!has_all(TT, TCT_eps_CONST) && n.S[I_K] != 0)
-          n.Src[I_EPS] = (C1eps * f1 * n.S[I_EPS] / n.S[I_K] * G -
-                          C2eps * f2 * n.S[I_EPS] * n.S[I_EPS] / n.S[I_K] + L_eps * n.S[I_RHO]);
+          n.Src[I_EPS] = (hf_div(C1eps * f1 * n.S[I_EPS], n.S[I_K]) * G -
+                          hf_div(C2eps * f2 * n.S[I_EPS] * n.S[I_EPS], n.S[I_K]) + L_eps * n.S[I_RHO]);
       }
       turb_axisym_addon(n, P, is_init);
     }
@@ -389,7 +389,7 @@ HF_HD inline bool fill_node_pre(N& n) {
   // which puts the whole node struct in scratch memory on the GPU
   const bool uc = has_all(n.CT, CT_U_CONST), vc = has_all(n.CT, CT_V_CONST);
   const real r = n.S[I_RHO], su = n.S[I_RHOU], sv = n.S[I_RHOV];
-  const real u = uc ? n.U : su / r, v = vc ? n.V : sv / r;
+  const real u = uc ? n.U : hf_div(su, r), v = vc ? n.V : hf_div(sv, r);
   n.S[I_RHOU] = uc ? u * r : su;
   n.S[I_RHOV] = vc ? v * r : sv;
   n.U = u;
@@ -435,7 +435,7 @@ template <class N, class MX = RefMix, int TURB = 1>   // TURB: 0 none, 1 every m
 HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
   if (!fill_node_pre(n)) return false;
   real Tmp1, Tmp2 = 0, Tmp3 = 0., _mu = 0, _lam = 0, L = 0;
-  if (!MX::MECH) n.k = n.CP / (n.CP - n.R);   // (k is not read by fill_node_pre's velocity part)
+  if (!MX::MECH) n.k = hf_div(n.CP, n.CP - n.R);   // (k is not read by fill_node_pre's velocity part)
 
   if (P.sm == SM_NS) {
     if (P.is_init && n.TurbType > 0) {
@@ -467,7 +467,7 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
     mx.state(n);   // T by Newton on the thermally perfect e(T); R, Cp, k, p at T
   } else {
     n.p = (n.k - 1.) * (n.S[I_RHOE] - n.S[I_RHO] * (n.U * n.U + n.V * n.V) * 0.5 - Tmp3);
-    n.Tg = n.p / n.R / n.S[I_RHO];
+    n.Tg = hf_div(hf_div(n.p, n.R), n.S[I_RHO]);
   }
 
   if (P.sm == SM_NS) {
@@ -484,10 +484,10 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
       _mu = n.mu;
       _lam = n.lam;
     }
-    n.Diff = _lam / n.CP;
+    n.Diff = hf_div(_lam, n.CP);
     L = (2. / 3.) * _mu;
     if (P.FT == FT_AXISYMMETRIC)
-      Tmp2 = L * (n.dUdx + n.dVdy + (real)P.FT * n.V / n.y);
+      Tmp2 = L * (n.dUdx + n.dVdy + hf_div((real)P.FT * n.V, n.y));
     else
       Tmp2 = L * (n.dUdx + n.dVdy);
   }
@@ -547,7 +547,7 @@ HF_HD inline bool fill_node(N& n, const FillParams& P, const MX& mx = MX{}) {
       n.B[i] = n.B[i] - n.RY[i];
     }
     if (P.FT == FT_AXISYMMETRIC) {
-      const real t00 = 2 * _mu * n.V / n.y - Tmp2;
+      const real t00 = hf_div(2 * _mu * n.V, n.y) - Tmp2;
       n.F[I_RHOU] -= n.RY[I_RHOU];
       n.F[I_RHOV] -= n.RY[I_RHOV] + t00;
       n.F[I_RHOE] -= n.RY[I_RHOE];

@@ -521,14 +521,14 @@ struct MechMix {
   template <class N>
   HF_HD void state(N& n) const {
     const real rho = n.S[I_RHO];
-    const real e = (n.S[I_RHOE] - rho * (n.U * n.U + n.V * n.V) * 0.5) / rho;
+    const real e = hf_div(n.S[I_RHOE] - rho * (n.U * n.U + n.V * n.V) * 0.5, rho);
     const real T = mech_T_from_e<NSB>(*m, Y, e, n.Tg);
     real ee, cv, R, cp;
     mech_mix_thermo<NSB>(*m, Y, T, &ee, &cv, &R, &cp);
     n.Tg = T;
     n.R = R;
     n.CP = cp;
-    n.k = cp / cv;
+    n.k = hf_div(cp, cv);
     n.p = rho * R * T;
   }
   template <class N>
@@ -756,7 +756,7 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
 #pragma unroll
     for (int s = 0; s < (MECH ? NSB : 1); s++) {
       const real ys = io.Ys(s < nsp ? s : nsp - 1);
-      mY[s] = (s < nsp && rho != 0) ? ys / rho : 0.0;
+      mY[s] = (s < nsp && rho != 0) ? hf_div(ys, rho) : 0.0;
       mgx[s] = mgy[s] = 0.0;
     }
   }
@@ -787,8 +787,8 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     const int n1 = (nbm & NB_XL) ? 1 : 0, n2 = (nbm & NB_XR) ? 1 : 0;
     const int n3 = (nbm & NB_YU) ? 1 : 0, n4 = (nbm & NB_YD) ? 1 : 0;
     io.set_nb(i, j, P.ny, n1, n2, n3, n4);
-    const real dx_1_n = (1.0 / P.dx) / (real)(n1 + n2 > 1 ? n1 + n2 : 1);
-    const real dy_1_m = (1.0 / P.dy) / (real)(n3 + n4 > 1 ? n3 + n4 : 1);
+    const real dx_1_n = hf_div(hf_div(1.0, P.dx), (real)(n1 + n2 > 1 ? n1 + n2 : 1));
+    const real dy_1_m = hf_div(hf_div(1.0, P.dy), (real)(n3 + n4 > 1 ? n3 + n4 : 1));
     lz_dx = dx_1_n;
     lz_dy = dy_1_m;
     real aR = io.Sn(0, ND_R), aL = io.Sn(0, ND_L), aU = io.Sn(0, ND_U), aD = io.Sn(0, ND_D);
@@ -844,13 +844,13 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
       c.dUdy = (io.Uon(ND_U) - io.Uon(ND_D)) * dy_1_m;
       c.dVdy = (io.Von(ND_U) - io.Von(ND_D)) * dy_1_m;
       if (is_two_eq(c.TurbType)) {
-        c.dkdx = (io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n / rho;
-        c.depsdx = (io.Sn(I_EPS, ND_R) - io.Sn(I_EPS, ND_L)) * dx_1_n / rho;
-        c.dkdy = (io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m / rho;
-        c.depsdy = (io.Sn(I_EPS, ND_U) - io.Sn(I_EPS, ND_D)) * dy_1_m / rho;
+        c.dkdx = hf_div((io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n, rho);
+        c.depsdx = hf_div((io.Sn(I_EPS, ND_R) - io.Sn(I_EPS, ND_L)) * dx_1_n, rho);
+        c.dkdy = hf_div((io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m, rho);
+        c.depsdy = hf_div((io.Sn(I_EPS, ND_U) - io.Sn(I_EPS, ND_D)) * dy_1_m, rho);
       } else if (has_all(c.TurbType, TCT_Spalart_Allmaras_Model)) {
-        c.dkdx = (io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n / rho;
-        c.dkdy = (io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m / rho;
+        c.dkdx = hf_div((io.Sn(I_K, ND_R) - io.Sn(I_K, ND_L)) * dx_1_n, rho);
+        c.dkdy = hf_div((io.Sn(I_K, ND_U) - io.Sn(I_K, ND_D)) * dy_1_m, rho);
       }
     }
     c.dTdx = (io.Ton(ND_R) - io.Ton(ND_L)) * dx_1_n;
@@ -892,8 +892,8 @@ HF_HD inline real fill_compute(const StepParams& P, IO& io, CellLocal& c, real* 
     if (c.Tg < 0. || (MECH && !(c.Tg > MECH_TMIN))) {
       if (neg_T) *neg_T = 1;
     } else {
-      const real AAA = std::sqrt(c.k * c.R * c.Tg);
-      dt_local = P.CFL_min * hf_min(P.dx / (AAA + std::fabs(c.U)), P.dy / (AAA + std::fabs(c.V)));
+      const real AAA = hf_sqrt(c.k * c.R * c.Tg);
+      dt_local = P.CFL_min * hf_min(hf_div(P.dx, AAA + std::fabs(c.U)), hf_div(P.dy, AAA + std::fabs(c.V)));
       if (P.visc_cfl > 0 && P.sm == SM_NS) {
         const real nu_eff = (c.mu + c.mu_t) / c.S[I_RHO];
         if (nu_eff > 0) dt_local = hf_min(dt_local, P.visc_cfl / (nu_eff * (1.0 / (P.dx * P.dx) + 1.0 / (P.dy * P.dy))));

@@ -400,6 +400,9 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
 // its own wave finished computing, after the block dt reduction barrier and
 // after the dt atomic, plus the HW_ID / XCC_ID registers (DeviceSolver::trace_tile).
 constexpr int TILE_TRACE_WORDS = 8;
+#ifndef HF2D_TILE_STAGGER
+#define HF2D_TILE_STAGGER 1
+#endif
 constexpr int LDS_PER_CU = 160 * 1024;
 __device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -420,7 +423,10 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   extern __shared__ real lds[];
   unsigned long long tr[5];
   if (TR) tr[0] = rt_clock();
-  if (!FX && P.stagger > 0) {
+  // (compiled into the single-gas two-cell kernel only: the mere presence of
+  // this block made the multi-gas one-cell kernel 3x slower on the triple
+  // point, 340 -> 1030 us, even with stagger 0)
+  if (HF2D_TILE_STAGGER && SG && CPT == 2 && !FX && P.stagger > 0) {
     // staggered start: every workgroup of a step is resident at once, so
     // without it they all stage together (HBM saturated, VALUs idle) and
     // then all compute (HBM idle); later dispatch rounds start loading while
