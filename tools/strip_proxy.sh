@@ -9,4 +9,5 @@ run() {  # tag args...
    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/proxyprof_$tag" -o run \
      -- python3 "$R/tools/strip_proxy.py" "$@" > "$R/gpurun_out/proxyprof_$tag.log" 2>&1)
 }
+export GPU_MAX_HW_QUEUES=16
 run reso4 --config resonator --ranks 4 --steps 60 && run scram8 --config scramjet --ranks 8 --steps 12 --warmup 12
