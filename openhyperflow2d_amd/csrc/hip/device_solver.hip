@@ -1355,19 +1355,34 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
   const unsigned long long seq = *a.seq + 1;
   const int par = (int)(seq & 1);
   const int ny = a.ny;
-  // 1. push boundary columns and this rank's dt into the peers' mailboxes
-  if (a.sides & 1) {
-    real* dst = a.peer_recv_l + ((long)par * 2 + 1) * a.cap;   // left neighbour receives "from right"
-    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
-      const int f = t / ny, j = t - f * ny;
-      p2p_store(dst + t, a.L.f[f][(long)(a.first + a.L.o[f]) * ny + j]);
+  // 1. push boundary columns and this rank's dt into the peers' mailboxes:
+  // PER loads of a thread in flight, then its PER system-coherent stores (one
+  // load latency per batch instead of one per value: the N-S halo is 23-43
+  // fields x ny per side)
+  constexpr int PER = 16;
+  const int total = ((a.sides & 1) ? a.cnt : 0) + ((a.sides & 2) ? a.cnt : 0);
+  for (int base = 0; base < total; base += PER * P2P_THREADS) {
+    real v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int t = base + u * P2P_THREADS + threadIdx.x;
+      if (t < total) {
+        const bool right = !(a.sides & 1) || t >= a.cnt;
+        const int tt = (a.sides & 1) && right ? t - a.cnt : t;
+        const int f = tt / ny, j = tt - f * ny;
+        v[u] = a.L.f[f][(long)(right ? a.last - a.L.o[f] : a.first + a.L.o[f]) * ny + j];
+      }
     }
-  }
-  if (a.sides & 2) {
-    real* dst = a.peer_recv_r + ((long)par * 2) * a.cap;       // right neighbour receives "from left"
-    for (int t = threadIdx.x; t < a.cnt; t += P2P_THREADS) {
-      const int f = t / ny, j = t - f * ny;
-      p2p_store(dst + t, a.L.f[f][(long)(a.last - a.L.o[f]) * ny + j]);
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int t = base + u * P2P_THREADS + threadIdx.x;
+      if (t < total) {
+        const bool right = !(a.sides & 1) || t >= a.cnt;
+        const int tt = (a.sides & 1) && right ? t - a.cnt : t;
+        // the left neighbour receives "from right", the right one "from left"
+        real* dst = right ? a.peer_recv_r + ((long)par * 2) * a.cap : a.peer_recv_l + ((long)par * 2 + 1) * a.cap;
+        p2p_store(dst + tt, v[u]);
+      }
     }
   }
   const double mydt = bits_to_d(a.sc->dt_bits[a.dslot]);
@@ -1403,8 +1418,6 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
   // 4. unpack this rank's mailbox into the ghost columns: all loads of a
   // thread first, then its stores (the stores may alias nothing the loads
   // read, but the compiler cannot know that)
-  constexpr int PER = 8;   // (2 sides * 48 fields * ny) / P2P_THREADS slots for ny <= 42; loop otherwise
-  const int total = ((a.sides & 1) ? a.cnt : 0) + ((a.sides & 2) ? a.cnt : 0);
   for (int base = 0; base < total; base += PER * P2P_THREADS) {
     real v[PER];
 #pragma unroll
