@@ -3696,7 +3696,12 @@ std::vector<unsigned long long> DeviceSolver::trace_tile(int steps) {
 }
 
 std::string DeviceSolver::autotune(int steps) {
-  if (!lean_ok || cs.cfg.ProblemType == SM_NS || !lean_tile || nstep != 0 || iter != 0) return "";
+  // inviscid lean tile: cells per thread x tile height; lean N-S tile (one
+  // cell per thread): tile height (resonator 2000x200: 92 us at the
+  // heuristic height, 87 us at 16 rows)
+  const bool ns = cs.cfg.ProblemType == SM_NS;
+  if (nstep != 0 || iter != 0) return "";
+  if (ns ? !(lean_ns && lns_ok) : !(lean_ok && lean_tile)) return "";
   flush_pending();
   const real s_dt = dt, s_dtr = dt_running, s_cur = cur_time_part, s_gt = cs.global_time;
   const long s_iter = iter, s_last = last_iter;
@@ -3708,9 +3713,11 @@ std::string DeviceSolver::autotune(int steps) {
     int cpt, tj;
   };
   std::vector<Cand> cands;
-  for (int cpt : {2, 1})
+  for (int cpt : {2, 1}) {
+    if (ns && cpt == 2) continue;
     for (int tj : {0, 16, 20, 25, 32, 40, 50, 64})
-      if (tj == 0 || tj <= h.ny) cands.push_back({cpt, tj});
+      if ((tj == 0 || tj <= h.ny) && !(ns && tj > 40)) cands.push_back({cpt, tj});
+  }
   double best = 1e30;
   Cand win{lean_cpt, lean_tj};
   char b[160];
@@ -3759,6 +3766,7 @@ std::string DeviceSolver::autotune(int steps) {
   last_res_valid = s_resv;
   upload();   // device scalars from the restored host state
   graph_launches = 0;
+  lns_steps = lnm_steps = 0;   // (the tuning steps do not count as the run's)
   std::snprintf(b, sizeof b, "best cpt=%d tj=%d (%.2f us/step)", win.cpt, win.tj, best);
   return log + b;
 }
