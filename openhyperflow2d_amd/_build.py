@@ -24,7 +24,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("HF2D_OFFLOAD_ARCH", "gfx950")
 
 CORE_SRCS = ["deck.cpp", "gasdyn.cpp", "config.cpp", "preprocess.cpp", "checkpoint.cpp", "postproc.cpp", "stripio.cpp", "case_io.cpp", "tcpcomm.cpp", "solver.cpp", "lean.cpp", "mechanism.cpp"]
-HIP_SRCS = ["device_solver.hip", "chem_mech.hip", "chem_fast.hip", "chem_rtc.hip"]
+HIP_SRCS = ["device_solver.hip", "chem_mech.hip", "chem_fast.hip", "chem_rtc.hip", "numerics.hip"]
 # headers handed to hiprtc by chem_rtc.hip (embedded as string literals)
 RTC_EMBED = [("kChemTypesSrc", "chem_fast_types.hpp"), ("kChemDevSrc", "chem_fast_dev.hpp")]
 

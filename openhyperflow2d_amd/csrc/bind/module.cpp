@@ -16,6 +16,7 @@
 #include "../hip/chem_fast.hpp"
 #include "../hip/chem_rtc.hpp"
 #include "../hip/device_solver.hpp"
+#include "../hip/numerics.hpp"
 
 namespace py = pybind11;
 using namespace hf2d;
@@ -133,6 +134,15 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
+  // hf_div / hf_sqrt evaluated on the GPU (csrc/hip/numerics.hip): (a / b, sqrt(a))
+  m.def("div_probe", [](py::array_t<double, py::array::c_style | py::array::forcecast> a,
+                        py::array_t<double, py::array::c_style | py::array::forcecast> b) {
+    if (a.size() != b.size()) throw std::runtime_error("div_probe: a and b differ in size");
+    const long n = (long)a.size();
+    py::array_t<double> q(n), s(n);
+    div_probe(a.data(), b.data(), q.mutable_data(), s.mutable_data(), n);
+    return py::make_tuple(q, s);
+  });
   // K12 kinetics for runtime mechanisms on the MFMA cores (csrc/hip/chem_mech.hip): mechanism
   // given as a built-in name or the text of a .mech file; returns (rhoY, T, mean ms)
   m.def(
