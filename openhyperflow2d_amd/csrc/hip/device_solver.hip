@@ -426,16 +426,21 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   // (compiled into the single-gas two-cell kernel only: the mere presence of
   // this block made the multi-gas one-cell kernel 3x slower on the triple
   // point, 340 -> 1030 us, even with stagger 0)
-  if (HF2D_TILE_STAGGER && SG && CPT == 2 && !FX && P.stagger > 0) {
+  if (HF2D_TILE_STAGGER && SG && CPT == 2 && !FX && P.stagger != 0) {
     // staggered start: every workgroup of a step is resident at once, so
     // without it they all stage together (HBM saturated, VALUs idle) and
     // then all compute (HBM idle); later dispatch rounds start loading while
     // the earlier ones compute
     // (rounds beyond the 4th are dispatched as earlier workgroups retire:
     // no wait for them)
+    // (stagger > 0: whole rounds of stagger_wgs workgroups; < 0: a linear
+    // ramp of the same slope over the first four rounds)
     const unsigned r = blockIdx.x / (unsigned)P.stagger_wgs;
-    if (r > 0 && r < 4) {
-      const unsigned long long t0 = rt_clock(), d = (unsigned long long)r * (unsigned)P.stagger;
+    if (r < 4 && (P.stagger < 0 || r > 0)) {
+      const unsigned long long d = P.stagger > 0 ? (unsigned long long)r * (unsigned)P.stagger
+                                                 : (unsigned long long)blockIdx.x * (unsigned)(-P.stagger) /
+                                                       (unsigned)P.stagger_wgs;
+      const unsigned long long t0 = rt_clock();
       while (rt_clock() - t0 < d) __builtin_amdgcn_s_sleep(2);
     }
   }
