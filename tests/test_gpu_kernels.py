@@ -614,3 +614,45 @@ def test_autotune_thread_block_size_zero(gpu, monkeypatch):
     assert a.summary()["time"] == b.summary()["time"]
     for f in FIELDS:
         np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("deck", ["step", "resonator"])
+def test_autotune_lean_ns_tile_height(gpu, monkeypatch, deck):
+    """The lean N-S tile height is tuned too (one cell per thread); the tuning
+    steps leave no trace: same fields, dt and time as an untuned run, and the
+    tuned run's lean steps are the run's own."""
+    text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5) if deck == "step" else \
+        decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    assert "best cpt=1 tj=" in a.autotune_log, a.autotune_log
+    assert a.solver.lns_steps == 0
+    monkeypatch.setenv("HF2D_AUTOTUNE", "0")
+    b = gpu.Simulation(text, "gpu")
+    assert b.autotune_log == ""
+    for n, res in [(4, True), (30, False), (6, True)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+    assert a.solver.lns_steps > 0
+    assert a.summary()["dt"] == b.summary()["dt"] and a.summary()["time"] == b.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("stagger", [0, 150, -300])
+def test_tile_stagger_is_timing_only(gpu, monkeypatch, stagger):
+    """The staggered start of the tile kernel's dispatch rounds (HF2D_STAGGER,
+    whole rounds or a ramp) delays workgroups only: bitwise the same run."""
+    text = decks.wedge15(600, 80, nmax=10 ** 6, nout=10 ** 5)
+    monkeypatch.setenv("HF2D_AUTOTUNE", "0")
+    ref = gpu.Simulation(text, "gpu")
+    ref.solver.tile_stagger = 0
+    monkeypatch.setenv("HF2D_STAGGER", str(stagger))
+    s = gpu.Simulation(text, "gpu")
+    assert s.solver.tile_stagger == stagger
+    s.solver.lean_cpt = ref.solver.lean_cpt = 2
+    for n, res in [(5, True), (25, False), (3, True)]:
+        s.step(n, residual=res)
+        ref.step(n, residual=res)
+    assert s.summary()["dt"] == ref.summary()["dt"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(s.field(f), ref.field(f), err_msg=f)
