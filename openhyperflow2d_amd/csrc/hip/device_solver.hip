@@ -3720,8 +3720,8 @@ std::string DeviceSolver::autotune(int steps) {
   std::vector<Cand> cands;
   for (int cpt : {2, 1}) {
     if (ns && cpt == 2) continue;
-    for (int tj : {0, 16, 20, 25, 32, 40, 50, 64})
-      if ((tj == 0 || tj <= h.ny) && !(ns && tj > 40)) cands.push_back({cpt, tj});
+    for (int tj : {0, 10, 12, 14, 16, 20, 25, 32, 40, 50, 64})
+      if ((tj == 0 || tj <= h.ny) && (ns ? tj <= 40 : (tj == 0 || tj >= 16))) cands.push_back({cpt, tj});
   }
   double best = 1e30;
   Cand win{lean_cpt, lean_tj};
