@@ -695,10 +695,12 @@ constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho 
 
 template <bool RES, int MODE, int TURB>
 __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
-                                              int slot, int slot_next, int serial, ResidualPack* partials) {
+                                              int slot, int slot_next, int serial, ResidualPack* partials,
+                                              int part) {
   extern __shared__ real lds[];
   constexpr int NL = Lns<MODE>::NL;
-  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  // part: 0 every tile, 1 / 2 the edge / interior tiles (comm overlap)
+  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
@@ -872,15 +874,16 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
 
 template <bool RES, int MODE, int TURB = 2>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
-                                                        int slot, int slot_next, int serial, ResidualPack* partials) {
-  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
+                                                        int slot, int slot_next, int serial, ResidualPack* partials,
+                                                        int part) {
+  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials, part);
 }
 // register budget of OCC waves per SIMD (DeviceSolver::lns_occ, measured)
 template <bool RES, int MODE, int OCC, int TURB = 2>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(OCC))) void hf2d_lns_step_occ(
     StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
-    ResidualPack* partials) {
-  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
+    ResidualPack* partials, int part) {
+  lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials, part);
 }
 
 // ---------------------------------------------------------------------------
@@ -1512,7 +1515,7 @@ using LeanEulerK = void (*)(StepParams, LeanSoA, long, long, DevScalars*, int, i
 static const LeanEulerK kLeanEuler[2][2] = {{hf2d_lean_euler<false, false>, hf2d_lean_euler<false, true>},
                                             {hf2d_lean_euler<true, false>, hf2d_lean_euler<true, true>}};
 
-using LnsK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*);
+using LnsK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*, int);
 // [laminar, k-eps, SST, SA][residual][register budget: default, 3, 5 waves per SIMD]
 static const LnsK kLns[4][2][3] = {
     {{hf2d_lns_step<false, SK_SGL>, hf2d_lns_step_occ<false, SK_SGL, 3>, hf2d_lns_step_occ<false, SK_SGL, 5>},
@@ -3557,7 +3560,24 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // (a residual step runs the compiler's register budget)
       const int tv = !t2 ? 0 : lns_turb == 3 ? 2 : lns_turb == 4 ? 3 : 1;
       const LnsK lk = kLns[tv][want_res][want_res ? 0 : (occ == 5 ? 2 : occ == 3 ? 1 : 0)];
-      hipLaunchKernelGGL(lk, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial, m.partials);
+      // RCCL / in-process transports: edge tiles first, their halo on the comm
+      // stream while the interior tiles compute, then the dt MIN (as the
+      // inviscid tile kernel; the xGMI mailbox exchange folds the dt into its
+      // handshake and runs after the step)
+      lns_split = comm_overlap && !m.p2p.on && (m.comm || m.local) && m.nranks > 1 && !want_res && T.nbi >= 3 &&
+                  cs.cfg.isAdiabaticWall;
+      if (lns_split) {
+        if (!m.comm_stream) {
+          HIP_CHECK(hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking));
+          HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
+          HIP_CHECK(hipEventCreateWithFlags(&m.ev_halo, hipEventDisableTiming));
+        }
+        hipLaunchKernelGGL(lk, dim3(2 * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
+                           m.partials, 1);
+      } else {
+        hipLaunchKernelGGL(lk, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
+                           m.partials, 0);
+      }
       HIP_CHECK(hipGetLastError());
       nres = (unsigned)ntile;
       sbuf = 1 - sbuf;
@@ -3565,6 +3585,26 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       cbuf = 1 - cbuf;
       dsbuf = 1 - dsbuf;
       lns_steps++;
+      if (lns_split) {
+        HIP_CHECK(hipEventRecord(m.ev_edge, st));
+        // interior tiles in flight before the exchange is issued; they write
+        // neither the edge columns nor the ghost columns
+        hipLaunchKernelGGL(lk, dim3((T.nbi - 2) * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
+                           serial, m.partials, 2);
+        HIP_CHECK(hipGetLastError());
+        if (m.local) {   // in-process group: the host orders the streams (see the inviscid path)
+          HIP_CHECK(hipEventSynchronize(m.ev_edge));
+          exchange(CpuSolver::HALO_LNS, -1, (void*)m.comm_stream);
+          HIP_CHECK(hipStreamSynchronize(m.comm_stream));
+        } else {
+          HIP_CHECK(hipStreamWaitEvent(m.comm_stream, m.ev_edge, 0));
+          exchange(CpuSolver::HALO_LNS, -1, (void*)m.comm_stream);
+          HIP_CHECK(hipEventRecord(m.ev_halo, m.comm_stream));
+          HIP_CHECK(hipStreamWaitEvent(st, m.ev_halo, 0));
+        }
+        exchange_dt(slot_next);
+        overlap_steps++;
+      }
     }
   } else {
     if (lean_state) lean_materialize();
@@ -3574,6 +3614,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   // new-state halo + global dt (MIN over ranks into the next slot)
   if (fx_step) {
     fx_pending = true;   // exchanged inside the tile kernel
+  } else if (lns_split) {
+    lns_split = false;   // exchanged above, overlapped with the interior tiles
   } else if ((m.comm || m.local || m.p2p.on) && m.nranks > 1) {
     exchange(lns_state ? CpuSolver::HALO_LNS : lean_state ? CpuSolver::HALO_LEAN : CpuSolver::HALO_STATE, slot_next);
   }

@@ -111,6 +111,7 @@ class DeviceSolver : public SolverBase {
   // RCCL / in-process transports: halo of the edge tiles on a comm stream while
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
+  bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
   long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
   void halo_fields(int group, std::vector<real*>& f, bool full = false) const;

@@ -315,6 +315,8 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
                                fields=fields)
     lean_steps = stats["lnm_steps"] if deck == "scramjet" else stats["lns_steps"]
     assert min(lean_steps) > 0, stats
+    if not p2p and deck != "scramjet":   # in-process transport: edge tiles first, halo overlapped
+        assert min(stats["overlap_steps"]) > 0, stats
     ref = gpu.Simulation(text, "gpu")
     for n, res in schedule:
         ref.step(n, residual=res)
