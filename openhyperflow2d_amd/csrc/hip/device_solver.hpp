@@ -194,14 +194,14 @@ class DeviceSolver : public SolverBase {
   std::string lnm_why;
   int lnm_turb = 0;       // fill_node turbulence set of the kernel: 0 none, 3 SST
   long lnm_steps = 0;
-  int lnm_ti = 16;
+  int lnm_ti = 16;   // mechanism tile columns (16 rows): 16 or 12 (lean_mech.hpp lnm_tile)
   // HF2D_STAGGER: staggered start of the inviscid tile kernel's resident
   // dispatch rounds, 10 ns ticks per round of cu_count workgroups; > 0 whole
-  // rounds, < 0 a linear ramp (headline 2000x200, 1x MI355X: off 31.3 us;
-  // rounds of 1.0 / 1.5 / 2.0 / 3.0 us 31.4 / 29.9 / 31.3 / 33.0 us; ramp of
-  // 0.5 / 1.0 / 1.5 / 2.0 / 3.0 us per round 30.7 / 30.1 / 29.6 / 30.4 / 32.3 us)
+  // rounds, < 0 a linear ramp (headline 2000x200, 1x MI355X, after the fast
+  // divide: off 31.3 us, rounds of 1.5 us 29.9 us; ramp of 0.5 / 1.0 / 1.5 /
+  // 2.0 / 3.0 us per round 30.7 / 30.1 / 29.6 / 30.4 / 32.3 us)
   int tile_stagger = -150;
-  std::vector<unsigned long long> lnm_trace_fetch();   // HF2D_LNM_TRACE: 12 clocks / ids per workgroup        // tile columns (16 rows): 16 or 12 (lean_mech.hpp lnm_tile)
+  std::vector<unsigned long long> lnm_trace_fetch();   // HF2D_LNM_TRACE: 12 clocks / ids per workgroup
   std::vector<uint8_t> lean_bytes;
   ScenarioTables scen_host;   // staged for upload (must outlive the async copy)
   void lean_materialize();
