@@ -921,7 +921,10 @@ __device__ __forceinline__ void lnm_fill(StepParams& P, const LnmArrays& a, cons
     }
 }
 
-template <bool RES, int TURB>
+// STRIP: the strip has a right neighbour, so a partial last tile may hold its
+// first ghost column (pass 1 below); without it the fill runs in one pass
+// (56 instead of 112 B/lane of scratch for the SST kernel)
+template <bool RES, int TURB, bool STRIP = true>
 __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
@@ -959,7 +962,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   // Both fills go through one call site: a second inlined copy of the fill
   // pushed the SST kernel from 56 to 784 B/lane of scratch (2x slower).
 #pragma unroll 1
-  for (int pass = 0; pass < 2; pass++) {
+  for (int pass = 0; pass < (STRIP ? 2 : 1); pass++) {
     int gi = -1, gj = 0, ri = 0, rj = 0;
     if (pass == 0) {
       if (rt >= 0 && rt < nring) {
@@ -1184,11 +1187,11 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
 
 // (two workgroups per CU: the LDS of a 16 x 16 tile is ~80 KB, so a budget
 // of 2 waves per SIMD costs no occupancy)
-template <bool RES, int TURB>
+template <bool RES, int TURB, bool STRIP = true>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void hf2d_lnm_step(
     StepParams P, LnmArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
     ResidualPack* partials) {
-  lnm_step_body<RES, TURB>(P, a, T, sc, slot, slot_next, serial, partials);
+  lnm_step_body<RES, TURB, STRIP>(P, a, T, sc, slot, slot_next, serial, partials);
 }
 
 // E_{m+1} of the cells the kinetics changed (after them): state and dt.
@@ -3303,8 +3306,11 @@ bool DeviceSolver::lnm_step_ok(const StepParams& P) const {
 
 using LnmK = void (*)(StepParams, LnmArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*);
 // [residual][SST]
-static const LnmK kLnm[2][2] = {{hf2d_lnm_step<false, 0>, hf2d_lnm_step<false, 3>},
-                                {hf2d_lnm_step<true, 0>, hf2d_lnm_step<true, 3>}};
+// [residual][SST][strip with a right neighbour] (residual steps: the strip variant)
+static const LnmK kLnm[2][2][2] = {
+    {{hf2d_lnm_step<false, 0, false>, hf2d_lnm_step<false, 0, true>},
+     {hf2d_lnm_step<false, 3, false>, hf2d_lnm_step<false, 3, true>}},
+    {{hf2d_lnm_step<true, 0>, hf2d_lnm_step<true, 0>}, {hf2d_lnm_step<true, 3>, hf2d_lnm_step<true, 3>}}};
 
 // One lean mechanism step (lean_mech.hpp): tile kernel, kinetics of the
 // listed cells in place on the new species, their state kernel.
@@ -3332,12 +3338,13 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
   const LeanTile T = lnm_tile(P.i1 - P.i0, P.ny, lnm_ti);
   const LnmLayout L(T.TI, T.TJ, m.nsp - 1);
   const size_t shmem = (size_t)L.total() * sizeof(real);
-  const LnmK k = kLnm[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0];
-  static bool attr_set[2][2] = {{false, false}, {false, false}};
-  if (!attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0]) {
+  const int strip = P.i1 < P.nx ? 1 : 0;
+  const LnmK k = kLnm[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip];
+  static bool attr_set[2][2][2] = {};
+  if (!attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip]) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
     (void)hipGetLastError();
-    attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0] = true;
+    attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip] = true;
   }
   hipLaunchKernelGGL(k, dim3(T.nbi * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
                      m.partials);
