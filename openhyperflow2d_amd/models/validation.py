@@ -11,6 +11,7 @@ Correlations, with Eckert's reference temperature for compressibility
 (T*/T_e = 0.5 + 0.039 M_e^2 + 0.5 T_w/T_e, Sutherland viscosity):
   laminar (Blasius)       Cf = 0.664 sqrt(C*) / sqrt(Re_x),  C* = rho* mu* / (rho_e mu_e)
   turbulent (Schlichting) Cf = 0.0592 (rho*/rho_e) (Re_x*)^-0.2,  Re_x* = rho* U_e x / mu*
+and, as a second compressible turbulent reference, van Driest II (van_driest_ii).
 """
 from __future__ import annotations
 
@@ -22,6 +23,28 @@ import numpy as np
 
 def sutherland(T: float) -> float:
     return 1.716e-5 * (T / 273.15) ** 1.5 * (273.15 + 110.4) / (T + 110.4)
+
+
+def van_driest_ii(re_x, mach: float, Te: float, Tw, r: float = 0.89, gamma: float = 1.4):
+    """Turbulent flat-plate Cf by the van Driest II transformation (Hopkins &
+    Inouye's form): Cf = Cf_inc(F_Rx Re_x) / F_c with
+      m = (gamma-1)/2 M^2,  T_aw/T_e = 1 + r m,
+      A = (r m T_e/T_w)^1/2,  B = T_aw/T_w - 1,
+      alpha = (2A^2 - B)/(4A^2 + B^2)^1/2,  beta = B/(4A^2 + B^2)^1/2,
+      F_c = (T_aw/T_e - 1) / (asin alpha + asin beta)^2,
+      F_Rx = (mu_e/mu_w) / F_c  (Sutherland viscosities),
+    and the same incompressible law as the Eckert comparison, Cf_inc = 0.0592 Re^-0.2."""
+    re_x = np.asarray(re_x, dtype=np.float64)
+    Tw = np.asarray(Tw, dtype=np.float64)
+    m = 0.5 * (gamma - 1.0) * mach * mach
+    taw_te = 1.0 + r * m
+    a = np.sqrt(r * m * Te / Tw)
+    b = taw_te * Te / Tw - 1.0
+    den = np.sqrt(4.0 * a * a + b * b)
+    fc = (taw_te - 1.0) / (np.arcsin((2.0 * a * a - b) / den) + np.arcsin(b / den)) ** 2
+    mu_w = np.array([sutherland(t) for t in np.atleast_1d(Tw)]).reshape(Tw.shape)
+    frx = (sutherland(Te) / mu_w) / fc
+    return 0.0592 * (frx * re_x) ** -0.2 / fc
 
 
 def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
@@ -69,7 +92,7 @@ def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
             tau_eff[q] = max(tau_eff[q], t)
     cf_eff = np.sign(cf) * tau_eff / (0.5 * rhoe * Ue * Ue)
     return {"x": x, "Re_x": rex, "Cf": cf, "Cf_eff": cf_eff, "Cf_lam": lam, "Cf_turb": turb,
-            "Mach": np.full_like(x, Me), "Tw": Tw}
+            "Cf_turb_vd2": van_driest_ii(rex, Me, Te, Tw), "Mach": np.full_like(x, Me), "Tw": Tw}
 
 
 def langley_phi(mc: float) -> float:

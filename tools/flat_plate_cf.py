@@ -59,9 +59,11 @@ print("model %d grid %dx%d dy=%g cfl=%s beta0=%s: %d steps, t=%.3g s (%.1f s wal
 print("Mach_e %.2f  Tw/Te %.2f..%.2f" % (r["Mach"][0], r["Tw"].min() / 288.9, r["Tw"].max() / 288.9))
 for q in (0.1, 0.25, 0.5, 0.75, 0.9):
     k = int(q * (len(r["x"]) - 1))
-    print("Re_x %9.3g  Cf %.4e  Cf/lam %.3f  Cf/turb %.3f  effective (max near-wall stress) Cf/lam %.3f Cf/turb %.3f" % (
-        r["Re_x"][k], r["Cf"][k], r["Cf"][k] / r["Cf_lam"][k], r["Cf"][k] / r["Cf_turb"][k],
-        r["Cf_eff"][k] / r["Cf_lam"][k], r["Cf_eff"][k] / r["Cf_turb"][k]))
+    print("Re_x %9.3g  Cf %.4e  Cf/lam %.3f  Cf/turb %.3f  effective (max near-wall stress) Cf/lam %.3f Cf/turb %.3f"
+          "  Cf/vdII %.3f" % (
+              r["Re_x"][k], r["Cf"][k], r["Cf"][k] / r["Cf_lam"][k], r["Cf"][k] / r["Cf_turb"][k],
+              r["Cf_eff"][k] / r["Cf_lam"][k], r["Cf_eff"][k] / r["Cf_turb"][k],
+              r["Cf_eff"][k] / r["Cf_turb_vd2"][k]))
 if a.model:
     mut, mu, yp = (np.asarray(sim.field(f)) for f in ("mu_t", "mu", "y_plus"))
     k_ = np.asarray(sim.field("S7")) / np.asarray(sim.field("rho"))
