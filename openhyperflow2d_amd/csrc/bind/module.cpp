@@ -508,6 +508,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_sg", &CpuSolver::lean_sg)
       .def_readwrite("lean_tj", &CpuSolver::lean_tj)
       .def_readwrite("lean_cpt", &CpuSolver::lean_cpt)
+      .def_readwrite("lean_nt", &CpuSolver::lean_nt)
       .def_readonly("lean_sg_ok", &CpuSolver::lean_sg_ok)
       .def_readonly("lean_ok", &CpuSolver::lean_ok)
       .def_readonly("lean_why", &CpuSolver::lean_why)
@@ -730,6 +731,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("chem_fast_ok", &DeviceSolver::chem_fast_ok)
       .def_readonly("graph_launches", &DeviceSolver::graph_launches)
       .def_readwrite("lean_cpt", &DeviceSolver::lean_cpt)
+      .def_readwrite("lean_nt", &DeviceSolver::lean_nt)
       .def_readwrite("sgl", &DeviceSolver::sgl)
       .def_readonly("sgl_ok", &DeviceSolver::sgl_ok)
       .def_readonly("sgl_why", &DeviceSolver::sgl_why)

@@ -957,7 +957,7 @@ StepResult CpuSolver::do_step(const StepParams& P0, bool want_res) {
     if (!fromg && lean_tile && P.ny >= LEAN_TILE_MIN_TJ) {
       // host emulation of the device's LDS-tiled kernel (same staging and
       // indexing); unstaged LDS entries are poisoned with NaN
-      constexpr int NT = 256;
+      const int NT = lean_nt == 128 || lean_nt == 64 ? lean_nt : 256;
       const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, NT, lean_tj, lean_cpt == 2 ? 2 : 1);
       const bool sg = lean_sg && lean_sg_ok;
       std::vector<real> lds((size_t)lean_tile_fields(sg) * T.NC);

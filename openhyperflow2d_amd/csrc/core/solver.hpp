@@ -214,6 +214,7 @@ class CpuSolver : public SolverBase {
   bool lean_tile = false;   // emulate the device's LDS-tiled lean kernel
   bool lean_sg = true;      // single-gas specialisation when the case allows it
   int lean_tj = 0, lean_cpt = 1;   // tile height override, cells per thread
+  int lean_nt = 256;               // threads per emulated tile workgroup (256 / 128 / 64)
   bool lean_sg_ok = false;
   bool lean_ok = false;
   std::string lean_why;

@@ -158,11 +158,11 @@ TcpComm::TcpComm(int rank, int size, const std::string& addr, int port, double t
   if (size < 1 || rank < 0 || rank >= size) throw std::runtime_error("TcpComm: bad rank/size");
   if (size == 1) return;
   // every rank >= 1 listens for its left neighbour on an ephemeral port of
-  // all its interfaces; rank 0 learns each rank's address from its control
-  // connection and publishes (address, port) pairs, so the neighbour chain
-  // also forms across hosts
+  // the interface its control connection uses (not every interface: a stray
+  // connection from elsewhere would be taken for the neighbour); rank 0
+  // learns each rank's address from its control connection and publishes
+  // (address, port) pairs, so the neighbour chain also forms across hosts
   int nb_lfd = -1, nb_port = 0;
-  if (r_ > 0) nb_lfd = listen_on("0.0.0.0", 0, 1, &nb_port);
   std::vector<uint32_t> nb_tab(2 * n_, 0);   // [2r] = IPv4 (network order), [2r+1] = port
   if (r_ == 0) {
     const int lfd = listen_on(addr, port, n_, nullptr);
@@ -184,6 +184,12 @@ TcpComm::TcpComm(int rank, int size, const std::string& addr, int port, double t
     for (int k = 1; k < n_; k++) send_all(ctrl_[k], nb_tab.data(), sizeof(uint32_t) * nb_tab.size());
   } else {
     ctrl_.assign(1, connect_retry(addr, port, timeout_s));
+    sockaddr_in me{};
+    socklen_t ml = sizeof me;
+    if (::getsockname(ctrl_[0], (sockaddr*)&me, &ml) != 0) fail("getsockname");
+    char mine[INET_ADDRSTRLEN] = "0.0.0.0";
+    ::inet_ntop(AF_INET, &me.sin_addr, mine, sizeof mine);
+    nb_lfd = listen_on(mine, 0, 1, &nb_port);
     const int hello[2] = {r_, nb_port};
     send_all(ctrl_[0], hello, sizeof hello);
     recv_all(ctrl_[0], nb_tab.data(), sizeof(uint32_t) * nb_tab.size());

@@ -19,7 +19,16 @@ struct DevScalars {
                                    // mechanism step's fill belongs to the previous one)
   unsigned hot_cnt[3];             // lean mechanism step: reacting cells listed by the step using the slot
   unsigned pad2;
+  // Sharded dt MIN: every workgroup of a step used to atomicMin into ONE word,
+  // and device-scope atomics to one address serialise at the memory side
+  // (~10 ns each: 800 workgroups of a small-strip step queued 7 us behind
+  // them, profiles/small_strip_r04.md).  Workgroup b min-reduces into shard
+  // b % DT_SHARDS (one 128-byte line each) instead; the value of a slot is
+  // MIN(dt_bits[slot], its shards) (dt_get), and folds that publish a
+  // global MIN store it into dt_bits[slot] (the shards stay >= it).
+  alignas(128) unsigned long long dt_sh[3][16][16];
 };
+constexpr int DT_SHARDS = 16;
 
 __device__ inline double bits_to_d(unsigned long long b) { return __longlong_as_double((long long)b); }
 __device__ inline unsigned long long d_to_bits(double d) { return (unsigned long long)__double_as_longlong(d); }
@@ -27,8 +36,49 @@ __device__ inline unsigned long long d_to_bits(double d) { return (unsigned long
 // Step n reads slot n%3, min-reduces into (n+1)%3 and resets (n+2)%3.
 __host__ __device__ inline int slot_reset(int slot) { return (slot + 2) % 3; }
 
+// (IEEE bits of positive doubles order like the values)
+__host__ __device__ inline unsigned long long dt_bits_min(unsigned long long a, unsigned long long b) {
+  return a < b ? a : b;
+}
+// value of a dt slot: the word and its shards (plain loads: the producers
+// are earlier kernels)
+__device__ inline double dt_get(const DevScalars* sc, int slot) {
+  unsigned long long b = sc->dt_bits[slot];
+#pragma unroll
+  for (int k = 0; k < DT_SHARDS; k++) b = dt_bits_min(b, sc->dt_sh[slot][k][0]);
+  return bits_to_d(b);
+}
+// same inside the producing kernel, after its workgroups' atomics (relaxed
+// agent-scope loads)
+__device__ inline double dt_get_fresh(DevScalars* sc, int slot) {
+  unsigned long long b = __hip_atomic_load(&sc->dt_bits[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < DT_SHARDS; k++)
+    b = dt_bits_min(b, __hip_atomic_load(&sc->dt_sh[slot][k][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  return bits_to_d(b);
+}
+// a step's contribution (one thread per workgroup)
+__device__ inline void dt_min(DevScalars* sc, int slot, double m) {
+  atomicMin(&sc->dt_sh[slot][blockIdx.x % DT_SHARDS][0], d_to_bits(m));
+}
+__device__ inline void dt_reset(DevScalars* sc, int slot) {
+  const unsigned long long one = d_to_bits(1.0);
+  sc->dt_bits[slot] = one;
+#pragma unroll
+  for (int k = 0; k < DT_SHARDS; k++) sc->dt_sh[slot][k][0] = one;
+}
+__host__ inline unsigned long long dt_get_host(const DevScalars& s, int slot) {
+  unsigned long long b = s.dt_bits[slot];
+  for (int k = 0; k < DT_SHARDS; k++) b = dt_bits_min(b, s.dt_sh[slot][k][0]);
+  return b;
+}
+__host__ inline void dt_set_host(DevScalars& s, int slot, unsigned long long b) {
+  s.dt_bits[slot] = b;
+  for (int k = 0; k < DT_SHARDS; k++) s.dt_sh[slot][k][0] = b;
+}
+
 __device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
-  const double dt = bits_to_d(sc->dt_bits[slot]);
+  const double dt = dt_get(sc, slot);
   P.dt = dt;
   P.dtdx = dt / P.dx;
   P.dtdy = dt / P.dy;

@@ -121,7 +121,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
     // Reset the slot the NEXT step will accumulate into (never the one this
     // step's fill is min-reducing, which other blocks may already be
     // writing) and accumulate physical time.
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     sc->dt_val[slot] = P.dt;
     sc->hot_cnt[slot_next] = 0;
@@ -205,7 +206,7 @@ __device__ __forceinline__ void fill_body(StepParams& P, const SoA& sin, const S
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
-    if (slot_next >= 0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));   // < 0: lean N-S materialize
+    if (slot_next >= 0) dt_min(sc, slot_next, m);   // < 0: lean N-S materialize
   }
 }
 
@@ -233,7 +234,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   apply_dt(P, sc, slot);
   const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
   if (g == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
   }
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);  // serial build: dt is a running minimum
-    if (slot_next >= 0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));   // < 0: lean N-S materialize
+    if (slot_next >= 0) dt_min(sc, slot_next, m);   // < 0: lean N-S materialize
   }
 }
 
@@ -277,7 +279,8 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
   const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
   const long g = (long)b * BLOCK + threadIdx.x;
   if (g == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
   }
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    dt_min(sc, slot_next, m);
   }
 }
 
@@ -362,6 +365,7 @@ __device__ inline void p2p_store(double* p, double v) {
 // have completed: the ordering point for the relaxed system-coherent stores
 __device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+constexpr int FX_DONE_STRIDE = 32;   // completion counters on lines of their own
 struct FusedX {
   real* peer_recv_l;   // left neighbour's mailbox recv base (we are its right side)
   real* peer_recv_r;
@@ -371,7 +375,7 @@ struct FusedX {
   const unsigned long long* my_flags;
   const double* my_dtr;
   unsigned long long* seq;   // last published sequence number
-  unsigned* done;            // workgroups finished in this step
+  unsigned* done;            // workgroups finished in this step: per dt shard, then the shards (FX_DONE_STRIDE apart)
   long cap;
   int rank, nranks, sides, on;
 };
@@ -415,7 +419,11 @@ __device__ inline unsigned tile_of_part(unsigned bl, int part, const LeanTile& T
   return bl;
 }
 
-template <bool RES, bool OUT, bool SG, int CPT, bool FX = false, bool TR = false>
+// NT: threads per workgroup (BLOCK, or 128 / 64 for the small strips of a
+// multi-GPU run: at 250 x 200 cells per GPU a 256-thread tiling leaves ~50 of
+// the 256 CUs without a workgroup, and the step is one workgroup's
+// load -> compute -> reduce chain)
+template <bool RES, bool OUT, bool SG, int CPT, bool FX = false, bool TR = false, int NT = BLOCK>
 __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, const LeanTile& T, DevScalars* sc,
                                                int slot, int slot_next, int serial, ResidualPack* partials,
                                                const FusedX& X = FusedX{}, unsigned long long* trace = nullptr,
@@ -426,7 +434,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   // (compiled into the single-gas two-cell kernel only: the mere presence of
   // this block made the multi-gas one-cell kernel 3x slower on the triple
   // point, 340 -> 1030 us, even with stagger 0)
-  if (HF2D_TILE_STAGGER && SG && CPT == 2 && !FX && P.stagger != 0) {
+  if (HF2D_TILE_STAGGER && SG && CPT == 2 && !FX && NT == BLOCK && P.stagger != 0) {
     // staggered start: every workgroup of a step is resident at once, so
     // without it they all stage together (HBM saturated, VALUs idle) and
     // then all compute (HBM idle); later dispatch rounds start loading while
@@ -449,7 +457,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   if (FX) seq_prev = *X.seq;
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
   }
@@ -463,7 +472,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     if (mine[q]) lean_load_own<TileIO<SG>::NE>(L, (long)i[q] * P.ny + j[q], own[q]);
   }
   if (!FX || seq_prev == 0 || (i0 - 1 > P.i0 - 1 && i0 + T.TI < P.i1)) {
-    lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, BLOCK);
+    lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, NT);
   } else {
     // edge tile: the ghost column comes from the mailbox of parity seq_prev
     constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
@@ -473,7 +482,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     const long N = L.N;
     constexpr int NS = SG ? 4 : 4 + NCOMP;
     constexpr int FU = SG ? 4 : 10;
-    for (int c = threadIdx.x; c < T.NC; c += BLOCK) {
+    for (int c = threadIdx.x; c < T.NC; c += NT) {
       const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
       const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
       const int gi = i0 + ii, gj = j0 + jj;
@@ -539,19 +548,19 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
-    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (BLOCK / WAVE) + threadIdx.x / WAVE] = r;
+    if ((threadIdx.x & (WAVE - 1)) == 0) partials[(long)b * (NT / WAVE) + threadIdx.x / WAVE] = r;
   }
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
-  __shared__ double sdt[BLOCK / WAVE];
+  __shared__ double sdt[NT / WAVE];
   if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
   if (neg) atomicOr(&sc->neg_T, 1);
   __syncthreads();
   if (TR) tr[3] = rt_clock();
   if (threadIdx.x == 0) {
     double m = sdt[0];
-    for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
+    for (int q = 1; q < NT / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    dt_min(sc, slot_next, m);
     if (TR) {
       vm_drain();
       tr[4] = rt_clock();
@@ -566,12 +575,25 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       // the barrier above drained every wave's mailbox stores; drain the
       // dt atomic before counting this workgroup as done
       vm_drain();
-      const unsigned prev = __hip_atomic_fetch_add(X.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {   // last workgroup: publish this rank's step, then fold the peers'
-        __hip_atomic_store(X.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // completion count in two levels (one counter per dt shard, then one
+      // for the shards): a single counter serialises every workgroup's
+      // returning atomic at the memory side
+      const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
+      const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
+      unsigned* cs = X.done + sh * FX_DONE_STRIDE;
+      unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
+      bool last = false;
+      if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
+        __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+          __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = true;
+        }
+      }
+      if (last) {   // last workgroup: publish this rank's step, then fold the peers'
         const unsigned long long sn = seq_prev + 1;
         const int pn = (int)(sn & 1);
-        double d = bits_to_d(__hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        double d = dt_get_fresh(sc, slot_next);
         for (int q = 0; q < X.nranks; q++)
           if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
         vm_drain();
@@ -627,6 +649,29 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile_fx(StepParams P, LeanSoA
   lean_tile_body<RES, OUT, SG, CPT, true>(P, L, T, sc, slot, slot_next, serial, partials, X);
 }
 
+// Small-strip geometries (single gas): NT = 128 / 64 threads per workgroup
+// (picked by the ThreadBlockSize = 0 autotune per strip)
+template <bool RES, bool OUT, int NT, int CPT>
+__global__ __launch_bounds__(NT) void hf2d_lean_tile_nt(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                       int slot, int slot_next, int serial, ResidualPack* partials,
+                                                       int part = 0) {
+  lean_tile_body<RES, OUT, true, CPT, false, false, NT>(P, L, T, sc, slot, slot_next, serial, partials, FusedX{},
+                                                        nullptr, part);
+}
+template <bool RES, bool OUT, int NT, int CPT>
+__global__ __launch_bounds__(NT) void hf2d_lean_tile_fx_nt(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                          int slot, int slot_next, int serial,
+                                                          ResidualPack* partials, FusedX X) {
+  lean_tile_body<RES, OUT, true, CPT, true, false, NT>(P, L, T, sc, slot, slot_next, serial, partials, X);
+}
+template <int NT, int CPT>
+__global__ __launch_bounds__(NT) void hf2d_lean_tile_tr_nt(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
+                                                          int slot, int slot_next, int serial,
+                                                          ResidualPack* partials, unsigned long long* trace) {
+  lean_tile_body<false, false, true, CPT, false, true, NT>(P, L, T, sc, slot, slot_next, serial, partials, FusedX{},
+                                                           trace);
+}
+
 // Ghost columns + global dt after fused steps, for any other consumer: wait
 // for the peers' last publication, copy the mailbox of that parity into the
 // ghost columns of the current state, fold the dt MIN into the slot.
@@ -654,7 +699,7 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_complete(ColList Lc, int
     }
   }
   if (threadIdx.x == 0) {
-    double m = bits_to_d(sc->dt_bits[dslot]);
+    double m = dt_get(sc, dslot);
     for (int q = 0; q < X.nranks; q++)
       if (q != X.rank) m = fmin(m, p2p_load(X.my_dtr + pp * X.nranks + q));
     sc->dt_bits[dslot] = d_to_bits(m);
@@ -703,7 +748,8 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     sc->dt_val[slot] = P.dt;
     scenario_next(P, sc, slot, slot_next);
@@ -868,7 +914,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     double m = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(m));
+    dt_min(sc, slot_next, m);
   }
 }
 
@@ -941,9 +987,10 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   apply_dt(P, sc, slot);
   const real dt_now = P.dt;
   P.dt = sc->dt_val[slot_reset(slot)];
-  const real dt_step = bits_to_d(sc->dt_bits[slot]);
+  const real dt_step = dt_get(sc, slot);
   if (b == 0 && threadIdx.x == 0) {
-    sc->dt_bits[slot_reset(slot)] = d_to_bits(1.0);
+    dt_reset(sc, slot_reset(slot));
+    sc->dt_bits[slot] = d_to_bits(dt_step);   // folded (the kinetics read the word)
     sc->time_part += dt_step;
     sc->dt_val[slot] = dt_step;
     sc->hot_cnt[slot_next] = 0;
@@ -1176,7 +1223,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
     double mn = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) mn = fmin(mn, sdt[q]);
     if (serial) mn = fmin(mn, P.dt);
-    atomicMin(&sc->dt_bits[slot_next], d_to_bits(mn));
+    dt_min(sc, slot_next, mn);
   }
   if (tr0) {
     tr[7] = rt_clock();
@@ -1230,7 +1277,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lnm_hot(StepParams P, LnmArrays a,
     double mn = sdt[0];
     for (int q = 1; q < BLOCK / WAVE; q++) mn = fmin(mn, sdt[q]);
     if (serial) mn = fmin(mn, P.dt);
-    if (mn < 1.0) atomicMin(&sc->dt_bits[slot_next], d_to_bits(mn));
+    if (mn < 1.0) dt_min(sc, slot_next, mn);
   }
 }
 
@@ -1280,18 +1327,26 @@ __global__ void hf2d_unpack(ColList L, int col, int ny, const real* buf) {
   L.f[f][(long)col * ny + j] = buf[t];
 }
 // Both sides in one launch (sides: bit 0 left, bit 1 right).
+// dt slot's shards into its word (before a host transport sends the word)
+__global__ void hf2d_dt_commit(DevScalars* sc, int slot) {
+  if (threadIdx.x == 0) sc->dt_bits[slot] = d_to_bits(dt_get(sc, slot));
+}
 // MIN of the peers' dt into this rank's slot (exchange_dt, in-process group)
 __global__ void hf2d_fold_dt(DevScalars* sc, int slot, const double* dt_recv, int nranks, int rank) {
   if (threadIdx.x != 0) return;
-  double m = bits_to_d(sc->dt_bits[slot]);
+  double m = dt_get(sc, slot);
   for (int q = 0; q < nranks; q++)
     if (q != rank) m = fmin(m, dt_recv[q]);
   sc->dt_bits[slot] = d_to_bits(m);
 }
 
-__global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, real* bufR, int sides) {
+// (dslot >= 0: also commits that dt slot's shards into its word, which the
+// host transports send)
+__global__ void hf2d_pack2(ColList L, int colL, int colR, int ny, real* bufL, real* bufR, int sides,
+                           DevScalars* sc, int dslot) {
   const int cnt = L.nf * ny;
   int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0 && dslot >= 0) sc->dt_bits[dslot] = d_to_bits(dt_get(sc, dslot));
   const bool right = t >= cnt;
   if (right) t -= cnt;
   if (t >= cnt || !(sides & (right ? 2 : 1))) return;
@@ -1305,7 +1360,7 @@ __global__ void hf2d_unpack2(ColList L, int colL, int colR, int ny, const real* 
   const int cnt = L.nf * ny;
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t == 0 && ndt > 0) {
-    double m = bits_to_d(sc->dt_bits[dslot]);
+    double m = dt_get(sc, dslot);
     for (int q = 0; q < ndt; q++)
       if (q != self) m = fmin(m, dtr[q]);
     sc->dt_bits[dslot] = d_to_bits(m);
@@ -1396,7 +1451,7 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_xchg(P2PArgs a) {
       }
     }
   }
-  const double mydt = bits_to_d(a.sc->dt_bits[a.dslot]);
+  const double mydt = dt_get(a.sc, a.dslot);
   for (int q = threadIdx.x; q < a.nranks; q += P2P_THREADS)
     if (q != a.rank) p2p_store(a.peer_dtr[q] + par * a.nranks + a.rank, mydt);
   // system-coherent stores drained (vmcnt) in every wave before the flag:
@@ -1512,6 +1567,18 @@ static const TileFxK kTileFx[2][2][3] = {
       hf2d_lean_tile_fx<true, true, true, 2>}}};
 static const TileTrK kTileTr[2][2] = {{hf2d_lean_tile_tr<false, 1>, hf2d_lean_tile_tr<false, 2>},
                                       {hf2d_lean_tile_tr<true, 1>, hf2d_lean_tile_tr<true, 2>}};
+// single gas, small workgroups: [0: 128 threads, 1: 64][cells per thread - 1][variant]
+#define HF2D_NT_ROW(K, NT, CPT) {K<false, false, NT, CPT>, K<false, true, NT, CPT>, K<true, true, NT, CPT>}
+static const TileK kTileNt[2][2][3] = {{HF2D_NT_ROW(hf2d_lean_tile_nt, 128, 1), HF2D_NT_ROW(hf2d_lean_tile_nt, 128, 2)},
+                                       {HF2D_NT_ROW(hf2d_lean_tile_nt, 64, 1), HF2D_NT_ROW(hf2d_lean_tile_nt, 64, 2)}};
+static const TileFxK kTileFxNt[2][2][3] = {
+    {HF2D_NT_ROW(hf2d_lean_tile_fx_nt, 128, 1), HF2D_NT_ROW(hf2d_lean_tile_fx_nt, 128, 2)},
+    {HF2D_NT_ROW(hf2d_lean_tile_fx_nt, 64, 1), HF2D_NT_ROW(hf2d_lean_tile_fx_nt, 64, 2)}};
+#undef HF2D_NT_ROW
+static const TileTrK kTileTrNt[2][2] = {{hf2d_lean_tile_tr_nt<128, 1>, hf2d_lean_tile_tr_nt<128, 2>},
+                                        {hf2d_lean_tile_tr_nt<64, 1>, hf2d_lean_tile_tr_nt<64, 2>}};
+// threads per workgroup of the inviscid tile kernel: 256, or 128 / 64 (single gas)
+inline int tile_nt(int want, bool sg) { return sg && (want == 128 || want == 64) ? want : BLOCK; }
 
 using LeanEulerK = void (*)(StepParams, LeanSoA, long, long, DevScalars*, int, int, int, ResidualPack*);
 // [residual][first lean step: from the generic arrays]
@@ -2195,10 +2262,13 @@ void DeviceSolver::upload() {
   cp(m.scen, &scen_host, sizeof(ScenarioTables));
   DevScalars s0{};
   const double d0 = dt;
-  std::memcpy(&s0.dt_bits[0], &d0, 8);
   const double one = 1.0;  // slot 1 accumulates step 0's min; slot 2 is reset by step 0
-  std::memcpy(&s0.dt_bits[1], &one, 8);
-  s0.dt_bits[2] = s0.dt_bits[1];
+  unsigned long long b0, b1;
+  std::memcpy(&b0, &d0, 8);
+  std::memcpy(&b1, &one, 8);
+  dt_set_host(s0, 0, b0);
+  dt_set_host(s0, 1, b1);
+  dt_set_host(s0, 2, b1);
   s0.time_part = 0.0;
   s0.iter[0] = s0.iter[1] = s0.iter[2] = (double)(last_iter + iter);
   {
@@ -2428,7 +2498,8 @@ void DeviceSolver::sync_scalars() {
   HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
   HIP_CHECK(hipStreamSynchronize(m.stream));
   const int slot = nstep % 3;
-  std::memcpy(&dt, &m.sc_host->dt_bits[slot], 8);
+  const unsigned long long db = dt_get_host(*m.sc_host, slot);
+  std::memcpy(&dt, &db, 8);
   cur_time_part = m.sc_host->time_part - time_offset;
   last_dev_time = m.sc_host->time_part;
   const int err = comm->allreduce_max_int(m.sc_host->neg_T);
@@ -2610,7 +2681,7 @@ std::string DeviceSolver::p2p_export(int rank, int nranks) {
   p.base = (char*)b;
   HIP_CHECK(hipMemset(p.base, 0, p.bytes));
   p.seq = m.mem.alloc<unsigned long long>(1);
-  p.done = m.mem.alloc<unsigned>(1);
+  p.done = m.mem.alloc<unsigned>((DT_SHARDS + 1) * FX_DONE_STRIDE);
   HIP_CHECK(hipDeviceSynchronize());
   P2PDesc d{};
   d.magic = P2P_MAGIC;
@@ -2858,9 +2929,9 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     HIP_CHECK(hipGetLastError());
     return;
   }
-  hipLaunchKernelGGL(hf2d_pack2, dim3(nb2), dim3(BLOCK), 0, st, L, first, last, ny, m.halo_send[0],
-                     m.halo_send[1], sides);
   const bool gather_dt = dt_slot >= 0;
+  hipLaunchKernelGGL(hf2d_pack2, dim3(std::max(nb2, 1u)), dim3(BLOCK), 0, st, L, first, last, ny, m.halo_send[0],
+                     m.halo_send[1], sides, m.sc, gather_dt ? dt_slot : -1);
   unsigned long long* my_dt = gather_dt ? &m.sc->dt_bits[dt_slot] : nullptr;
   if (m.local) {
     LocalGroup& g = *m.local;
@@ -2946,7 +3017,10 @@ std::string DeviceSolver::p2p_probe() {
     std::memcpy(&b, &d, sizeof b);
     return b;
   }();
-  HIP_CHECK(hipMemcpyAsync(&m.sc->dt_bits[0], &tag, sizeof tag, hipMemcpyHostToDevice, st));
+  DevScalars tagged = saved;
+  dt_set_host(tagged, 0, tag);
+  HIP_CHECK(hipMemcpyAsync(m.sc, &tagged, sizeof tagged, hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));
   exchange(CpuSolver::HALO_STATE, 0);
   auto column = [&](int col) {
     std::vector<real> v(fl.size() * (size_t)ny);
@@ -2976,7 +3050,8 @@ std::string DeviceSolver::p2p_probe() {
   b.sent_r = has_right ? fnv1a(sr) : 0;
   b.recv_l = has_left ? fnv1a(rl) : 0;
   b.recv_r = has_right ? fnv1a(rr) : 0;
-  std::memcpy(&b.dt, &after.dt_bits[0], sizeof b.dt);
+  const unsigned long long adt = dt_get_host(after, 0);
+  std::memcpy(&b.dt, &adt, sizeof b.dt);
   return std::string((const char*)&b, sizeof b);
 }
 
@@ -3019,6 +3094,8 @@ void DeviceSolver::exchange_dt(int dt_slot) {
   Impl& m = *impl;
   if (m.nranks <= 1) return;
   unsigned long long* my_dt = &m.sc->dt_bits[dt_slot];
+  hipLaunchKernelGGL(hf2d_dt_commit, dim3(1), dim3(64), 0, m.stream, m.sc, dt_slot);
+  HIP_CHECK(hipGetLastError());
   if (m.comm) {
     NCCL_CHECK(ncclAllReduce(my_dt, my_dt, 1, ncclUint64, ncclMin, m.comm, m.stream));
     return;
@@ -3122,7 +3199,7 @@ void DeviceSolver::flush_pending() {
 
 uint64_t DeviceSolver::mode_signature() const {
   const int fields[] = {lean_state, (int)lean, (int)fused, (int)lean_tile, (int)(lean_sg && lean_sg_ok), lean_cpt,
-                        lean_tj, lean_wgcu, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok), lns_state,
+                        lean_tj, lean_nt, lean_wgcu, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok), lns_state,
                         (int)lean_ns, (int)lean_mech};
   uint64_t h = 0;
   for (int f : fields) h = h * 1000003ull + (uint64_t)(f + 1);
@@ -3411,6 +3488,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   const bool euler = P.sm != SM_NS;
   hipStream_t st = m.stream;
   unsigned nres = nblk;   // workgroups that wrote residual partials
+  int nres_waves = BLOCK / WAVE;   // ... and partials per workgroup
   const bool sg_now = lean_sg && lean_sg_ok;
   fx_step = false;
   const bool tile_path = euler && lean && lean_ok && lean_tile &&
@@ -3420,14 +3498,17 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
     // two cells per thread unless that leaves fewer than ~2 workgroups per CU
     // (small strips of a multi-GPU run)
+    // (256-thread tiles only: the small-workgroup geometries are explicit
+    // choices of the autotune)
+    const bool sg = lean_sg && lean_sg_ok;
+    const int nt = tile_nt(lean_nt, sg), nts = nt == 128 ? 0 : 1;
     int cpt = lean_cpt == 2 ? 2 : 1;
-    if (cpt == 2) {
+    if (cpt == 2 && nt == BLOCK) {
       const LeanTile T2 = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, 2);
       if ((long)T2.nbi * T2.nbj < 2L * cu_count) cpt = 1;
     }
-    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj, cpt);
+    const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, nt, lean_tj, cpt);
     const unsigned ntile = (unsigned)(T.nbi * T.nbj);
-    const bool sg = lean_sg && lean_sg_ok;
     size_t shmem = (size_t)lean_tile_fields(sg) * T.NC * sizeof(real);
     if (lean_wgcu > 0)   // cap the resident workgroups per CU through the LDS request (160 KB per CU)
       shmem = std::max(shmem, (size_t)((LDS_PER_CU / lean_wgcu - 1024) & ~255));
@@ -3436,7 +3517,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     // rounds: measured 1.5 us faster on the headline grid; the 4000x1000 triple
     // point, dispatched in ~15 waves, ran 350 -> 550 us with it)
     P.stagger_wgs = cu_count > 0 ? cu_count : 256;
-    P.stagger = ntile <= 4u * (unsigned)P.stagger_wgs ? tile_stagger : 0;
+    P.stagger = ntile <= 4u * (unsigned)P.stagger_wgs && nt == BLOCK ? tile_stagger : 0;
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
@@ -3454,8 +3535,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       }
       const bool parts = T.nbi >= 3;
       const unsigned ne = parts ? (unsigned)(2 * T.nbj) : ntile, ni = parts ? (unsigned)((T.nbi - 2) * T.nbj) : 0u;
-      const TileK pk = kTile[sg][cpt - 1][0];
-      hipLaunchKernelGGL(pk, dim3(ne), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
+      const TileK pk = nt == BLOCK ? kTile[sg][cpt - 1][0] : kTileNt[nts][cpt - 1][0];
+      hipLaunchKernelGGL(pk, dim3(ne), dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
                          parts ? 1 : 0);
       HIP_CHECK(hipGetLastError());
       sbuf = 1 - sbuf;   // the new state is this step's output arrays
@@ -3465,7 +3546,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // interior tiles in flight before the (possibly host-blocking) exchange
       // is issued; they write neither the edge columns nor the ghost columns
       if (ni > 0)
-        hipLaunchKernelGGL(pk, dim3(ni), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
+        hipLaunchKernelGGL(pk, dim3(ni), dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials,
                            2);
       HIP_CHECK(hipGetLastError());
       if (m.local) {
@@ -3493,11 +3574,14 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     // the cpt the tile geometry was built for)
     const int var = want_res ? 2 : out ? 1 : 0;
     if (tile_trace && var == 0 && !fx_step)
-      hipLaunchKernelGGL(kTileTr[sg][cpt - 1], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot, slot_next,
-                         serial, m.partials, tile_trace);
+      hipLaunchKernelGGL(nt == BLOCK ? kTileTr[sg][cpt - 1] : kTileTrNt[nts][cpt - 1], dim3(ntile), dim3(nt), shmem,
+                         st, P, L, T, m.sc, slot, slot_next, serial, m.partials, tile_trace);
     else if (fx_step)
-      hipLaunchKernelGGL(kTileFx[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
-                         slot_next, serial, m.partials, X);
+      hipLaunchKernelGGL(nt == BLOCK ? kTileFx[sg][cpt - 1][var] : kTileFxNt[nts][cpt - 1][var], dim3(ntile),
+                         dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials, X);
+    else if (nt != BLOCK)
+      hipLaunchKernelGGL(kTileNt[nts][cpt - 1][var], dim3(ntile), dim3(nt), shmem, st, P, L, T, m.sc, slot,
+                         slot_next, serial, m.partials, 0);
     else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace)
       hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                          m.sc, slot, slot_next, serial, m.partials);
@@ -3506,6 +3590,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
                          slot_next, serial, m.partials, 0);
     HIP_CHECK(hipGetLastError());
     nres = ntile;
+    nres_waves = nt / WAVE;
     sbuf = 1 - sbuf;
     dsbuf = 1 - dsbuf;
     pbuf = 1 - pbuf;
@@ -3639,7 +3724,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   r.async = true;
   if (want_res) {
     hipLaunchKernelGGL(hf2d_reduce_residual, dim3(1), dim3(BLOCK), 0, st, m.partials,
-                       (long)nres * (BLOCK / WAVE), m.res_out);
+                       (long)nres * nres_waves, m.res_out);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(m.res_host, m.res_out, sizeof(ResidualPack), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
@@ -3729,7 +3814,7 @@ std::vector<unsigned long long> DeviceSolver::trace_tile(int steps) {
   use_graph = false;
   if (steps > 0) run_steps(steps);
   const int cpt = lean_cpt == 2 ? 2 : 1;
-  const LeanTile T = lean_tile_geom(gi1 - gi0, h.ny, BLOCK, lean_tj, cpt);
+  const LeanTile T = lean_tile_geom(gi1 - gi0, h.ny, tile_nt(lean_nt, lean_sg && lean_sg_ok), lean_tj, cpt);
   const long n = (long)T.nbi * T.nbj * TILE_TRACE_WORDS * 2;   // room for either cpt
   tile_trace = impl->mem.alloc<unsigned long long>(n);
   try {
@@ -3764,16 +3849,23 @@ std::string DeviceSolver::autotune(int steps) {
   const ResidualSummary s_res = last_res;
   const bool s_resv = last_res_valid;
   struct Cand {
-    int cpt, tj;
+    int cpt, tj, nt;
   };
   std::vector<Cand> cands;
   for (int cpt : {2, 1}) {
     if (ns && cpt == 2) continue;
     for (int tj : {0, 10, 12, 14, 16, 20, 25, 32, 40, 50, 64})
-      if ((tj == 0 || tj <= h.ny) && (ns ? tj <= 40 : (tj == 0 || tj >= 16))) cands.push_back({cpt, tj});
+      if ((tj == 0 || tj <= h.ny) && (ns ? tj <= 40 : (tj == 0 || tj >= 16))) cands.push_back({cpt, tj, BLOCK});
   }
+  // small workgroups (single-gas inviscid): the geometries of the narrow
+  // strips of a multi-GPU run, where 256-thread tiles leave CUs idle
+  if (!ns && lean_sg && lean_sg_ok)
+    for (int nt : {128, 64})
+      for (int cpt : {1, 2})
+        for (int tj : {0, 8, 16, 32, 64})
+          if (tj <= nt && (tj == 0 || tj <= h.ny)) cands.push_back({cpt, tj, nt});
   double best = 1e30;
-  Cand win{lean_cpt, lean_tj};
+  Cand win{lean_cpt, lean_tj, lean_nt};
   char b[160];
   std::string log;
   // same work per candidate whatever the grid (~50 M cell-steps): big grids get fewer steps
@@ -3782,6 +3874,7 @@ std::string DeviceSolver::autotune(int steps) {
   for (const Cand& c : cands) {
     lean_cpt = c.cpt;
     lean_tj = c.tj;
+    lean_nt = c.nt;
     graph.reset();   // the state just keeps marching; it is restored once at the end
     double us = 1e30;
     try {
@@ -3797,7 +3890,10 @@ std::string DeviceSolver::autotune(int steps) {
       log += std::string("stopped: ") + e.what() + "; ";
       break;
     }
-    std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
+    if (c.nt == BLOCK)
+      std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
+    else
+      std::snprintf(b, sizeof b, "nt=%d cpt=%d tj=%d %.2f us; ", c.nt, c.cpt, c.tj, us);
     log += b;
     if (us < best) {
       best = us;
@@ -3806,6 +3902,7 @@ std::string DeviceSolver::autotune(int steps) {
   }
   lean_cpt = win.cpt;
   lean_tj = win.tj;
+  lean_nt = win.nt;
   graph.reset();
   dt = s_dt;
   dt_running = s_dtr;
@@ -3821,7 +3918,7 @@ std::string DeviceSolver::autotune(int steps) {
   upload();   // device scalars from the restored host state
   graph_launches = 0;
   lns_steps = lnm_steps = 0;   // (the tuning steps do not count as the run's)
-  std::snprintf(b, sizeof b, "best cpt=%d tj=%d (%.2f us/step)", win.cpt, win.tj, best);
+  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d (%.2f us/step)", win.nt, win.cpt, win.tj, best);
   return log + b;
 }
 

@@ -143,6 +143,7 @@ class DeviceSolver : public SolverBase {
   int lean_wgcu = 0;       // >0: at most this many tile workgroups resident per CU (LDS request)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
   int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
+  int lean_nt = 256;       // threads per tile workgroup: 256, or 128 / 64 (single gas; small strips)
   int cu_count = 256;
   bool lean_sg_ok = false;
   bool lean_has_cauchy_x = true;   // some node reads dS/dx of an x neighbour (halo must carry it)

@@ -96,6 +96,26 @@ def test_euler_gpu_equals_reference_order(gpu):
         assert _rel(g.field(f), r.field(f)) < 1e-12, f
 
 
+@pytest.mark.parametrize("nt,cpt,tj", [(128, 1, 0), (128, 2, 16), (64, 1, 16), (64, 2, 8), (64, 1, 64)])
+def test_small_workgroup_tiles_bitwise(gpu, nt, cpt, tj):
+    """The small-strip tile geometries (64 / 128-thread workgroups, one or two
+    cells per thread) == the 256-thread tile kernel bit for bit: fields, dt,
+    time (residual sums: reduced over other partials)."""
+    text = decks.wedge15(250, 200, nmax=10 ** 6, nout=10 ** 5)
+    ref = gpu.Simulation(text, "gpu")
+    s = gpu.Simulation(text, "gpu")
+    ref.solver.lean_nt, ref.solver.lean_cpt, ref.solver.lean_tj = 256, 2, 0
+    s.solver.lean_nt, s.solver.lean_cpt, s.solver.lean_tj = nt, cpt, tj
+    for n, res in [(5, True), (30, False), (7, True)]:
+        s.step(n, residual=res)
+        ref.step(n, residual=res)
+        assert s.summary()["dt"] == ref.summary()["dt"]
+    assert s.summary()["time"] == ref.summary()["time"]
+    np.testing.assert_allclose(s.summary()["rms"], ref.summary()["rms"], rtol=1e-12, atol=0)
+    for f in FIELDS + ["k", "R", "CP"]:
+        np.testing.assert_array_equal(s.field(f), ref.field(f), err_msg=f)
+
+
 def test_lean_bitwise_with_switches(gpu):
     """Lean GPU steps interleaved with downloads and generic steps stay
     bit-identical to the generic CPU stepper (dt, residuals, fields)."""
@@ -347,10 +367,11 @@ def test_comm_overlap_split_step_matches_single_gpu(gpu):
 # <= 3 in-process ranks: their streams must land on distinct hardware queues
 # (GPU_MAX_HW_QUEUES=4) or a spinning exchange could sit in front of the step
 # it waits for; separate processes (the real deployment) have no such limit.
-@pytest.mark.parametrize("nranks,physics,lean,fuse", [(2, "euler", True, False), (3, "euler", True, False),
-                                                      (3, "kes", False, True), (2, "euler", True, True),
-                                                      (3, "euler", True, True), (3, "euler", True, "toggle")])
-def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse):
+@pytest.mark.parametrize("nranks,physics,lean,fuse,nt", [(2, "euler", True, False, 256), (3, "euler", True, False, 256),
+                                                         (3, "kes", False, True, 256), (2, "euler", True, True, 256),
+                                                         (3, "euler", True, True, 256), (3, "euler", True, "toggle", 256),
+                                                         (3, "euler", True, True, 64), (2, "euler", True, True, 128)])
+def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse, nt):
     """xGMI mailbox transport (hf2d_p2p_xchg: direct peer stores, system-scope
     flags, device-side dt MIN; fuse: the same exchange folded into the lean
     tile kernel, hf2d_lean_tile_fx + hf2d_p2p_complete) inside captured step
@@ -359,8 +380,11 @@ def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse):
     ns = physics != "euler"
     text = decks.wedge15(240, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
     schedule = [(5, True), (30, False), (7, True), (25, False)]
+    def setup(s):
+        s.lean_nt = nt
+
     got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=lean, p2p=True, fuse=fuse is True,
-                               toggle=fuse == "toggle")
+                               toggle=fuse == "toggle", setup=setup)
     ref = gpu.Simulation(text, "gpu", lean=lean)
     for n, res in schedule:
         ref.step(n, residual=res)
@@ -605,7 +629,7 @@ def test_autotune_thread_block_size_zero(gpu, monkeypatch):
     geometries on the device before the first step; the run is unchanged."""
     text = decks.wedge15(300, 60, nmax=10 ** 6, nout=10 ** 5)
     a = gpu.Simulation(text, "gpu")
-    assert "best cpt=" in a.autotune_log, a.autotune_log
+    assert "best nt=" in a.autotune_log and "nt=64 cpt=1" in a.autotune_log, a.autotune_log
     monkeypatch.setenv("HF2D_AUTOTUNE", "0")
     b = gpu.Simulation(text, "gpu")
     assert b.autotune_log == ""
@@ -626,7 +650,7 @@ def test_autotune_lean_ns_tile_height(gpu, monkeypatch, deck):
     text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5) if deck == "step" else \
         decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
     a = gpu.Simulation(text, "gpu")
-    assert "best cpt=1 tj=" in a.autotune_log, a.autotune_log
+    assert "best nt=256 cpt=1 tj=" in a.autotune_log, a.autotune_log
     assert a.solver.lns_steps == 0
     monkeypatch.setenv("HF2D_AUTOTUNE", "0")
     b = gpu.Simulation(text, "gpu")

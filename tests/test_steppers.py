@@ -27,9 +27,12 @@ def _records_wo_scratch(sim):
 
 
 @pytest.mark.parametrize("name", list(_decks()))
-@pytest.mark.parametrize("tile,sg,cpt,tj", [(False, False, 1, 0), (True, False, 1, 0), (True, True, 1, 0),
-                                           (True, True, 2, 0), (True, False, 2, 11)])
-def test_lean_equals_generic(hf, name, tile, sg, cpt, tj):
+@pytest.mark.parametrize("tile,sg,cpt,tj,nt", [(False, False, 1, 0, 256), (True, False, 1, 0, 256),
+                                              (True, True, 1, 0, 256), (True, True, 2, 0, 256),
+                                              (True, False, 2, 11, 256), (True, True, 1, 16, 64),
+                                              (True, True, 2, 0, 128), (True, True, 2, 32, 64)])
+def test_lean_equals_generic(hf, name, tile, sg, cpt, tj, nt):
+    """nt: threads per emulated tile workgroup (the small-strip geometries)."""
     text = _decks()[name]
     a = hf.Simulation(text, "cpu", lean=False)
     b = hf.Simulation(text, "cpu", lean=True)
@@ -37,6 +40,7 @@ def test_lean_equals_generic(hf, name, tile, sg, cpt, tj):
     b.solver.lean_sg = sg
     b.solver.lean_cpt = cpt
     b.solver.lean_tj = tj
+    b.solver.lean_nt = nt
     assert b.solver.lean_ok, b.solver.lean_why
     assert b.solver.lean_sg_ok
     for s in range(3):

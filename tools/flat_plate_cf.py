@@ -27,7 +27,7 @@ ap.add_argument("--cfl", type=float, default=None, help="constant CFL (default: 
 ap.add_argument("--beta0", type=float, default=None, help="DEEPS blending factor beta0 (deck default 0.9875)")
 ap.add_argument("--bff", type=int, default=None, help="blending-factor function (deck default 4)")
 ap.add_argument("--max-steps", type=int, default=10 ** 9)
-ap.add_argument("--sst-d1", type=float, default=None, help="SSTWallDistance (wall omega distance / dy; deck default 0.5)")
+ap.add_argument("--sst-d1", type=float, default=None, help="SSTWallDistance (wall omega distance / dy; default 1.0, the Menter first-cell distance)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 

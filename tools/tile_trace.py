@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--cpt", type=int, default=0)
     ap.add_argument("--tj", type=int, default=-1)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--nt", type=int, default=256, help="threads per workgroup (256, 128, 64)")
     a = ap.parse_args()
     os.environ.setdefault("HF2D_AUTOTUNE", "0")
     import openhyperflow2d_amd as hf
@@ -39,7 +40,8 @@ def main():
         s.lean_cpt = a.cpt
     if a.tj >= 0:
         s.lean_tj = a.tj
-    print("grid %dx%d cpt=%d tj=%d" % (a.nx, a.ny, s.lean_cpt, s.lean_tj))
+    s.lean_nt = a.nt
+    print("grid %dx%d nt=%d cpt=%d tj=%d" % (a.nx, a.ny, s.lean_nt, s.lean_cpt, s.lean_tj))
     for rep in range(a.reps):
         t = np.asarray(s.trace_tile(20), dtype=np.uint64).reshape(-1, 8)
         t = t[t[:, 0] > 0]
