@@ -3849,7 +3849,7 @@ std::string DeviceSolver::autotune(int steps) {
   const ResidualSummary s_res = last_res;
   const bool s_resv = last_res_valid;
   struct Cand {
-    int cpt, tj, nt;
+    int cpt, tj, nt, wgcu = 0;
   };
   std::vector<Cand> cands;
   for (int cpt : {2, 1}) {
@@ -3865,16 +3865,23 @@ std::string DeviceSolver::autotune(int steps) {
         for (int tj : {0, 8, 16, 32, 64})
           if (tj <= nt && (tj == 0 || tj <= h.ny)) cands.push_back({cpt, tj, nt});
   double best = 1e30;
-  Cand win{lean_cpt, lean_tj, lean_nt};
+  Cand win{lean_cpt, lean_tj, lean_nt, lean_wgcu};
   char b[160];
   std::string log;
   // same work per candidate whatever the grid (~50 M cell-steps): big grids get fewer steps
   const long cells = std::max(1L, (long)(gi1 - gi0) * h.ny);
   steps = (int)std::max(12L, std::min((long)steps, 50000000L / cells));
-  for (const Cand& c : cands) {
+  // second stage (inviscid): resident workgroups per CU for the winning
+  // geometry (through the LDS request).  Fewer resident workgroups than
+  // tiles make later dispatch rounds stage their tiles while earlier ones
+  // compute instead of every workgroup loading, then computing, at once.
+  bool stage2 = ns;
+  for (size_t ci = 0; ci < cands.size(); ci++) {
+    const Cand c = cands[ci];
     lean_cpt = c.cpt;
     lean_tj = c.tj;
     lean_nt = c.nt;
+    lean_wgcu = c.wgcu;
     graph.reset();   // the state just keeps marching; it is restored once at the end
     double us = 1e30;
     try {
@@ -3890,7 +3897,9 @@ std::string DeviceSolver::autotune(int steps) {
       log += std::string("stopped: ") + e.what() + "; ";
       break;
     }
-    if (c.nt == BLOCK)
+    if (c.wgcu)
+      std::snprintf(b, sizeof b, "wgcu=%d %.2f us; ", c.wgcu, us);
+    else if (c.nt == BLOCK)
       std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
     else
       std::snprintf(b, sizeof b, "nt=%d cpt=%d tj=%d %.2f us; ", c.nt, c.cpt, c.tj, us);
@@ -3899,10 +3908,20 @@ std::string DeviceSolver::autotune(int steps) {
       best = us;
       win = c;
     }
+    if (!stage2 && ci + 1 == cands.size()) {
+      stage2 = true;
+      for (int w : {2, 3, 4, 6, 8, 12, 16}) {
+        if (w * (win.nt / WAVE) > 32) break;   // (32 waves per CU)
+        Cand c2 = win;
+        c2.wgcu = w;
+        cands.push_back(c2);
+      }
+    }
   }
   lean_cpt = win.cpt;
   lean_tj = win.tj;
   lean_nt = win.nt;
+  lean_wgcu = win.wgcu;
   graph.reset();
   dt = s_dt;
   dt_running = s_dtr;
@@ -3918,7 +3937,8 @@ std::string DeviceSolver::autotune(int steps) {
   upload();   // device scalars from the restored host state
   graph_launches = 0;
   lns_steps = lnm_steps = 0;   // (the tuning steps do not count as the run's)
-  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d (%.2f us/step)", win.nt, win.cpt, win.tj, best);
+  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d wgcu=%d (%.2f us/step)", win.nt, win.cpt, win.tj, win.wgcu,
+                best);
   return log + b;
 }
 
