@@ -126,6 +126,24 @@ def cases():
         # the Integral turbulence model (TurbulenceModel = 1: Re_local only,
         # hyper_flow_node.hpp:921-924)
         "integral_model": _wedge(turb=1),
+        # round 4: forces on an airfoil.  The reference's airfoil only exists
+        # at attack_angle = 0 (RotateBoundContour2D compares node coordinates
+        # against an unset Bound2D::dx and fails), and Calc_Cx_2D /
+        # CalcXForce2D (out_cfd_param.cpp:256-496) count only no-slip /
+        # wall-law nodes, which an N-S deck gives the airfoil contour: a
+        # cambered NACA section in the turbulent wedge with non-zero Cx, Cy,
+        # Fx, Fy after 30 steps
+        "naca_airfoil_ns": _wedge(turb=4, NumAirfoils=1, Airfoil1__Xstart=0.02, Airfoil1__Ystart=0.026,
+                                  Airfoil1__Type=0, Airfoil1__pp=0.4, Airfoil1__mm=0.2, Airfoil1__thick=0.12,
+                                  Airfoil1__scale=0.04, Airfoil1__attack_angle=0.0, Airfoil1__Flow2D=1,
+                                  Airfoil1__TurbulenceModel=0, is_Cx_calc=1, x_body=0.015, y_body=0.015,
+                                  dx_body=0.05, dy_body=0.02, Cx_Flow_Index=1),
+        # wall-law nodes that stay bounded: the no-slip plate of the flat-plate
+        # deck (k-eps, M = 0.8) as NT_WALL_LAW_2D, 60 steps
+        # (hyper_flow_node.hpp:447 ff; the velocity projection onto BGX/BGY)
+        "wall_law_plate": _finite(decks.set_key(decks.flat_plate(120, 40, mach=0.8, p=1.0e5, turbulence=4),
+                                                "Contour1.Bound3.Cond", "NT_WALL_LAW_2D, TCT_eps_Cmk2kXn_WALL_2D"),
+                                  60, 20),
     }
 
 
