@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <iostream>
 #include <sstream>
 
 #include "../core/case.hpp"
@@ -325,7 +326,59 @@ PYBIND11_MODULE(_hf2d, m) {
              c.write_strip_payload(off, (const char*)bi.ptr, (size_t)bi.size * (size_t)bi.itemsize);
            })
       .def("compute_facts", &Case::compute_facts)
+      .def_static(
+          "from_deck_window",
+          [](const std::string& text, const std::string& workdir, bool use_checkpoint, int a, int b, bool verbose) {
+            InputDeck d = InputDeck::from_string(text);
+            py::gil_scoped_release nogil;
+            return std::make_shared<Case>(
+                Case::from_deck_window(d, workdir, use_checkpoint, a, b, verbose ? &std::cout : nullptr));
+          },
+          py::arg("text"), py::arg("workdir") = ".", py::arg("use_checkpoint") = false, py::arg("a") = 0,
+          py::arg("b") = 0, py::arg("verbose") = false,
+          "strip-local pre-processing: records of the columns [a, b) only (whole-grid flags in 16 B/cell while it "
+          "runs; a restart reads this slab of the .hf2d); facts valid after merge_facts")
+      .def_static(
+          "partition_deck",
+          [](const std::string& text, const std::string& workdir, bool use_checkpoint, int nparts) {
+            InputDeck d = InputDeck::from_string(text);
+            py::gil_scoped_release nogil;
+            return Case::partition_deck(d, workdir, use_checkpoint, nparts);
+          },
+          py::arg("text"), py::arg("workdir") = ".", py::arg("use_checkpoint") = false, py::arg("nparts") = 1,
+          "active-cell-balanced strips of a deck from a flags-only pre-processing pass (16 B/cell)")
+      .def("facts_part", [](const Case& c) { return py::bytes(c.facts_part().pack()); },
+           "the cell-level eligibility facts of this Case's resident records (Case.merge_facts)")
+      .def("merge_facts",
+           [](Case& c, const std::vector<std::string>& parts) {
+             std::vector<FactsPart> v;
+             for (const auto& p : parts) v.push_back(FactsPart::unpack(p));
+             c.merge_facts(v);
+           },
+           py::arg("parts"), "whole-field facts from every strip's facts_part, in rank order")
       .def_property_readonly("facts_valid", [](const Case& c) { return c.facts.valid; })
+      .def_property_readonly("facts",
+                             [](const Case& c) {
+                               if (!c.facts.valid) throw std::runtime_error("facts not computed / merged");
+                               py::dict d;
+                               d["lean_ok"] = c.facts.lean_ok;
+                               d["lean_why"] = c.facts.lean_why;
+                               d["sk_mode"] = c.facts.sk_mode;
+                               d["sk_why"] = c.facts.sk_why;
+                               d["single_gas"] = c.facts.single_gas;
+                               d["any_cauchy_x"] = c.facts.any_cauchy_x;
+                               d["species_cauchy"] = c.facts.species_cauchy;
+                               return d;
+                             })
+      .def("resident_records",
+           [](const Case& c) { return py::bytes((const char*)c.J.c.data(), c.J.c.size() * sizeof(CellRecord)); },
+           "the 1248-byte records of the resident columns (x-major)")
+      .def("resident_species",
+           [](const Case& c) {
+             return py::array_t<double>((py::ssize_t)c.mech_rhoY.size(), c.mech_rhoY.data());
+           },
+           "mechanism mode: the species partial densities of the resident columns, species-major")
+      .def_property_readonly("subdomains", [](const Case& c) { return c.subdomains; })
       .def("trim_to_columns", &Case::trim_to_columns, py::arg("a"), py::arg("b"),
            "strip rank: keep only columns [a, b) of the host field resident (after the solver uploaded its strip)")
       .def_property_readonly("resident_columns", [](const Case& c) { return py::make_tuple(c.J.i0, c.J.i0 + c.J.nxl); })

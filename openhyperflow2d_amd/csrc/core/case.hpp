@@ -102,19 +102,44 @@ struct Config {
 // A strip rank keeps only the columns [i0, i0 + nxl) resident (its strip plus
 // one ghost column each side, Field::trim); nx stays the global width and
 // at() takes global column indices.
+//
+// Windowed pre-processing (Case::from_deck_window): a strip rank builds the
+// records of its resident columns only, while the geometry steps -- bounds,
+// contours, flood fills, wall / NRBC tagging -- run over the whole grid on a
+// 16 B/cell plane of the two flag words (CT, TurbType) of the non-resident
+// cells.  ct() / tt() / is() address either, so every geometry step sees the
+// whole grid's flags and every state write lands only in resident records.
+struct CellFlags {
+  u64 CT = 0, TurbType = 0;
+};
 struct Field {
   int nx = 0, ny = 0;
   int i0 = 0, nxl = 0;   // resident columns
   std::vector<CellRecord> c;
+  std::vector<CellFlags> g;   // windowed pre-processing: flags of every cell (empty otherwise)
   void resize(int X, int Y);
+  // records of the columns [a, b) only, plus the whole grid's flag plane
+  void resize_window(int X, int Y, int a, int b);
   CellRecord& at(int i, int j) { return c[(size_t)(i - i0) * ny + j]; }
   const CellRecord& at(int i, int j) const { return c[(size_t)(i - i0) * ny + j]; }
   bool in(long i, long j) const { return i >= 0 && j >= 0 && i < nx && j < ny; }
   bool resident(long i) const { return i >= i0 && i < i0 + nxl; }
   bool whole() const { return i0 == 0 && nxl == nx; }
+  bool windowed() const { return !g.empty(); }
+  u64& ct(int i, int j) { return resident(i) ? at(i, j).CT : g[(size_t)i * ny + j].CT; }
+  u64 ct(int i, int j) const { return resident(i) ? at(i, j).CT : g[(size_t)i * ny + j].CT; }
+  u64& tt(int i, int j) { return resident(i) ? at(i, j).TurbType : g[(size_t)i * ny + j].TurbType; }
+  u64 tt(int i, int j) const { return resident(i) ? at(i, j).TurbType : g[(size_t)i * ny + j].TurbType; }
+  bool is(int i, int j, u64 mask) const { return (ct(i, j) & mask) == mask; }
+  void drop_flags() { std::vector<CellFlags>().swap(g); }
   // drop every column outside [a, b) (global indices, clipped to the grid)
   void trim(int a, int b);
 };
+
+// [gi0, gi1) per rank with about equal active (non-solid) cells per strip:
+// the same cut as parallel/strips.py balanced_columns (flags only: works on
+// a windowed field's flag plane)
+std::vector<std::pair<int, int>> balanced_columns(const Field& J, int nparts);
 
 // Whole-field eligibility of the specialised steppers (lean.cpp), evaluated
 // on the full pre-processed field: a strip rank that never held it
@@ -126,6 +151,20 @@ struct CaseFacts {
   int sk_mode = 0;
   std::string sk_why;
   bool single_gas = false, any_cauchy_x = false, species_cauchy = false;
+};
+// The cell-level part of the facts over the resident records of one strip
+// (lean.cpp facts_part); facts_merge folds the parts of all strips, in rank
+// (= column) order, with the deck-level conditions into the whole field's
+// facts -- the same answer, reasons included, as one pass over the whole field.
+struct FactsPart {
+  bool single_gas = true, any_cauchy_x = false, species_cauchy = false;
+  bool lean_cells_ok = true;   // first failing cell's reason otherwise
+  std::string lean_why;
+  bool sk_cells_ok = true;
+  std::string sk_why;
+  bool laminar = true;
+  std::string pack() const;
+  static FactsPart unpack(const std::string& b);
 };
 
 class Case {
@@ -172,6 +211,19 @@ class Case {
   // looked up; checkpoint=false ignores any existing swap file.
   static Case from_deck(InputDeck deck, const std::string& workdir = ".", bool use_checkpoint = true,
                         std::ostream* log = nullptr);
+  // Strip-local pre-processing (no whole-field copy anywhere):
+  // the same pre-processor with records for the columns [a, b) only and the
+  // whole grid's flags in a 16 B/cell plane; a checkpoint restart reads the
+  // rank's own slab of the .hf2d (plus the flag words of the rest).  The
+  // facts are not valid until merge_facts() got every strip's facts_part().
+  static Case from_deck_window(InputDeck deck, const std::string& workdir, bool use_checkpoint, int a, int b,
+                               std::ostream* log = nullptr);
+  // The active-cell-balanced strips of a deck from a flags-only pass (no
+  // records at all): what every rank computes before its windowed pass.
+  static std::vector<std::pair<int, int>> partition_deck(InputDeck deck, const std::string& workdir,
+                                                         bool use_checkpoint, int nparts);
+  FactsPart facts_part() const;
+  void merge_facts(const std::vector<FactsPart>& parts);
 
   // Individual pre-processing steps (public for tests).
   void fill_node(CellRecord& n, int is_mu_t, int is_init) const;
@@ -193,6 +245,12 @@ class Case {
   void refresh_mechanism_primitives();
 
  private:
+  int win_a = -1, win_b = -1;   // windowed pre-processing: resident columns (-1: the whole grid)
+  // record (i, j) as the geometry steps left it: resident, or read from the
+  // preloaded checkpoint (windowed restart), or nullptr
+  const CellRecord* far_record(int i, int j);
+  std::vector<std::pair<long, CellRecord>> far_cache;
+  void load_and_preprocess(InputDeck& deck, const std::string& workdir, bool use_checkpoint, bool flags_only = false);
   void preprocess(InputDeck& d, const std::string& workdir, bool use_checkpoint);
 };
 

@@ -183,14 +183,7 @@ std::vector<std::pair<int, int>> pairs_of(const std::vector<int>& f) {
 
 void Case::compute_facts() {
   if (!J.whole()) throw std::runtime_error("Case::compute_facts needs the whole field");
-  CaseFacts f;
-  f.lean_ok = lean_eligible(*this, &f.lean_why);
-  f.sk_mode = sk_eligible(*this, &f.sk_why);
-  f.single_gas = lean_single_gas(*this);
-  f.any_cauchy_x = lean_any_cauchy_x(*this);
-  f.species_cauchy = mech_species_cauchy(*this);
-  f.valid = true;
-  facts = f;
+  merge_facts({facts_part()});
 }
 
 std::string Case::pack_strip_header(int a, int b) const {

@@ -53,6 +53,45 @@ bool read_hf2d(const std::string& path, Field& J) {
   return ok;
 }
 
+bool read_hf2d_window(const std::string& path, Field& J) {
+  if (!J.windowed()) throw std::runtime_error("read_hf2d_window: not a windowed field");
+  struct stat st;
+  if (::stat(path.c_str(), &st) != 0) return false;
+  const size_t rec = sizeof(CellRecord), want = (size_t)J.nx * J.ny * rec;
+  if ((size_t)st.st_size != want) return false;
+  int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  // the rank's own slab: contiguous x-major columns [i0, i0 + nxl)
+  bool ok = J.c.empty() || pread_all(fd, J.c.data(), J.c.size() * rec, (off_t)((size_t)J.i0 * J.ny * rec));
+  // the flag words of every other column, streamed in ~8 MB blocks of whole columns
+  const int per = std::max(1, (int)((8u << 20) / (rec * (size_t)J.ny)));
+  std::vector<CellRecord> blk;
+  for (int a = 0; ok && a < J.nx; a += per) {
+    const int b = std::min(J.nx, a + per);
+    if (a >= J.i0 && b <= J.i0 + J.nxl) continue;
+    blk.resize((size_t)(b - a) * J.ny);
+    ok = pread_all(fd, blk.data(), blk.size() * rec, (off_t)((size_t)a * J.ny * rec));
+    for (int i = a; ok && i < b; i++) {
+      if (J.resident(i)) continue;
+      for (int j = 0; j < J.ny; j++) {
+        const CellRecord& c = blk[(size_t)(i - a) * J.ny + j];
+        J.g[(size_t)i * J.ny + j] = CellFlags{c.CT, c.TurbType};
+      }
+    }
+  }
+  ::close(fd);
+  return ok;
+}
+
+bool read_hf2d_record(const std::string& path, int nx, int ny, int i, int j, CellRecord& out) {
+  if (!checkpoint_image_present(path, nx, ny)) return false;
+  int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  const bool ok = pread_all(fd, &out, sizeof(CellRecord), (off_t)(((size_t)i * ny + j) * sizeof(CellRecord)));
+  ::close(fd);
+  return ok;
+}
+
 void write_hf2d(const std::string& path, const Field& J) {
   if (!J.whole()) throw std::runtime_error("write_hf2d: the field holds a strip only (use write_hf2d_slab)");
   int fd = ::open(path.c_str(), O_WRONLY | O_CREAT, 0644);

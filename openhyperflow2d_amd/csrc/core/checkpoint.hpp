@@ -13,6 +13,12 @@ namespace hf2d {
 
 // Returns true and fills J when `path` exists with exactly nx*ny*1248 bytes.
 bool read_hf2d(const std::string& path, Field& J);
+// Windowed field (Field::resize_window): the resident columns' slab at its
+// file offset plus the CT / TurbType words of every other cell (streamed in
+// blocks, nothing else of them is kept).  False unless the size matches.
+bool read_hf2d_window(const std::string& path, Field& J);
+// one record (i, j) of an image of nx*ny records
+bool read_hf2d_record(const std::string& path, int nx, int ny, int i, int j, CellRecord& out);
 // zero-filled image of the full size (the reference's swap file of a cold start)
 void create_zero_hf2d(const std::string& path, int nx, int ny);
 // a file of exactly nx*ny records exists at path

@@ -83,35 +83,24 @@ int main(int argc, char** argv) {
       device = deck.get_int_or("isSingleGPU", 0) ? deck.get_int_or("ActiveSingleGPU", 0) : 0;
       if (env.world > 1) device = env.local_rank;   // one GPU per local rank
     }
-    // Multi-rank: rank 0 pre-processes the deck once and sends every rank its
-    // strip (its columns + one ghost column each side, case_io.cpp), as the
-    // reference's rank 0 does (hf2d_start.cpp:143-205); no other rank builds
-    // the whole field
+    // Multi-rank: strip-local pre-processing, no whole field anywhere (SURVEY
+    // 5.7; the reference's rank 0 pre-processes all of it and scatters,
+    // hf2d_start.cpp:143-205): every rank cuts the strips from a flags-only
+    // pass, pre-processes its own columns + one ghost column each side on the
+    // whole grid's 16 B/cell flag plane (a restart reads its slab of the
+    // .hf2d), and the whole-field eligibility facts are gathered from every
+    // strip in rank order
     Case cs;
     std::vector<std::pair<int, int>> parts;
     if (env.world > 1) {
-      std::string my_blob, ptxt;
-      if (root) {
-        Case full = Case::from_deck(deck, outdir, use_ckpt, &std::cout);
-        if (serial) full.cfg.semantics = Semantics::SERIAL;
-        parts = balanced_columns(full.J, env.world);
-        for (const auto& p : parts) ptxt += std::to_string(p.first) + " " + std::to_string(p.second) + " ";
-        auto strip = [&](int r) {
-          return full.pack_strip(std::max(parts[r].first - 1, 0), std::min(parts[r].second + 1, full.J.nx));
-        };
-        tcp->broadcast(ptxt, 0);
-        for (int r = 1; r < env.world; r++) tcp->send_to(r, strip(r));
-        my_blob = strip(0);
-      } else {
-        ptxt = tcp->broadcast(std::string(), 0);
-        my_blob = tcp->recv_from_root();
-      }
-      if (!root) {
-        std::istringstream ps(ptxt);
-        int a, b;
-        while (ps >> a >> b) parts.push_back({a, b});
-      }
-      cs = Case::unpack_strip(my_blob, nullptr);
+      parts = Case::partition_deck(deck, outdir, use_ckpt, env.world);
+      const int a = parts[env.rank].first, b = parts[env.rank].second;
+      cs = Case::from_deck_window(deck, outdir, use_ckpt, std::max(a - 1, 0), std::min(b + 1, parts.back().second),
+                                  root ? &std::cout : nullptr);
+      if (serial) cs.cfg.semantics = Semantics::SERIAL;
+      std::vector<FactsPart> fp;
+      for (const std::string& blob : tcp->allgather_bytes(cs.facts_part().pack())) fp.push_back(FactsPart::unpack(blob));
+      cs.merge_facts(fp);
     } else {
       cs = Case::from_deck(deck, outdir, use_ckpt, &std::cout);
       if (serial) cs.cfg.semantics = Semantics::SERIAL;

@@ -9,33 +9,166 @@
 
 namespace hf2d {
 
+// The cell-level conditions of the eligibility tests below over the resident
+// records of this Case (the whole field, or one strip of a windowed
+// pre-processing), in x-major order; facts_merge() adds the deck-level
+// conditions.  A strip rank's facts are the merge of every strip's part.
+FactsPart Case::facts_part() const {
+  FactsPart f;
+  const Config& C = cfg;
+  static const real zero = 0.0;
+  const real Rair = C.species.R[H_AIR];
+  const u64 model = TCT_k_eps_Model | TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
+                    TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model | TCT_nut_92_Model |
+                    TCT_Smagorinsky_Model;
+  for (const CellRecord& c : J.c) {
+    for (int k = 4; k < 4 + NCOMP; k++)
+      if (std::memcmp(&c.S[k], &zero, sizeof(real)) != 0) f.single_gas = false;   // +0 only
+    if (is_active(c.CT)) {
+      const EqFlags y = eq_flags(I_YFU, c.CT, c.TurbType, C.ProblemType);
+      if (y.dx2 || y.dy2) f.species_cauchy = true;
+      for (int k = 0; k < NEQ && !f.any_cauchy_x; k++)
+        if (eq_flags(k, c.CT, c.TurbType, C.ProblemType).dx2) f.any_cauchy_x = true;
+    }
+    // lean inviscid: set nodes, no Src, no SrcAdd off no-slip walls
+    // (equations >= 4 + NCOMP are frozen for inviscid nodes: their Src/SrcAdd
+    // -- e.g. left by a k-eps initialisation -- are never read)
+    if (f.lean_cells_ok && !c.is(CT_SOLID)) {
+      const char* w = nullptr;
+      if (!c.is(CT_NODE_IS_SET)) w = "unset non-solid node";
+      for (int k = 0; k < 4 + NCOMP && !w; k++)
+        if (c.Src[k] != 0.) w = "non-zero Src";
+      if (!c.is(CT_WALL_NO_SLIP))
+        for (int k = 0; k < 4 + NCOMP && !w; k++)
+          if (c.SrcAdd[k] != 0.) w = "non-zero SrcAdd off no-slip walls";
+      if (w) {
+        f.lean_cells_ok = false;
+        f.lean_why = w;
+      }
+    }
+    // single-gas split kernels: the laminar test covers every cell up to the
+    // first failing one (the whole-field scan stops there)
+    if (f.sk_cells_ok) {
+      if ((c.TurbType & model) != 0 || (c.TurbType != 0 && C.isTurbulenceReset)) f.laminar = false;
+      if (!c.is(CT_SOLID)) {
+        if (c.mu_t != 0. || c.lam_t != 0.) f.laminar = false;
+        const char* w = nullptr;
+        for (int k = 4; k < 4 + NCOMP && !w; k++)
+          if (c.Src[k] != 0.) w = "species sources";
+        if (!w && !(c.Y[0] == 0. && c.Y[1] == 0. && c.Y[2] == 0. && c.Y[3] == 1.)) w = "mixture fractions";
+        if (!w && C.chem_model != NO_REACTIONS && std::memcmp(&c.R, &Rair, sizeof(real)) != 0) w = "R != R_air";
+        if (w) {
+          f.sk_cells_ok = false;
+          f.sk_why = w;
+        }
+      }
+    }
+  }
+  return f;
+}
+
+void Case::merge_facts(const std::vector<FactsPart>& parts) {
+  CaseFacts f;
+  const Config& C = cfg;
+  f.single_gas = true;
+  for (const FactsPart& p : parts) {
+    f.single_gas = f.single_gas && p.single_gas;
+    f.any_cauchy_x = f.any_cauchy_x || p.any_cauchy_x;
+    f.species_cauchy = f.species_cauchy || p.species_cauchy;
+  }
+  // lean inviscid
+  f.lean_ok = false;
+  if (C.ProblemType == SM_NS) f.lean_why = "viscous problem";
+  else if (!C.sources.empty()) f.lean_why = "gas sources";
+  else if (!C.isAdiabaticWall) f.lean_why = "wall heat transfer";
+  else if (C.chem_model == CRM_ARRENIUS) f.lean_why = "finite-rate chemistry sources";
+  else {
+    f.lean_ok = true;
+    for (const FactsPart& p : parts)   // the first failing cell in x-major (= rank) order
+      if (!p.lean_cells_ok) {
+        f.lean_ok = false;
+        f.lean_why = p.lean_why;
+        break;
+      }
+  }
+  // single-gas split kernels
+  f.sk_mode = SK_GENERIC;
+  if (C.mech_mode()) {   // species block on SK_MECH for Euler and N-S decks
+    f.sk_mode = SK_MECH;
+    f.sk_why = "mechanism: SK_MECH";
+  } else if (C.ProblemType != SM_NS) f.sk_why = "inviscid problem";
+  else if (!C.sources.empty()) f.sk_why = "gas sources";
+  else if (C.chem_model == CRM_ARRENIUS) f.sk_why = "finite-rate chemistry sources";
+  else if (!f.single_gas) f.sk_why = "species present";
+  else {
+    bool laminar = true, ok = true;
+    for (const FactsPart& p : parts) {
+      laminar = laminar && p.laminar;
+      if (!p.sk_cells_ok) {
+        ok = false;
+        f.sk_why = p.sk_why;
+        break;
+      }
+    }
+    if (ok) {
+      f.sk_mode = laminar ? SK_SGL : SK_SGT;
+      f.sk_why = laminar ? "" : "turbulent: SK_SGT";
+    }
+  }
+  f.valid = true;
+  facts = f;
+}
+
+std::string FactsPart::pack() const {
+  std::string b;
+  b += (char)single_gas;
+  b += (char)any_cauchy_x;
+  b += (char)species_cauchy;
+  b += (char)lean_cells_ok;
+  b += (char)sk_cells_ok;
+  b += (char)laminar;
+  b += lean_why;
+  b += '\0';
+  b += sk_why;
+  return b;
+}
+
+FactsPart FactsPart::unpack(const std::string& b) {
+  if (b.size() < 7) throw std::runtime_error("FactsPart::unpack: short blob");
+  FactsPart f;
+  f.single_gas = b[0];
+  f.any_cauchy_x = b[1];
+  f.species_cauchy = b[2];
+  f.lean_cells_ok = b[3];
+  f.sk_cells_ok = b[4];
+  f.laminar = b[5];
+  const size_t z = b.find('\0', 6);
+  if (z == std::string::npos) throw std::runtime_error("FactsPart::unpack: bad blob");
+  f.lean_why = b.substr(6, z - 6);
+  f.sk_why = b.substr(z + 1);
+  return f;
+}
+
+// The whole field's facts: a strip rank's merged ones (they must be there:
+// a strip alone cannot tell), else one pass over the whole resident field.
+static const CaseFacts& whole_facts(const Case& cs, CaseFacts& tmp) {
+  if (!cs.J.whole()) {
+    if (!cs.facts.valid) throw std::runtime_error("eligibility of a strip Case without the merged whole-field facts");
+    return cs.facts;
+  }
+  Case& m = const_cast<Case&>(cs);
+  const CaseFacts keep = m.facts;
+  m.merge_facts({cs.facts_part()});
+  tmp = m.facts;
+  m.facts = keep;
+  return tmp;
+}
+
 bool lean_eligible(const Case& cs, std::string* why) {
-  if (!cs.J.whole() && cs.facts.valid) {   // strip rank: the whole field's answer
-    if (why) *why = cs.facts.lean_why;
-    return cs.facts.lean_ok;
-  }
-  auto no = [&](const char* w) {
-    if (why) *why = w;
-    return false;
-  };
-  const Config& C = cs.cfg;
-  if (C.ProblemType == SM_NS) return no("viscous problem");
-  if (!C.sources.empty()) return no("gas sources");
-  if (!C.isAdiabaticWall) return no("wall heat transfer");
-  if (C.chem_model == CRM_ARRENIUS) return no("finite-rate chemistry sources");
-  for (const CellRecord& c : cs.J.c) {
-    if (c.is(CT_SOLID)) continue;
-    if (!c.is(CT_NODE_IS_SET)) return no("unset non-solid node");
-    // equations >= 4 + NCOMP are frozen for inviscid nodes: their Src/SrcAdd
-    // (e.g. left by a k-eps initialisation) are never read
-    for (int k = 0; k < 4 + NCOMP; k++)
-      if (c.Src[k] != 0.) return no("non-zero Src");
-    if (!c.is(CT_WALL_NO_SLIP))
-      for (int k = 0; k < 4 + NCOMP; k++)
-        if (c.SrcAdd[k] != 0.) return no("non-zero SrcAdd off no-slip walls");
-  }
-  if (why) why->clear();
-  return true;
+  CaseFacts t;
+  const CaseFacts& f = whole_facts(cs, t);
+  if (why) *why = f.lean_ok ? "" : f.lean_why;
+  return f.lean_ok;
 }
 
 // Single-gas laminar N-S specialisation of the generic stepper (fill_cell /
@@ -43,72 +176,29 @@ bool lean_eligible(const Case& cs, std::string* why) {
 // reads move through memory.  Requires species +0 everywhere, no species
 // sources, no turbulence model, mu_t = lam_t = 0, Y = (0,0,0,1) and (with
 // chemistry on) R = R_air everywhere -- then the generic stepper leaves every
-// skipped field unchanged.
+// skipped field unchanged.  Boundary-condition bits alone leave turb_model()
+// a no-op; the model bits (or an initial-reset pass on any TurbType, which
+// sets mu_t = 5 mu) do not.
 int sk_eligible(const Case& cs, std::string* why) {
-  if (!cs.J.whole() && cs.facts.valid) {
-    if (why) *why = cs.facts.sk_why;
-    return cs.facts.sk_mode;
-  }
-  auto no = [&](const char* w) {
-    if (why) *why = w;
-    return (int)SK_GENERIC;
-  };
-  const Config& C = cs.cfg;
-  if (C.mech_mode()) {   // species block on SK_MECH for Euler and N-S decks
-    if (why) *why = "mechanism: SK_MECH";
-    return SK_MECH;
-  }
-  if (C.ProblemType != SM_NS) return no("inviscid problem");
-  if (!C.sources.empty()) return no("gas sources");
-  if (C.chem_model == CRM_ARRENIUS) return no("finite-rate chemistry sources");
-  if (!lean_single_gas(cs)) return no("species present");
-  const real Rair = C.species.R[H_AIR];
-  // boundary-condition bits alone leave turb_model() a no-op; the model bits
-  // (or an initial-reset pass on any TurbType, which sets mu_t = 5 mu) do not
-  const u64 model = TCT_k_eps_Model | TCT_Prandtl_Model | TCT_Integral_Model | TCT_Spalart_Allmaras_Model |
-                    TCT_k_omega_Model | TCT_k_omega_SST_Model | TCT_Baldwin_Lomax_Model | TCT_nut_92_Model |
-                    TCT_Smagorinsky_Model;
-  bool laminar = true;
-  for (const CellRecord& c : cs.J.c) {
-    if ((c.TurbType & model) != 0 || (c.TurbType != 0 && C.isTurbulenceReset)) laminar = false;
-    if (c.is(CT_SOLID)) continue;
-    if (c.mu_t != 0. || c.lam_t != 0.) laminar = false;
-    for (int k = 4; k < 4 + NCOMP; k++)
-      if (c.Src[k] != 0.) return no("species sources");
-    if (!(c.Y[0] == 0. && c.Y[1] == 0. && c.Y[2] == 0. && c.Y[3] == 1.)) return no("mixture fractions");
-    if (C.chem_model != NO_REACTIONS && std::memcmp(&c.R, &Rair, sizeof(real)) != 0) return no("R != R_air");
-  }
-  if (why) *why = laminar ? "" : "turbulent: SK_SGT";
-  return laminar ? SK_SGL : SK_SGT;
+  CaseFacts t;
+  const CaseFacts& f = whole_facts(cs, t);
+  if (why) *why = f.sk_why;
+  return f.sk_mode;
 }
 
 bool mech_species_cauchy(const Case& cs) {
-  if (!cs.J.whole() && cs.facts.valid) return cs.facts.species_cauchy;
-  for (const CellRecord& c : cs.J.c) {
-    if (!is_active(c.CT)) continue;
-    const EqFlags f = eq_flags(I_YFU, c.CT, c.TurbType, cs.cfg.ProblemType);
-    if (f.dx2 || f.dy2) return true;
-  }
-  return false;
+  CaseFacts t;
+  return whole_facts(cs, t).species_cauchy;
 }
 
 bool lean_single_gas(const Case& cs) {
-  if (!cs.J.whole() && cs.facts.valid) return cs.facts.single_gas;
-  static const real zero = 0.0;
-  for (const CellRecord& c : cs.J.c)
-    for (int k = 4; k < 4 + NCOMP; k++)
-      if (std::memcmp(&c.S[k], &zero, sizeof(real)) != 0) return false;   // +0 only
-  return true;
+  CaseFacts t;
+  return whole_facts(cs, t).single_gas;
 }
 
 bool lean_any_cauchy_x(const Case& cs) {
-  if (!cs.J.whole() && cs.facts.valid) return cs.facts.any_cauchy_x;
-  for (const CellRecord& c : cs.J.c) {
-    if (!is_active(c.CT)) continue;
-    for (int k = 0; k < NEQ; k++)
-      if (eq_flags(k, c.CT, c.TurbType, cs.cfg.ProblemType).dx2) return true;
-  }
-  return false;
+  CaseFacts t;
+  return whole_facts(cs, t).any_cauchy_x;
 }
 
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {

@@ -417,8 +417,13 @@ void write_species_slab(const std::string& path, const MechInfo& m, int nx, int 
   ::close(fd);
 }
 
-bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, std::vector<real>& rhoY) {
+bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, std::vector<real>& rhoY,
+                          int a, int b) {
   const int ns = (int)m.species.size();
+  if (a < 0) {
+    a = 0;
+    b = nx;
+  }
   struct stat st;
   if (::stat(path.c_str(), &st) != 0 || (size_t)st.st_size != species_sidecar_bytes(ns, nx, ny)) return false;
   std::ifstream f(path, std::ios::binary);
@@ -426,7 +431,9 @@ bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, in
   std::string h(SPECIES_HEADER + 16 * ns, '\0');
   f.read(&h[0], (std::streamsize)h.size());
   if (h != species_header(m, nx, ny)) return false;
-  const long N = (long)nx * ny;
+  // columns [a, b): cell-major [cell][species] records at their offset
+  const long N = (long)(b - a) * ny;
+  f.seekg((std::streamoff)(h.size() + (size_t)a * ny * ns * sizeof(real)));
   std::vector<real> buf((size_t)N * ns);
   f.read((char*)buf.data(), (std::streamsize)(buf.size() * sizeof(real)));
   if (!f) return false;

@@ -40,7 +40,9 @@ void write_species_sidecar(const std::string& path, const MechInfo& m, int nx, i
 // global column col0 (per-rank slab write into an existing full-size file)
 void write_species_slab(const std::string& path, const MechInfo& m, int nx, int ny, const real* rhoY_local,
                         long local_n, int local_i0, int gi0, int ncols);
-bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, std::vector<real>& rhoY);
+// (a >= 0: only the columns [a, b), species-major over them)
+bool read_species_sidecar(const std::string& path, const MechInfo& m, int nx, int ny, std::vector<real>& rhoY,
+                          int a = -1, int b = -1);
 
 // Tecplot Y_fuel / Y_ox / Y_cp / Y_i columns of a mechanism state: the
 // dominant species of each reference slot, the rest lumped into Y_i.

@@ -218,9 +218,13 @@ struct PreCtx {
     cs.fill_node(n, 0, 1);
   }
 
-  void mark_cell(CellRecord& n, const Segment& s, real alpha) {
-    n.CT = n.CT | (u64)(int64_t)s.bnt | CT_NODE_IS_SET;
-    n.TurbType = s.btc;
+  // (flags of every cell; the rest of the record only where it is resident)
+  void mark_cell(int i, int j, const Segment& s, real alpha) {
+    Field& J = cs.J;
+    J.ct(i, j) = J.ct(i, j) | (u64)(int64_t)s.bnt | CT_NODE_IS_SET;
+    J.tt(i, j) = s.btc;
+    if (!J.resident(i)) return;
+    CellRecord& n = J.at(i, j);
     n.NGX = (3 - n.idXr - n.idXl);
     n.NGY = (3 - n.idYu - n.idYd);
     n.BGX = std::cos(alpha);
@@ -251,9 +255,9 @@ struct PreCtx {
     } else {
       Alpha = PI / 2.;
     }
-    auto cell = [&](unsigned i, unsigned j) -> CellRecord& {
+    auto mark = [&](unsigned i, unsigned j) {
       if (i >= MX || j >= MY) throw DeckError("bound segment leaves the computation area");
-      return J.at((int)i, (int)j);
+      mark_cell((int)i, (int)j, s, Alpha);
     };
     if (std::fabs(DX) > std::fabs(DY)) {
       const unsigned j1 = std::min(s.sx, s.ex);
@@ -261,7 +265,7 @@ struct PreCtx {
       const unsigned j2 = std::max(s.sx, s.ex);
       for (unsigned i = j1; i <= j2; i++) {
         const unsigned j = k1 + (int)((real)(i - j1) * std::tan(Alpha));
-        mark_cell(cell(i, j), s, Alpha);
+        mark(i, j);
       }
     } else {
       const unsigned j1 = std::min(s.sy, s.ey);
@@ -273,7 +277,7 @@ struct PreCtx {
           j = k1 + (int)((real)(i - j1) / std::tan(Alpha));
         else
           j = k1;
-        mark_cell(cell(j, i), s, Alpha);
+        mark(j, i);
       }
     }
     return true;
@@ -360,40 +364,44 @@ struct PreCtx {
     return true;
   }
 
-  // Area2D::FillArea2D — level-synchronous flood fill from a seed node.
+  // Area2D::FillArea2D — level-synchronous flood fill from a seed node
+  // (over the whole grid's flags; flows and fills of resident records only).
   void fill_area(unsigned X, unsigned Y, u64 bnt, const GasFlow* f2d, const real* pY, u64 att) {
     Field& J = cs.J;
     const unsigned XMax = (unsigned)J.nx, YMax = (unsigned)J.ny;
     if (!(XMax > X && YMax > Y))
       throw DeckError("Init Area point [" + std::to_string(X) + "," + std::to_string(Y) + "] out of range.");
-    if (J.at(X, Y).is(CT_NODE_IS_SET))
+    if (J.is(X, Y, CT_NODE_IS_SET))
       throw DeckError("Init Area point [" + std::to_string(X) + "," + std::to_string(Y) +
                       "] already in initialized node.");
     const u64 ANT = bnt | CT_NODE_IS_SET;
     const u64 ATT = att;
     std::vector<std::pair<unsigned, unsigned>> BNA, FNA;
-    J.at(X, Y).CT = ANT;
-    J.at(X, Y).TurbType = ATT;
+    J.ct(X, Y) = ANT;
+    J.tt(X, Y) = ATT;
     BNA.push_back({X, Y});
     while (!BNA.empty()) {
       for (size_t q = 0; q < BNA.size(); q++) {
         const unsigned tX = BNA[q].first, tY = BNA[q].second;
-        CellRecord& n = J.at(tX, tY);
-        if (pY)
-          for (int ii = 0; ii < NSPEC; ii++) n.Y[ii] = pY[ii];
-        if (f2d) assign_flow2d(n, *f2d);
-        n.BGX = 1.;
-        n.BGY = 1.;
-        n.NGX = 1;
-        n.NGY = 1;
-        n.idXl = n.idYu = n.idXr = n.idYd = 1;
+        CellRecord* n = J.resident(tX) ? &J.at(tX, tY) : nullptr;
+        if (n) {
+          if (pY)
+            for (int ii = 0; ii < NSPEC; ii++) n->Y[ii] = pY[ii];
+          if (f2d) assign_flow2d(*n, *f2d);
+          n->BGX = 1.;
+          n->BGY = 1.;
+          n->NGX = 1;
+          n->NGY = 1;
+          n->idXl = n->idYu = n->idXr = n->idYd = 1;
+        }
+        const bool n_solid = J.is(tX, tY, CT_SOLID);
         auto visit = [&](unsigned x, unsigned y, int side) {
-          CellRecord& m = J.at(x, y);
-          if (!m.is(CT_NODE_IS_SET)) {
-            m.CT = ANT;
-            m.TurbType = ATT;
+          if (!J.is(x, y, CT_NODE_IS_SET)) {
+            J.ct(x, y) = ANT;
+            J.tt(x, y) = ATT;
             FNA.push_back({x, y});
-          } else if (!m.is(CT_SOLID) && n.is(CT_SOLID)) {
+          } else if (!J.is(x, y, CT_SOLID) && n_solid && J.resident(x)) {
+            CellRecord& m = J.at(x, y);
             switch (side) {
               case 0: m.NGX = 0; m.idXr = 0; break;   // left neighbour
               case 1: m.NGX = 0; m.idXl = 0; break;   // right neighbour
@@ -406,7 +414,7 @@ struct PreCtx {
         if (tX < XMax - 1) visit(tX + 1, tY, 1);
         if (tY > 0) visit(tX, tY - 1, 2);
         if (tY < YMax - 1) visit(tX, tY + 1, 3);
-        cs.fill_node(n, 1, 0);
+        if (n) cs.fill_node(*n, 1, 0);
       }
       BNA.swap(FNA);
       FNA.clear();
@@ -425,6 +433,18 @@ void Field::resize(int X, int Y) {
   std::memset((void*)c.data(), 0, c.size() * sizeof(CellRecord));
 }
 
+void Field::resize_window(int X, int Y, int a, int b) {
+  a = std::max(a, 0);
+  b = std::min(b, X);
+  nx = X;
+  ny = Y;
+  i0 = a;
+  nxl = std::max(b - a, 0);
+  c.assign((size_t)nxl * Y, CellRecord{});
+  std::memset((void*)c.data(), 0, c.size() * sizeof(CellRecord));
+  g.assign((size_t)X * Y, CellFlags{});
+}
+
 void Field::trim(int a, int b) {
   a = std::max(a, i0);
   b = std::min(b, i0 + nxl);
@@ -437,6 +457,7 @@ void Field::trim(int a, int b) {
 }
 
 void Case::trim_to_columns(int a, int b) {
+  if (J.whole() && !facts.valid) compute_facts();   // a strip alone cannot tell
   a = std::max(a, J.i0);
   b = std::min(b, J.i0 + J.nxl);
   if (!mech_rhoY.empty()) {
@@ -458,9 +479,48 @@ void Case::fill_node(CellRecord& n, int is_mu_t, int is_init) const {
   hf2d::fill_node(n, P);
 }
 
+const CellRecord* Case::far_record(int i, int j) {
+  if (J.resident(i)) return &J.at(i, j);
+  if (!preloaded) return nullptr;
+  const long key = (long)i * J.ny + j;
+  for (auto& e : far_cache)
+    if (e.first == key) return &e.second;
+  CellRecord r;
+  if (!read_hf2d_record(swap_path, J.nx, J.ny, i, j, r)) throw std::runtime_error("cannot read record of " + swap_path);
+  far_cache.push_back({key, r});
+  return &far_cache.back().second;
+}
+
+Case Case::from_deck_window(InputDeck deck, const std::string& workdir, bool use_checkpoint, int a, int b,
+                            std::ostream* log) {
+  Case cs;
+  cs.win_a = std::max(a, 0);
+  cs.win_b = b;
+  cs.log = log;
+  cs.load_and_preprocess(deck, workdir, use_checkpoint);
+  cs.J.drop_flags();
+  std::vector<std::pair<long, CellRecord>>().swap(cs.far_cache);
+  cs.win_a = cs.win_b = -1;
+  return cs;
+}
+
+std::vector<std::pair<int, int>> Case::partition_deck(InputDeck deck, const std::string& workdir, bool use_checkpoint,
+                                                      int nparts) {
+  Case cs;   // flags only: an empty window
+  cs.win_a = cs.win_b = 0;
+  cs.load_and_preprocess(deck, workdir, use_checkpoint, true);
+  return balanced_columns(cs.J, nparts);
+}
+
 Case Case::from_deck(InputDeck deck, const std::string& workdir, bool use_checkpoint, std::ostream* log) {
   Case cs;
   cs.log = log;
+  cs.load_and_preprocess(deck, workdir, use_checkpoint);
+  return cs;
+}
+
+void Case::load_and_preprocess(InputDeck& deck, const std::string& workdir, bool use_checkpoint, bool flags_only) {
+  Case& cs = *this;
   cs.cfg.load_globals(deck);
   if (cs.cfg.chem_model == CRM_ARRENIUS && !cs.cfg.mechanism.empty()) {
     cs.cfg.mech = load_mechanism(cs.cfg.mechanism, workdir);
@@ -470,10 +530,11 @@ Case Case::from_deck(InputDeck deck, const std::string& workdir, bool use_checkp
       throw DeckError("mechanism " + cs.cfg.mech->name + " has no slot map (slot fuel|ox|cp|air records)");
   }
   cs.preprocess(deck, workdir, use_checkpoint);
-  if (cs.cfg.mech_mode()) {
+  if (cs.cfg.mech_mode() && !flags_only) {
     if (!cs.cfg.sources.empty())
       throw DeckError("SourceList2D species sources are not supported in mechanism mode (NumSrc must be 0)");
-    if (!(cs.preloaded && read_species_sidecar(cs.species_path(), *cs.cfg.mech, cs.J.nx, cs.J.ny, cs.mech_rhoY))) {
+    if (!(cs.preloaded && read_species_sidecar(cs.species_path(), *cs.cfg.mech, cs.J.nx, cs.J.ny, cs.mech_rhoY,
+                                                cs.J.i0, cs.J.i0 + cs.J.nxl))) {
       if (cs.preloaded)
         throw DeckError("checkpoint " + cs.swap_path + " has no matching species sidecar (" + cs.species_path() +
                         ") for mechanism " + cs.cfg.mech->name);
@@ -483,7 +544,6 @@ Case Case::from_deck(InputDeck deck, const std::string& workdir, bool use_checkp
       cs.refresh_mechanism_primitives();
     }
   }
-  return cs;
 }
 
 void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpoint) {
@@ -606,20 +666,28 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
   }
 
   // ---- Swap file (checkpoint) ----
-  J.resize(C.MaxX, C.MaxY);
+  if (win_a >= 0)
+    J.resize_window(C.MaxX, C.MaxY, win_a, win_b);
+  else
+    J.resize(C.MaxX, C.MaxY);
   preloaded = false;
   swap_path = workdir.empty() ? C.swap_file : (workdir + "/" + C.swap_file);
   if (use_checkpoint) {
     // an all-zero image is the placeholder a failed first cycle leaves behind
     // (create_zero_hf2d): not a checkpoint
     bool any_set = false;
-    if (read_hf2d(swap_path, J))
+    if (J.windowed() ? read_hf2d_window(swap_path, J) : read_hf2d(swap_path, J)) {
       for (const CellRecord& c : J.c)
         if (c.CT != 0) {
           any_set = true;
           break;
         }
-    if (!any_set) std::fill(J.c.begin(), J.c.end(), CellRecord{});
+      for (size_t q = 0; q < J.g.size() && !any_set; q++) any_set = J.g[q].CT != 0;
+    }
+    if (!any_set) {
+      std::fill(J.c.begin(), J.c.end(), CellRecord{});
+      std::fill(J.g.begin(), J.g.end(), CellFlags{});
+    }
     if (any_set) {
       preloaded = true;
       say("Mapping computation area...OK (preloaded " + swap_path + ")\n");
@@ -729,7 +797,7 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
 
   if (!PreloadFlag) {
     for (int j = 0; j < C.MaxY; j++)
-      for (int i = 0; i < C.MaxX; i++) {
+      for (int i = J.i0; i < J.i0 + J.nxl; i++) {
         CellRecord& n = J.at(i, j);
         n.x = (i + 0.5) * C.dx;
         n.y = (j + 0.5) * C.dy;
@@ -996,35 +1064,45 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
 
   // ---- First initialisation ----
   if (!PreloadFlag) {
-    for (int i = 0; i < C.MaxX; i++)
+    auto unset = [&](int i, int j) {
+      if (!C.isIgnoreUnsetNodes && !J.is(i, j, CT_NODE_IS_SET))
+        throw DeckError("Node (" + std::to_string(i) + "," + std::to_string(j) +
+                        ") has not CT_NODE_IS_SET flag. Possible some \"Area\" objects not defined.");
+    };
+    for (int i = 0; i < C.MaxX; i++) {
+      if (!J.resident(i)) {   // windowed: only the unset-node check
+        for (int j = 0; j < C.MaxY; j++) unset(i, j);
+        continue;
+      }
       for (int j = 0; j < C.MaxY; j++) {
         CellRecord& n = J.at(i, j);
         n.idXl = n.idXr = n.idYu = n.idYd = 1;
         n.l_min = std::min(C.dx * C.MaxX, C.dy * C.MaxY);
         for (int k = 0; k < NEQ; k++) n.beta[k] = C.beta0;
-        if (j == 0 || J.at(i, j - 1).is(CT_SOLID)) n.idYd = 0;
-        if (j == C.MaxY - 1 || J.at(i, j + 1).is(CT_SOLID)) n.idYu = 0;
-        if (i == 0 || J.at(i - 1, j).is(CT_SOLID)) n.idXl = 0;
-        if (i == C.MaxX - 1 || J.at(i + 1, j).is(CT_SOLID)) n.idXr = 0;
+        if (j == 0 || J.is(i, j - 1, CT_SOLID)) n.idYd = 0;
+        if (j == C.MaxY - 1 || J.is(i, j + 1, CT_SOLID)) n.idYu = 0;
+        if (i == 0 || J.is(i - 1, j, CT_SOLID)) n.idXl = 0;
+        if (i == C.MaxX - 1 || J.is(i + 1, j, CT_SOLID)) n.idXr = 0;
         if (n.is(CT_WALL_NO_SLIP) || n.is(CT_WALL_LAW)) {
           n.NGX = n.idXl - n.idXr + n.idXl * n.idXr;
           n.NGY = n.idYd - n.idYu + n.idYd * n.idYu;
         }
-        if (!C.isIgnoreUnsetNodes && !n.is(CT_NODE_IS_SET))
-          throw DeckError("Node (" + std::to_string(i) + "," + std::to_string(j) +
-                          ") has not CT_NODE_IS_SET flag. Possible some \"Area\" objects not defined.");
+        unset(i, j);
         if (n.is(CT_SOLID))
           n.Tg = C.Ts0;
         else
           fill_node(n, 0, 1);
         if (n.p == 0.) n.Tg = C.Ts0;
       }
+    }
   }
 
-  if (global_time > 0.)
-    J.at(0, 0).time = global_time;
-  else
-    global_time = J.at(0, 0).time;
+  if (global_time > 0.) {
+    if (J.resident(0)) J.at(0, 0).time = global_time;
+  } else {
+    const CellRecord* c00 = far_record(0, 0);
+    global_time = c00 ? c00->time : 0.0;   // (a fresh non-resident record: 0)
+  }
 
   if (C.ProblemType == SM_NS) set_wall_nodes();
   scan_area(1);
@@ -1077,11 +1155,10 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
 void Case::set_wall_nodes() {
   for (int j = 0; j < J.ny; j++)
     for (int i = 0; i < J.nx; i++) {
-      CellRecord& n = J.at(i, j);
-      if (n.is(CT_SOLID) || n.is(NT_FC)) continue;
-      bool hit = (j < J.ny - 1 && J.at(i, j + 1).is(CT_SOLID)) || (j > 0 && J.at(i, j - 1).is(CT_SOLID)) ||
-                 (i > 0 && J.at(i - 1, j).is(CT_SOLID)) || (i < J.nx - 1 && J.at(i + 1, j).is(CT_SOLID));
-      if (hit) n.CT |= NT_WNS;
+      if (J.is(i, j, CT_SOLID) || J.is(i, j, NT_FC)) continue;
+      bool hit = (j < J.ny - 1 && J.is(i, j + 1, CT_SOLID)) || (j > 0 && J.is(i, j - 1, CT_SOLID)) ||
+                 (i > 0 && J.is(i - 1, j, CT_SOLID)) || (i < J.nx - 1 && J.is(i + 1, j, CT_SOLID));
+      if (hit) J.ct(i, j) |= NT_WNS;
     }
 }
 
@@ -1089,10 +1166,8 @@ void Case::set_wall_nodes() {
 void Case::collect_wall_nodes() {
   wall_nodes.clear();
   for (int j = 0; j < J.ny; j++)
-    for (int i = 0; i < J.nx; i++) {
-      const CellRecord& n = J.at(i, j);
-      if (!n.is(CT_SOLID) && (n.is(CT_WALL_LAW) || n.is(CT_WALL_NO_SLIP))) wall_nodes.push_back({i, j});
-    }
+    for (int i = 0; i < J.nx; i++)
+      if (!J.is(i, j, CT_SOLID) && (J.is(i, j, CT_WALL_LAW) || J.is(i, j, CT_WALL_NO_SLIP))) wall_nodes.push_back({i, j});
 }
 
 // SetMinDistanceToWall2D (deeps2d_core.cpp:4783-4832) scans every wall node
@@ -1109,7 +1184,7 @@ void Case::collect_wall_nodes() {
 // columns.  set_min_distance_to_wall_bruteforce() is the literal scan.
 void Case::set_min_distance_to_wall_bruteforce(real x0) {
   const real min_l = std::min(cfg.dx, cfg.dy);
-  for (int i = 0; i < J.nx; i++)
+  for (int i = J.i0; i < J.i0 + J.nxl; i++)
     for (int j = 0; j < J.ny; j++) {
       CellRecord& n = J.at(i, j);
       if (!n.is(CT_NODE_IS_SET) || n.is(CT_SOLID)) continue;
@@ -1201,7 +1276,7 @@ void Case::set_min_distance_to_wall(real x0) {
   std::atomic<int> next{0};
   for (int t = 0; t < nth; t++)
     pool.emplace_back([&] {
-      for (int i; (i = next.fetch_add(1)) < J.nx;)
+      for (int i; (i = J.i0 + next.fetch_add(1)) < J.i0 + J.nxl;)
         for (int j = 0; j < J.ny; j++) cell(i, j);
     });
   for (auto& th : pool) th.join();
@@ -1209,13 +1284,15 @@ void Case::set_min_distance_to_wall(real x0) {
 
 // Recalc_y_plus (serial variant): u_tau from the nearest wall node.
 void Case::recalc_y_plus() {
-  for (int i = 0; i < J.nx; i++)
+  static const CellRecord fresh{};   // a wall record no step has touched: no shear (y+ = 0)
+  for (int i = J.i0; i < J.i0 + J.nxl; i++)
     for (int j = 0; j < J.ny; j++) {
       CellRecord& n = J.at(i, j);
       if (!n.is(CT_NODE_IS_SET) || n.is(CT_SOLID)) continue;
       const int iw = n.i_wall, jw = n.j_wall;
       if (!J.in(iw, jw)) continue;
-      const CellRecord& w = J.at(iw, jw);
+      const CellRecord* wp = far_record(iw, jw);
+      const CellRecord& w = wp ? *wp : fresh;
       const real tau_w = (std::fabs(w.dUdy) + std::fabs(w.dVdx)) * w.mu;
       if (w.S[I_RHO] > 0.0 && tau_w > 0.0) {
         const real U_w = std::sqrt(tau_w / w.S[I_RHO] + 1e-30);
@@ -1229,7 +1306,7 @@ void Case::recalc_y_plus() {
 // SetInitBoundaryLayer (the reference's missing-brace quirk Q6 is kept:
 // rhoV is scaled for every fresh cell, rhoU only inside delta).
 void Case::set_init_boundary_layer(real delta) {
-  for (int i = 0; i < J.nx; i++)
+  for (int i = J.i0; i < J.i0 + J.nxl; i++)
     for (int j = 0; j < J.ny; j++) {
       CellRecord& n = J.at(i, j);
       if (n.is(CT_NODE_IS_SET) && !n.is(CT_SOLID) && n.time == 0. && delta > 0) {
@@ -1243,17 +1320,16 @@ void Case::set_init_boundary_layer(real delta) {
 int Case::set_non_reflected_bc() {
   int nr = 0;
   auto ok = [&](int i, int j) {
-    const CellRecord& m = J.at(i, j);
-    return m.is(CT_NODE_IS_SET) && !m.is(CT_WALL_NO_SLIP) && !m.is(CT_SOLID) && !m.is(NT_FC);
+    return J.is(i, j, CT_NODE_IS_SET) && !J.is(i, j, CT_WALL_NO_SLIP) && !J.is(i, j, CT_SOLID) && !J.is(i, j, NT_FC);
   };
   for (int ii = 0; ii < J.nx; ii++)
     for (int jj = 0; jj < J.ny; jj++) {
-      if (!J.at(ii, jj).is(NT_FARFIELD)) continue;
+      if (!J.is(ii, jj, NT_FARFIELD)) continue;
       nr++;
-      if (ii > 0 && ok(ii - 1, jj)) { J.at(ii - 1, jj).CT |= CT_NONREFLECTED; nr++; }
-      if (ii < J.nx - 1 && ok(ii + 1, jj)) { J.at(ii + 1, jj).CT |= CT_NONREFLECTED; nr++; }
-      if (jj > 0 && ok(ii, jj - 1)) { J.at(ii, jj - 1).CT |= CT_NONREFLECTED; nr++; }
-      if (jj < J.ny - 1 && ok(ii, jj + 1)) { J.at(ii, jj + 1).CT |= CT_NONREFLECTED; nr++; }
+      if (ii > 0 && ok(ii - 1, jj)) { J.ct(ii - 1, jj) |= CT_NONREFLECTED; nr++; }
+      if (ii < J.nx - 1 && ok(ii + 1, jj)) { J.ct(ii + 1, jj) |= CT_NONREFLECTED; nr++; }
+      if (jj > 0 && ok(ii, jj - 1)) { J.ct(ii, jj - 1) |= CT_NONREFLECTED; nr++; }
+      if (jj < J.ny - 1 && ok(ii, jj + 1)) { J.ct(ii, jj + 1) |= CT_NONREFLECTED; nr++; }
     }
   return nr;
 }
@@ -1262,20 +1338,20 @@ int Case::set_non_reflected_bc() {
 // active-cell-balanced column partition.
 void Case::scan_area(int num_parts) {
   for (int j = 0; j < J.ny; j++)
-    for (int i = 0; i < J.nx; i++) {
-      CellRecord& n = J.at(i, j);
-      if (!n.is(CT_SOLID)) n.CT |= CT_NODE_IS_SET;
-    }
+    for (int i = 0; i < J.nx; i++)
+      if (!J.is(i, j, CT_SOLID)) J.ct(i, j) |= CT_NODE_IS_SET;
   if (cfg.isTurbulenceReset && cfg.ProblemType == SM_NS) {
     const u64 TM = turb_model_bits(cfg.TurbMod);
     for (int i = 0; i < J.nx; i++)
       for (int j = 0; j < J.ny; j++) {
-        CellRecord& n = J.at(i, j);
+        u64& tt = J.tt(i, j);
         const u64 models[] = {TCT_Integral_Model, TCT_Prandtl_Model, TCT_Spalart_Allmaras_Model, TCT_k_eps_Model,
                               TCT_Smagorinsky_Model, TCT_k_omega_SST_Model};
         for (u64 m : models)
-          if (n.is_turb(m)) n.TurbType = (n.TurbType ^ m) & n.TurbType;
-        n.TurbType |= TM;
+          if ((tt & m) == m) tt = (tt ^ m) & tt;
+        tt |= TM;
+        if (!J.resident(i)) continue;
+        CellRecord& n = J.at(i, j);
         n.dkdx = n.dkdy = n.depsdx = n.depsdy = 0.0;
         n.S[I_K] = n.S[I_EPS] = n.Src[I_K] = n.Src[I_EPS] = 0.0;
         n.mu_t = n.lam_t = 0.0;
@@ -1290,14 +1366,14 @@ std::vector<std::pair<int, int>> Case::partition_columns(int num_parts) const {
   long active = 0;
   for (int i = 0; i < J.nx; i++)
     for (int j = 0; j < J.ny; j++)
-      if (J.at(i, j).is(CT_NODE_IS_SET) && !J.at(i, j).is(CT_SOLID)) active++;
+      if (J.is(i, j, CT_NODE_IS_SET) && !J.is(i, j, CT_SOLID)) active++;
   std::vector<std::pair<int, int>> parts;
   const long per = std::max<long>(1, active / std::max(1, num_parts));
   long cnt = 0;
   int start = 0;
   for (int i = 0; i < J.nx; i++) {
     for (int j = 0; j < J.ny; j++) {
-      if (J.at(i, j).is(CT_NODE_IS_SET) && !J.at(i, j).is(CT_SOLID)) {
+      if (J.is(i, j, CT_NODE_IS_SET) && !J.is(i, j, CT_SOLID)) {
         cnt++;
         if (cnt >= per) {
           parts.push_back({start, i + 1});
@@ -1316,9 +1392,10 @@ void Case::set_sources(int iter) {
   for (auto& s : cfg.sources) {
     if (iter < s.start_iter) continue;
     const int DX = s.sx - s.ex, DY = s.sy - s.ey;
+    CellRecord scratch;   // a source cell of another strip: its writes go nowhere
     auto at = [&](unsigned x, unsigned y) -> CellRecord& {
       if (!J.in(x, y)) throw DeckError("gas source outside the computation area");
-      return J.at((int)x, (int)y);
+      return J.resident(x) ? J.at((int)x, (int)y) : scratch;
     };
     if (DX == 0 && DY == 0) {
       CellRecord& n = at(s.sx, s.sy);
@@ -1366,6 +1443,31 @@ void Case::set_sources(int iter) {
       for (int i = 0; i != DY + SKY; i += SKY) apply(at((unsigned)(s.sx + i * dF * SKX), (unsigned)(s.sy + i * SKY)), false);
     }
   }
+}
+
+std::vector<std::pair<int, int>> balanced_columns(const Field& J, int nparts) {
+  const int nx = J.nx;
+  if (nparts <= 1) return {{0, nx}};
+  if (nparts > nx) throw std::runtime_error("more strips than columns");
+  std::vector<double> cum(nx + 1, 0.0);
+  for (int i = 0; i < nx; i++) {
+    double a = 0;
+    for (int j = 0; j < J.ny; j++) a += J.is(i, j, CT_SOLID) ? 0.0 : 1.0;
+    cum[i + 1] = cum[i] + a;
+  }
+  const double total = cum[nx];
+  std::vector<int> cuts{0};
+  for (int k = 1; k < nparts; k++) {
+    const double target = total * k / nparts;
+    int c = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
+    c = std::max(c, cuts.back() + 1);
+    c = std::min(c, nx - (nparts - k));
+    cuts.push_back(c);
+  }
+  cuts.push_back(nx);
+  std::vector<std::pair<int, int>> out;
+  for (int k = 0; k < nparts; k++) out.push_back({cuts[k], cuts[k + 1]});
+  return out;
 }
 
 int Config::num_active_eq() const { return NEQ; }

@@ -355,29 +355,5 @@ RankEnv RankEnv::from_environ() {
   return e;
 }
 
-std::vector<std::pair<int, int>> balanced_columns(const Field& J, int nparts) {
-  const int nx = J.nx;
-  if (nparts <= 1) return {{0, nx}};
-  if (nparts > nx) throw std::runtime_error("more strips than columns");
-  std::vector<double> cum(nx + 1, 0.0);
-  for (int i = 0; i < nx; i++) {
-    double a = 0;
-    for (int j = 0; j < J.ny; j++) a += J.at(i, j).is(CT_SOLID) ? 0.0 : 1.0;
-    cum[i + 1] = cum[i] + a;
-  }
-  const double total = cum[nx];
-  std::vector<int> cuts{0};
-  for (int k = 1; k < nparts; k++) {
-    const double target = total * k / nparts;
-    int c = (int)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-    c = std::max(c, cuts.back() + 1);
-    c = std::min(c, nx - (nparts - k));
-    cuts.push_back(c);
-  }
-  cuts.push_back(nx);
-  std::vector<std::pair<int, int>> out;
-  for (int k = 0; k < nparts; k++) out.push_back({cuts[k], cuts[k + 1]});
-  return out;
-}
 
 }  // namespace hf2d

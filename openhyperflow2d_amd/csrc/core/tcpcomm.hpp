@@ -63,8 +63,5 @@ struct RankEnv {
   static RankEnv from_environ();
 };
 
-// [gi0, gi1) per rank with about equal active (non-solid) cells per strip:
-// the same cut as parallel/strips.py balanced_columns
-std::vector<std::pair<int, int>> balanced_columns(const Field& J, int nparts);
 
 }  // namespace hf2d

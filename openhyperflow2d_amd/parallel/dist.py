@@ -39,8 +39,6 @@ def init_from_env(backend: Optional[str] = None):
 class DistributedSimulation:
     """A strip of a deck run on this rank."""
 
-    SCATTER_CHUNK = 8 << 20   # bytes per message of the strip scatter
-
     def __init__(self, deck_text: str, backend: str = "gpu", *, rank: int = 0, world: int = 1,
                  device: int = 0, semantics: str = "mpi", fused: bool = True, lean: bool = True, parts=None,
                  workdir: str = ".", use_checkpoint: bool = False, transport: Optional[str] = None):
@@ -50,7 +48,7 @@ class DistributedSimulation:
         self.hf = hf
         self.rank, self.world = rank, world
         if world > 1:
-            self.case, self.parts = self._scatter_case(deck_text, workdir, use_checkpoint, semantics, parts)
+            self.case, self.parts = self._window_case(deck_text, workdir, use_checkpoint, semantics, parts)
         else:
             self.case = hf.Case.from_deck(deck_text, workdir, use_checkpoint)
             self.case.set_semantics(semantics)
@@ -79,57 +77,31 @@ class DistributedSimulation:
             # each side on the host (outputs are written per strip, stripio.cpp)
             self.case.trim_to_columns(gi0 - 1, gi1 + 1)
 
-    def _scatter_case(self, deck_text, workdir, use_checkpoint, semantics, parts):
-        """Rank 0 pre-processes the deck once and sends every rank its strip
-        (Case.pack_strip: its columns plus one ghost column each side and the
-        per-case data), as the reference's rank 0 sends each rank its
-        subdomain (hf2d_start.cpp:143-205).  No other rank builds the whole
-        1248 B/cell field; rank 0 frees it after the scatter.  The blobs go
-        one at a time over a host (gloo) group."""
-        import torch
+    def _window_case(self, deck_text, workdir, use_checkpoint, semantics, parts):
+        """Strip-local pre-processing: no rank ever holds the whole field
+        (SURVEY 5.7).  Every rank runs the pre-processor's geometry over the
+        whole grid on a 16 B/cell flag plane and builds the 1248 B records of
+        its own columns (+ one ghost column each side) only
+        (Case.from_deck_window); a restart reads the rank's slab of the .hf2d.
+        The reference instead pre-processes on rank 0 and sends each rank its
+        subdomain (hf2d_start.cpp:115-116,143-205).  The strips come from a
+        flags-only pass (Case.partition_deck), identical on every rank, and
+        the whole-field eligibility facts from every strip's part, gathered
+        in rank order over a host (gloo) group."""
         import torch.distributed as dist
 
         rank, world = self.rank, self.world
+        if not parts:
+            parts = self.hf.Case.partition_deck(deck_text, workdir, use_checkpoint, world)
+        parts = [tuple(p) for p in parts]
+        a, b = parts[rank]
+        nx = parts[-1][1]
+        case = self.hf.Case.from_deck_window(deck_text, workdir, use_checkpoint, max(a - 1, 0), min(b + 1, nx))
+        case.set_semantics(semantics)
         grp = None if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
-        if rank == 0:
-            full = self.hf.Case.from_deck(deck_text, workdir, use_checkpoint)
-            full.set_semantics(semantics)
-            parts = parts or balanced_columns(np.asarray(full.field("solid")), world)
-            nx = full.nx
-        obj = [parts if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=grp)
-        parts = [tuple(p) for p in obj[0]]
-        chunk = self.SCATTER_CHUNK
-        if rank == 0:
-            buf = torch.empty(chunk, dtype=torch.uint8)
-            for r in range(1, world):
-                a, b = parts[r]
-                a, b = max(a - 1, 0), min(b + 1, nx)
-                hdr = torch.frombuffer(bytearray(full.pack_strip_header(a, b)), dtype=torch.uint8)
-                dist.send(torch.tensor([hdr.numel()], dtype=torch.int64), r, group=grp)
-                dist.send(hdr, r, group=grp)
-                n = full.strip_payload_bytes(a, b)
-                for off in range(0, n, chunk):
-                    k = min(chunk, n - off)
-                    full.read_strip_payload(a, b, off, buf[:k].numpy())
-                    dist.send(buf[:k], r, group=grp)
-            a, b = parts[0]
-            case = self.hf.Case.unpack_strip(full.pack_strip(max(a - 1, 0), min(b + 1, nx)))
-            del full
-        else:
-            n = torch.zeros(1, dtype=torch.int64)
-            dist.recv(n, 0, group=grp)
-            hdr = torch.empty(int(n.item()), dtype=torch.uint8)
-            dist.recv(hdr, 0, group=grp)
-            case = self.hf.Case.unpack_strip_header(hdr.numpy())
-            a, b = case.resident_columns
-            total = case.strip_payload_bytes(a, b)
-            buf = torch.empty(min(chunk, max(total, 1)), dtype=torch.uint8)
-            for off in range(0, total, chunk):
-                k = min(chunk, total - off)
-                dist.recv(buf[:k], 0, group=grp)
-                case.write_strip_payload(off, buf[:k].numpy())
-            del buf
+        facts = [None] * world
+        dist.all_gather_object(facts, case.facts_part(), group=grp)
+        case.merge_facts(facts)
         if grp is not None:
             dist.destroy_process_group(grp)
         return case, parts

@@ -6,6 +6,9 @@
 #   bash tools/gpu_suite.sh configs          bench.py for every BASELINE config
 #   bash tools/gpu_suite.sh prof [ARGS...]   rocprofv3 kernel trace + stats of bench.py ARGS
 #   bash tools/gpu_suite.sh pmc CTRS [ARGS]  one rocprofv3 --pmc pass (counters in CTRS, space separated)
+#   bash tools/gpu_suite.sh strips           one-GPU proxies of the 8- and 4-GPU headline strips
+#                                            (250 / 500 columns + fused xGMI mailbox exchange) and
+#                                            the same strips alone on one rank
 #   bash tools/gpu_suite.sh all              tests && bench && prof
 #
 # Every GPU step has its own time limit and the steps are chained with &&:
@@ -30,6 +33,13 @@ run_configs() {
     timeout -k 10 240 python bench.py --config $c --steps 100 --warmup 10 > gpurun_out/bench_$c.log 2>&1 || return 1
   done
 }
+run_strips() {
+  for w in 250 500; do
+    timeout -k 10 240 python tools/p2p_probe.py --nx $((w + 10)) --tail 10 --autotune --steps 2000 --warmup 200 \
+      > gpurun_out/p2p_tail$w.log 2>&1 &&
+    timeout -k 10 240 python bench.py --nx $w --steps 2000 --warmup 200 > gpurun_out/bench_nx$w.log 2>&1 || return 1
+  done
+}
 run_prof() {
   local tag=${PROF_TAG:-bench}
   (cd /tmp && export TMPDIR=/tmp &&
@@ -49,6 +59,7 @@ case $mode in
   tests) run_tests ;;
   bench) run_bench "$@" ;;
   configs) run_configs ;;
+  strips) run_strips ;;
   prof) run_prof "$@" ;;
   pmc) run_pmc "$@" ;;
   all) run_tests && run_bench && run_prof --steps 500 --warmup 50 ;;

@@ -45,9 +45,11 @@ def main():
     solvers = []
     for r, (lo, hi) in enumerate(parts):
         s = nat.DeviceSolver(cases[r], 0, lo, hi)
-        s.init_local(group, r)
         if a.autotune:
-            print("rank %d autotune: %s" % (r, s.autotune().strip().splitlines()[-1]), flush=True)
+            # before the rank joins the group, as in a multi-GPU run
+            # (DistributedSimulation tunes each strip before wiring the transport)
+            print("rank %d autotune: %s" % (r, s.autotune().strip().replace("; ", "\n    ")), flush=True)
+        s.init_local(group, r)
         solvers.append(s)
     descs = [s.p2p_export(r, a.ranks) for r, s in enumerate(solvers)]
     for s in solvers:
