@@ -283,6 +283,7 @@ PYBIND11_MODULE(_hf2d, m) {
         return field_scalar(c.J, n);
       })
       .def_property_readonly("mech_mode", [](const Case& c) { return c.cfg.mech_mode(); })
+      .def_property_readonly("chem_tmin", [](const Case& c) { return c.cfg.chem_tmin; })
       .def_property_readonly("mech_species", [](const Case& c) {
         return c.cfg.mech ? c.cfg.mech->species : std::vector<std::string>{};
       })
@@ -759,6 +760,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lnm_ti", &DeviceSolver::lnm_ti)
       .def("lnm_trace_fetch", &DeviceSolver::lnm_trace_fetch, py::call_guard<py::gil_scoped_release>())
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
+      .def_readonly("lns_fx_steps", &DeviceSolver::lns_fx_steps)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())

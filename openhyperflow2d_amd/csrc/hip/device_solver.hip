@@ -398,6 +398,63 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
   return true;
 }
 
+// Tail of a step kernel with the exchange fused in (thread 0 of every
+// workgroup, after the workgroup's mailbox stores and dt MIN): the last
+// workgroup to finish publishes this rank's step (its dt to every peer, then
+// flag seq_prev + 1), waits (bounded) for every peer's flag of the same step
+// and folds their dt into the slot the next step reads.
+__device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
+                                        unsigned long long seq_prev) {
+  // the workgroup barrier drained every wave's mailbox stores; drain the dt
+  // atomic before counting this workgroup as done
+  vm_drain();
+  // completion count in two levels (one counter per dt shard, then one for
+  // the shards): a single counter serialises every workgroup's returning
+  // atomic at the memory side
+  const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
+  const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
+  unsigned* cs = X.done + sh * FX_DONE_STRIDE;
+  unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
+  bool last = false;
+  if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
+    __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = true;
+    }
+  }
+  if (!last) return;
+  // last workgroup: publish this rank's step, then fold the peers'
+  const unsigned long long sn = seq_prev + 1;
+  const int pn = (int)(sn & 1);
+  double d = dt_get_fresh(sc, slot_next);
+  for (int q = 0; q < X.nranks; q++)
+    if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
+  vm_drain();
+  for (int q = 0; q < X.nranks; q++)
+    if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
+  for (int q = 0; q < X.nranks && ok; q++) {
+    if (q == X.rank) continue;
+    long spins = 0;
+    while (__hip_atomic_load(&X.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sn) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > P2P_SPIN_LIMIT) {
+        atomicOr(&sc->neg_T, 2);
+        ok = false;
+        break;
+      }
+    }
+    // acquire the peer's publication: its dt and mailbox stores (released
+    // by its vmcnt drain before the flag) are visible to every load ordered
+    // after this one, here and in later kernels
+    if (ok) (void)p2p_acquire(&X.my_flags[q]);
+    if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
+  }
+  __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *X.seq = sn;
+}
+
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
 // In-kernel phase trace (TR): thread 0 of every workgroup records the
 // 100 MHz s_memrealtime clock at entry, after the LDS staging barrier, when
@@ -571,56 +628,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       o[6] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
       o[7] = blockIdx.x;
     }
-    if (FX) {
-      // the barrier above drained every wave's mailbox stores; drain the
-      // dt atomic before counting this workgroup as done
-      vm_drain();
-      // completion count in two levels (one counter per dt shard, then one
-      // for the shards): a single counter serialises every workgroup's
-      // returning atomic at the memory side
-      const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
-      const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
-      unsigned* cs = X.done + sh * FX_DONE_STRIDE;
-      unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
-      bool last = false;
-      if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
-        __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
-          __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          last = true;
-        }
-      }
-      if (last) {   // last workgroup: publish this rank's step, then fold the peers'
-        const unsigned long long sn = seq_prev + 1;
-        const int pn = (int)(sn & 1);
-        double d = dt_get_fresh(sc, slot_next);
-        for (int q = 0; q < X.nranks; q++)
-          if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
-        vm_drain();
-        for (int q = 0; q < X.nranks; q++)
-          if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        bool ok = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
-        for (int q = 0; q < X.nranks && ok; q++) {
-          if (q == X.rank) continue;
-          long spins = 0;
-          while (__hip_atomic_load(&X.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sn) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > P2P_SPIN_LIMIT) {
-              atomicOr(&sc->neg_T, 2);
-              ok = false;
-              break;
-            }
-          }
-          // acquire the peer's publication: its dt and mailbox stores
-          // (released by its vmcnt drain before the flag) are visible to
-          // every load ordered after this one, here and in later kernels
-          if (ok) (void)p2p_acquire(&X.my_flags[q]);
-          if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
-        }
-        __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *X.seq = sn;
-      }
-    }
+    if (FX) fx_tail(X, sc, slot_next, seq_prev);
   }
 }
 
@@ -738,12 +746,19 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
 // ---------------------------------------------------------------------------
 constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
 
-template <bool RES, int MODE, int TURB>
+// FX: the multi-GPU exchange fused in (xGMI mailboxes): the cells of the
+// strip's first / last two columns store this step's HALO_LNS values (Lc:
+// the post-step pointers, DeviceSolver::halo_list) into the neighbour's
+// mailbox, the last workgroup publishes the step and folds the peers' dt
+// (fx_tail); hf2d_p2p_unpack then fills the ghost columns.
+template <bool RES, int MODE, int TURB, bool FX = false>
 __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials,
-                                              int part) {
+                                              int part, const FusedX& X = FusedX{}, const ColList* Lc = nullptr) {
   extern __shared__ real lds[];
   constexpr int NL = Lns<MODE>::NL;
+  unsigned long long seq_prev = 0;
+  if (FX) seq_prev = *X.seq;
   // part: 0 every tile, 1 / 2 the edge / interior tiles (comm overlap)
   const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   apply_dt(P, sc, slot);
@@ -899,6 +914,20 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
                                                          &f2);
     }
   }
+  if (FX && mine) {
+    // an edge cell's new HALO_LNS values (its own stores above, read back
+    // after they completed) -> the neighbour's mailbox of parity seq_prev + 1
+    const int pn = (int)((seq_prev + 1) & 1);
+    for (int side = 0; side < 2; side++) {
+      const int o = side == 0 ? i - P.i0 : P.i1 - 1 - i;
+      if (!(X.sides & (1 << side)) || o > 1) continue;
+      vm_drain();
+      real* mb = side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap;
+      for (int f = 0; f < Lc->nf; f++)
+        if (Lc->o[f] == o) p2p_store(mb + (long)f * P.ny + j, Lc->f[f][idx]);
+      vm_drain();
+    }
+  }
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
@@ -915,6 +944,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
     dt_min(sc, slot_next, m);
+    if (FX) fx_tail(X, sc, slot_next, seq_prev);
   }
 }
 
@@ -923,6 +953,37 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
                                                         int slot, int slot_next, int serial, ResidualPack* partials,
                                                         int part) {
   lns_step_body<RES, MODE, TURB>(P, a, T, sc, slot, slot_next, serial, partials, part);
+}
+// the same step with the xGMI mailbox exchange fused in (the register
+// budgets of the default kernels: laminar unbounded, k-eps / SST / SA 3
+// waves per SIMD)
+template <bool RES, int MODE, int TURB>
+__global__ __launch_bounds__(BLOCK) void hf2d_lns_step_fx(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
+                                                           int slot, int slot_next, int serial,
+                                                           ResidualPack* partials, FusedX X, ColList Lc) {
+  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc);
+}
+template <bool RES, int MODE, int TURB>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void hf2d_lns_step_fx3(
+    StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
+    ResidualPack* partials, FusedX X, ColList Lc) {
+  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc);
+}
+
+// Ghost columns of the HALO_LNS group from the mailbox of the step the fused
+// tail just completed (it waited for every peer's flag): entry f of side s
+// goes to ghost column ghostL - o[f] / ghostR + o[f] (grid-stride, one value
+// per thread).
+__global__ __launch_bounds__(BLOCK) void hf2d_p2p_unpack(ColList Lc, int ghostL, int ghostR, int ny, int cnt,
+                                                        FusedX X) {
+  const int par = (int)(*X.seq & 1);
+  for (long t = (long)blockIdx.x * BLOCK + threadIdx.x; t < 2L * cnt; t += (long)gridDim.x * BLOCK) {
+    const int side = t < cnt ? 0 : 1;
+    if (!(X.sides & (1 << side))) continue;
+    const int tt = (int)(t - (long)side * cnt), f = tt / ny, j = tt - f * ny;
+    const real v = p2p_load(X.my_recv + ((long)par * 2 + side) * X.cap + tt);
+    Lc.f[f][(long)(side == 0 ? ghostL - Lc.o[f] : ghostR + Lc.o[f]) * ny + j] = v;
+  }
 }
 // register budget of OCC waves per SIMD (DeviceSolver::lns_occ, measured)
 template <bool RES, int MODE, int OCC, int TURB = 2>
@@ -1596,6 +1657,14 @@ static const LnsK kLns[4][2][3] = {
      {hf2d_lns_step<true, SK_SGT, 3>, hf2d_lns_step<true, SK_SGT, 3>, hf2d_lns_step<true, SK_SGT, 3>}},
     {{hf2d_lns_step<false, SK_SGT, 4>, hf2d_lns_step_occ<false, SK_SGT, 3, 4>, hf2d_lns_step_occ<false, SK_SGT, 5, 4>},
      {hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>}}};
+
+using LnsFxK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*, FusedX, ColList);
+// [laminar, k-eps, SST, SA][residual] (the default kernels' register budgets)
+static const LnsFxK kLnsFx[4][2] = {
+    {hf2d_lns_step_fx<false, SK_SGL, 2>, hf2d_lns_step_fx<true, SK_SGL, 2>},
+    {hf2d_lns_step_fx3<false, SK_SGT, 2>, hf2d_lns_step_fx<true, SK_SGT, 2>},
+    {hf2d_lns_step_fx3<false, SK_SGT, 3>, hf2d_lns_step_fx<true, SK_SGT, 3>},
+    {hf2d_lns_step_fx3<false, SK_SGT, 4>, hf2d_lns_step_fx<true, SK_SGT, 4>}};
 
 struct DevBuf {
   std::vector<void*> ptrs;
@@ -3652,13 +3721,40 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // (a residual step runs the compiler's register budget)
       const int tv = !t2 ? 0 : lns_turb == 3 ? 2 : lns_turb == 4 ? 3 : 1;
       const LnsK lk = kLns[tv][want_res][want_res ? 0 : (occ == 5 ? 2 : occ == 3 ? 1 : 0)];
+      // xGMI mailboxes: the exchange fused into the tile kernel (edge cells
+      // push their HALO_LNS values to the neighbour, the last workgroup
+      // publishes the step and folds the peers' dt), then one unpack kernel;
       // RCCL / in-process transports: edge tiles first, their halo on the comm
       // stream while the interior tiles compute, then the dt MIN (as the
-      // inviscid tile kernel; the xGMI mailbox exchange folds the dt into its
-      // handshake and runs after the step)
-      lns_split = comm_overlap && !m.p2p.on && (m.comm || m.local) && m.nranks > 1 && !want_res && T.nbi >= 3 &&
-                  cs.cfg.isAdiabaticWall;
-      if (lns_split) {
+      // inviscid tile kernel)
+      ColList Lc{};
+      lns_fx = m.p2p.on && p2p_fuse && m.nranks > 1;
+      if (lns_fx) {   // the HALO_LNS pointers of the post-step buffers
+        sbuf = 1 - sbuf, pbuf = 1 - pbuf, cbuf = 1 - cbuf, dsbuf = 1 - dsbuf;
+        std::vector<real*> fl;
+        std::vector<unsigned char> fo;
+        halo_fields(CpuSolver::HALO_LNS, fl, fo, false);
+        sbuf = 1 - sbuf, pbuf = 1 - pbuf, cbuf = 1 - cbuf, dsbuf = 1 - dsbuf;
+        if (fl.size() > (size_t)MAX_HALO_FIELDS || (long)fl.size() * h.ny > m.halo_cap)
+          throw std::runtime_error("lean N-S halo exceeds the mailbox capacity");
+        Lc.nf = (int)fl.size();
+        for (int k = 0; k < Lc.nf; k++) {
+          Lc.f[k] = fl[k];
+          Lc.o[k] = fo[k];
+        }
+      }
+      lns_split = !lns_fx && comm_overlap && !m.p2p.on && (m.comm || m.local) && m.nranks > 1 && !want_res &&
+                  T.nbi >= 3 && cs.cfg.isAdiabaticWall;
+      if (lns_fx) {
+        hipLaunchKernelGGL(kLnsFx[tv][want_res ? 1 : 0], dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
+                           slot_next, serial, m.partials, fused_args(), Lc);
+        HIP_CHECK(hipGetLastError());
+        const int cnt = Lc.nf * h.ny;
+        hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
+                           dim3(BLOCK), 0, st, Lc, l_off - 1, l_off + (gi1 - gi0), h.ny, cnt, fused_args());
+        ghost_stale = true;   // lean representation in the ghosts
+        lns_fx_steps++;
+      } else if (lns_split) {
         if (!m.comm_stream) {
           HIP_CHECK(hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking));
           HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
@@ -3706,6 +3802,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   // new-state halo + global dt (MIN over ranks into the next slot)
   if (fx_step) {
     fx_pending = true;   // exchanged inside the tile kernel
+  } else if (lns_fx) {
+    lns_fx = false;   // exchanged inside the lean N-S kernel + unpacked
   } else if (lns_split) {
     lns_split = false;   // exchanged above, overlapped with the interior tiles
   } else if ((m.comm || m.local || m.p2p.on) && m.nranks > 1) {

@@ -112,6 +112,8 @@ class DeviceSolver : public SolverBase {
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
   bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
+  bool lns_fx = false;      // this lean N-S step exchanged through the fused mailbox kernel
+  long lns_fx_steps = 0;    // lean N-S steps with the fused xGMI mailbox exchange
   long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
   void halo_fields(int group, std::vector<real*>& f, bool full = false) const;

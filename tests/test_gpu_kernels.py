@@ -224,6 +224,7 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
         stats["overlap_steps"] = [s.overlap_steps for s in solvers]
         stats["lns_steps"] = [s.lns_steps for s in solvers]
         stats["lnm_steps"] = [s.lnm_steps for s in solvers]
+        stats["lns_fx_steps"] = [s.lns_fx_steps for s in solvers]
     out = {}
     for f in fields:
         full = None
@@ -309,14 +310,17 @@ def test_compact_state_halo_matches_single_gpu(gpu, deck, p2p):
 
 
 @pytest.mark.parametrize("deck,nranks,p2p", [("step", 3, False), ("resonator", 4, False), ("sst_plate", 3, False),
-                                            ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True)])
+                                            ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True),
+                                            ("resonator", 3, "fx"), ("step", 2, "fx"), ("sst_plate", 3, "fx")])
 def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     """Lean N-S / mechanism tiles on strips (two ghost columns: the tile
     evaluates the fill of the first one, which reads the second; HALO_LNS
     carries the next lean step's inputs of both, the second column only what
     a neighbour's fill reads) == one GPU bit for bit, across residual steps,
     downloads (materialize) and re-entry, over the in-process and the xGMI
-    mailbox transports."""
+    mailbox transports; p2p="fx": the mailbox exchange fused into the lean
+    N-S tile kernel (edge cells push, the last workgroup publishes and folds
+    the dt, hf2d_p2p_unpack fills the ghosts) -- asserted to have run."""
     fields = list(FIELDS) + ["k", "mu", "mu_t"]
     if deck == "step":
         text = decks.step(240, 80, nmax=10 ** 6, nout=10 ** 5)
@@ -331,10 +335,12 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
         fields += ["S7", "S8", "Y:H2", "Y:O2", "Y:OH", "Y:H2O"]
     schedule = [(4, True), (17, False), (5, True), (14, False)]
     stats = {}
-    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=p2p, fuse=False, stats=stats,
-                               fields=fields)
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=bool(p2p), fuse=p2p == "fx",
+                               stats=stats, fields=fields)
     lean_steps = stats["lnm_steps"] if deck == "scramjet" else stats["lns_steps"]
     assert min(lean_steps) > 0, stats
+    if p2p == "fx":
+        assert min(stats["lns_fx_steps"]) > 0, stats
     if not p2p and deck != "scramjet":   # in-process transport: edge tiles first, halo overlapped
         assert min(stats["overlap_steps"]) > 0, stats
     ref = gpu.Simulation(text, "gpu")

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=24)
     ap.add_argument("--nx", type=int, default=0)
     ap.add_argument("--ny", type=int, default=0)
+    ap.add_argument("--nofuse", action="store_true", help="separate exchange kernel (hf2d_p2p_xchg) after each step")
     args = ap.parse_args()
 
     import numpy as np
@@ -56,22 +57,26 @@ def main():
         s = nat.DeviceSolver(cases[r], 0, a, b)
         s.init_local(group, r)
         solvers.append(s)
-    descs = [s.p2p_export(r, n) for r, s in enumerate(solvers)]
-    for s in solvers:
-        s.p2p_import(descs)
-    blobs = [None] * n
+    if n > 1:
+        descs = [s.p2p_export(r, n) for r, s in enumerate(solvers)]
+        for s in solvers:
+            s.p2p_import(descs)
+            # the exchange fused into the tile kernels, as DistributedSimulation
+            # sets it (HF2D_P2P_FUSE=0: separate exchange kernel)
+            s.p2p_fuse = not args.nofuse
+        blobs = [None] * n
 
-    def probe(r):
-        blobs[r] = solvers[r].p2p_probe()
+        def probe(r):
+            blobs[r] = solvers[r].p2p_probe()
 
-    th = [threading.Thread(target=probe, args=(r,), daemon=True) for r in range(n)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=120)
-    ok, why = nat.DeviceSolver.p2p_probe_ok(blobs, 0)
-    if not ok:
-        raise SystemExit("p2p probe failed: %s" % why)
+        th = [threading.Thread(target=probe, args=(r,), daemon=True) for r in range(n)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        ok, why = nat.DeviceSolver.p2p_probe_ok(blobs, 0)
+        if not ok:
+            raise SystemExit("p2p probe failed: %s" % why)
     errors = []
 
     def run(s, k):
@@ -103,6 +108,7 @@ def main():
         "strips": [[int(a), int(b)] for a, b in parts],
         "lean_ns_steps": [int(s.lns_steps) for s in solvers], "lean_mech_steps": [int(s.lnm_steps) for s in solvers],
         "graph_launches": [int(s.graph_launches) for s in solvers],
+        "fused_exchange": not args.nofuse, "lean_ns_fx_steps": [int(s.lns_fx_steps) for s in solvers],
         "summary_dt": solvers[0].summary()["dt"],
     }), flush=True)
 

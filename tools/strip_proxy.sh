@@ -10,4 +10,5 @@ run() {  # tag args...
      -- python3 "$R/tools/strip_proxy.py" "$@" > "$R/gpurun_out/proxyprof_$tag.log" 2>&1)
 }
 export GPU_MAX_HW_QUEUES=16
-run reso4 --config resonator --ranks 4 --steps 60 && run scram8 --config scramjet --ranks 8 --steps 12 --warmup 12
+run reso4 --config resonator --ranks 4 --steps 60 && run reso4x --config resonator --ranks 4 --steps 60 --nofuse && \
+run reso1 --config resonator --ranks 1 --steps 60 && run scram8 --config scramjet --ranks 8 --steps 12 --warmup 12
