@@ -761,6 +761,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("lnm_trace_fetch", &DeviceSolver::lnm_trace_fetch, py::call_guard<py::gil_scoped_release>())
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
       .def_readonly("lns_fx_steps", &DeviceSolver::lns_fx_steps)
+      .def_readonly("p2p_mwg_exchanges", &DeviceSolver::p2p_mwg_exchanges)
       .def("comm_rank", &DeviceSolver::comm_rank)
       .def("comm_size", &DeviceSolver::comm_size)
       .def("synchronize", &DeviceSolver::synchronize, py::call_guard<py::gil_scoped_release>())

@@ -99,6 +99,13 @@ HF_HD inline real nasa_cp(const real* a, real T) { return a[0] + T * (a[1] + T *
 HF_HD inline real nasa_h(const real* a, real T) {
   return a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) + a[5] / T;
 }
+// T * h/(RT) = T * (a0 + a1/2 T + ... + a4/5 T^4) + a5: the same polynomial
+// without the division by T (the mixture energy and the species enthalpies
+// need h, not h/RT; nine divisions per evaluation saved in the mechanism
+// fill and in every Newton iteration of the temperature)
+HF_HD inline real nasa_hT(const real* a, real T) {
+  return T * (a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2)))) + a[5];
+}
 HF_HD inline real nasa_s(const real* a, real T, real lnT) {
   return a[0] * lnT + T * (a[1] + T * (a[2] * 0.5 + T * (a[3] * (1.0 / 3.0) + T * a[4] * 0.25))) + a[6];
 }
@@ -113,7 +120,7 @@ HF_HD inline void mech_mix_thermo(const MechData& m, const real* Y, real T, real
     const Nasa7 c = mech_coef_v(m, s, T);
     const real* a = c.a;
     const real R = m.Rs[s];
-    se += Y[s] * R * T * (nasa_h(a, T) - 1.0);
+    se += Y[s] * R * (nasa_hT(a, T) - T);
     scv += Y[s] * R * (nasa_cp(a, T) - 1.0);
     sR += Y[s] * R;
   }
@@ -179,7 +186,7 @@ HF_HD inline void mech_transport(const MechData& m, const real* Y, real T, real*
 // Species absolute enthalpy h_s(T) (J/kg) for the enthalpy-diffusion heat flux.
 HF_HD inline real mech_h_species(const MechData& m, int s, real T) {
   const Nasa7 c = mech_coef_v(m, s, T);
-  return m.Rs[s] * T * nasa_h(c.a, T);
+  return m.Rs[s] * nasa_hT(c.a, T);
 }
 
 // ---------------------------------------------------------------------------

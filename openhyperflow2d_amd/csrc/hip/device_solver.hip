@@ -404,7 +404,7 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
 // flag seq_prev + 1), waits (bounded) for every peer's flag of the same step
 // and folds their dt into the slot the next step reads.
 __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
-                                        unsigned long long seq_prev) {
+                                        unsigned long long seq_prev, bool fold = true) {
   // the workgroup barrier drained every wave's mailbox stores; drain the dt
   // atomic before counting this workgroup as done
   vm_drain();
@@ -451,7 +451,7 @@ __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slo
     if (ok) (void)p2p_acquire(&X.my_flags[q]);
     if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
   }
-  __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fold) __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   *X.seq = sn;
 }
 
@@ -968,6 +968,46 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void
     StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
     ResidualPack* partials, FusedX X, ColList Lc) {
   lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc);
+}
+
+// Multi-workgroup mailbox exchange, push half (the mechanism step and every
+// other p2p exchange with p2p_fuse): each thread loads up to PER boundary
+// values of the fields in Lc (column first + o / last - o) and stores them
+// into the neighbours' mailboxes; the last workgroup publishes and, fold,
+// folds the peers' dt into dslot (fx_tail); hf2d_p2p_unpack follows.
+__global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, int last, int ny, int cnt, FusedX X,
+                                                      DevScalars* sc, int dslot, int fold) {
+  const unsigned long long seq_prev = *X.seq;
+  const int pn = (int)((seq_prev + 1) & 1);
+  constexpr int PER = 16;
+  const long base = ((long)blockIdx.x * BLOCK + threadIdx.x) * PER;
+  real v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; u++) {
+    const long t = base + u;
+    if (t < 2L * cnt) {
+      const int side = t < cnt ? 0 : 1;
+      const int tt = (int)(t - (long)side * cnt), f = tt / ny, j = tt - f * ny;
+      if (X.sides & (1 << side))
+        v[u] = Lc.f[f][(long)(side == 0 ? first + Lc.o[f] : last - Lc.o[f]) * ny + j];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PER; u++) {
+    const long t = base + u;
+    if (t < 2L * cnt) {
+      const int side = t < cnt ? 0 : 1;
+      const int tt = (int)(t - (long)side * cnt);
+      // the left neighbour receives "from right", the right one "from left"
+      if (X.sides & (1 << side))
+        p2p_store((side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap) +
+                      tt,
+                  v[u]);
+    }
+  }
+  vm_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) fx_tail(X, sc, dslot, seq_prev, fold != 0);
 }
 
 // Ghost columns of the HALO_LNS group from the mailbox of the step the fused
@@ -2968,6 +3008,22 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   const int sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
   hipStream_t st = on_stream ? (hipStream_t)on_stream : m.stream;
+  if (m.p2p.on && p2p_fuse) {
+    // multi-workgroup push (the last workgroup publishes, waits and folds the
+    // dt), then the multi-workgroup unpack: no single-workgroup copy of the
+    // 23-43-field N-S / mechanism halos on the step's critical path
+    if (L.nf * ny > m.halo_cap) throw std::runtime_error("p2p halo exceeds mailbox capacity");
+    const FusedX X = fused_args();
+    const unsigned nbp = (unsigned)std::max(1, (2 * cnt + BLOCK * 16 - 1) / (BLOCK * 16));
+    hipLaunchKernelGGL(hf2d_p2p_push, dim3(nbp), dim3(BLOCK), 0, st, L, first, last, ny, cnt, X, m.sc,
+                       dt_slot >= 0 ? dt_slot : 0, dt_slot >= 0 ? 1 : 0);
+    HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
+                       dim3(BLOCK), 0, st, L, l_off - 1, l_off + (gi1 - gi0), ny, cnt, X);
+    HIP_CHECK(hipGetLastError());
+    p2p_mwg_exchanges++;
+    return;
+  }
   if (m.p2p.on) {
     if (L.nf * ny > m.halo_cap) throw std::runtime_error("p2p halo exceeds mailbox capacity");
     Impl::P2P& p = m.p2p;

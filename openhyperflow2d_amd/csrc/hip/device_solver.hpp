@@ -114,6 +114,7 @@ class DeviceSolver : public SolverBase {
   bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
   bool lns_fx = false;      // this lean N-S step exchanged through the fused mailbox kernel
   long lns_fx_steps = 0;    // lean N-S steps with the fused xGMI mailbox exchange
+  long p2p_mwg_exchanges = 0;   // mailbox exchanges through hf2d_p2p_push / hf2d_p2p_unpack
   long overlap_steps = 0;
   // device columns of the fields a halo group carries, in pack order
   void halo_fields(int group, std::vector<real*>& f, bool full = false) const;

@@ -72,24 +72,23 @@ def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
     cstar = rhos * mus / (rhoe * mue)
     lam = 0.664 * np.sqrt(cstar) / np.sqrt(rex)
     turb = 0.0592 * (rhos / rhoe) * (rhos * Ue * x / mus) ** -0.2
-    # Effective wall stress: the DEEPS predictor blends every conserved
-    # variable with its neighbours' mean by (1 - beta), a diffusion
-    # (1 - beta) dyy / 2 * dy^2 / dt (dyy = dx / (dx + dy)) acting in parallel
-    # with the molecular one; in the viscous sublayer it carries part of the
-    # wall stress (mu_w dU/dy sees only the rest), beyond it mu_t dominates.
-    # In a zero-pressure-gradient layer the total stress is ~ tau_w through
-    # the buffer layer, so the largest modelled stress (mu + mu_t) dU/dy within
-    # y+ < 150 is the wall stress the discrete momentum balance carries
-    # (profiles/flat_plate_validation.md).
+    # Diagnostic only (the validation asserts on the molecular Cf above): the
+    # modelled stress (mu + mu_t) dU/dy averaged over 30 <= y+ <= 100.  The
+    # DEEPS predictor blends every conserved variable with its neighbours'
+    # mean by (1 - beta), a diffusion (1 - beta) dyy / 2 * dy^2 / dt
+    # (dyy = dx / (dx + dy)) in parallel with the molecular one: in the
+    # viscous sublayer it carries part of the wall stress, so mu_w dU/dy sees
+    # only the rest, while in a zero-pressure-gradient layer the total stress
+    # stays ~ tau_w through the log layer (profiles/flat_plate_validation.md).
     mut = np.asarray(sim.field("mu_t"))
     uplus_tau = np.sqrt(np.abs(tau) / rho[i, 0])
     tau_eff = np.abs(tau).copy()
     for q, ii in enumerate(i):
         yplus = np.arange(ny) * dy * uplus_tau[q] * rho[ii, 0] / mu[ii, 0]
-        jm = int(np.searchsorted(yplus, 150.0))
-        for j in range(1, min(jm, ny - 1)):
-            t = (mu[ii, j] + mut[ii, j]) * (U[ii, j + 1] - U[ii, j - 1]) / (2 * dy)
-            tau_eff[q] = max(tau_eff[q], t)
+        band = [j for j in range(1, ny - 1) if 30.0 <= yplus[j] <= 100.0]
+        if band:
+            tau_eff[q] = float(np.mean([(mu[ii, j] + mut[ii, j]) * (U[ii, j + 1] - U[ii, j - 1]) / (2 * dy)
+                                        for j in band]))
     cf_eff = np.sign(cf) * tau_eff / (0.5 * rhoe * Ue * Ue)
     return {"x": x, "Re_x": rex, "Cf": cf, "Cf_eff": cf_eff, "Cf_lam": lam, "Cf_turb": turb,
             "Cf_turb_vd2": van_driest_ii(rex, Me, Te, Tw), "Mach": np.full_like(x, Me), "Tw": Tw}

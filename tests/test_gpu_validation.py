@@ -40,28 +40,34 @@ def turbulent_runs(request):
 
     if not hf.gpu_available():
         pytest.fail("GPU test requires a HIP device")
-    return {6: _run(hf, 6, 312, 750, 1e-3, 4e-5, 1e4, 5.0, cfl=0.4), 4: _run(hf, 4, 312, 750, 2e-3, 4e-5, 1e4, 2.0)}
+    return {6: _run(hf, 6, 312, 750, 1e-3, 4e-5, 1e4, 5.0, cfl=0.4), 4: _run(hf, 4, 312, 750, 2e-3, 4e-5, 1e4, 2.0),
+            "6_dy20": _run(hf, 6, 312, 1500, 1e-3, 2e-5, 1e4, 5.0, cfl=0.4)}
 
 
-def test_sst_plate_matches_the_turbulent_correlation(turbulent_runs):
+def test_sst_plate_molecular_wall_friction_and_its_grid_convergence(turbulent_runs):
     """k-omega SST (Menter's wall omega at the first cell) on a developed
-    turbulent layer, Re_x 0.7-1.3e6, CFL 0.4: the wall stress the discrete
-    momentum balance carries -- the largest modelled stress (mu + mu_t) dU/dy
-    within y+ < 150, where a zero-pressure-gradient layer holds ~tau_w --
-    is 0.8-0.85 of Schlichting's turbulent law with Eckert's reference
-    temperature, the same on grids of dy = 40 and 20 um (0.83 / 0.84).  The
-    molecular mu_w dU/dy alone is lower (0.53 / 0.65 of the law, converging
-    as dy -> 0): across the viscous sublayer the DEEPS blend's own diffusion
-    (1 - beta) dyy/2 dy^2/dt, ~0.5 nu_w here, carries the rest
-    (profiles/flat_plate_validation.md).  The layer is turbulent: Cf is 2x
-    the laminar law."""
-    r = turbulent_runs[6]
-    hi = r["Re_x"] > 7e5
-    assert (r["Cf"][hi] / r["Cf_lam"][hi]).min() > 1.6
-    eff = r["Cf_eff"][hi] / r["Cf_turb"][hi]
-    assert 0.75 < eff.mean() < 1.15, eff.mean()
-    mol = r["Cf"][hi] / r["Cf_turb"][hi]
-    assert 0.4 < mol.mean() < eff.mean(), (mol.mean(), eff.mean())
+    turbulent layer, Re_x 0.7-1.3e6, CFL 0.4, asserting on the MOLECULAR wall
+    friction mu_w dU/dy: 0.53 of Schlichting's turbulent law (Eckert's
+    reference temperature) at dy = 40 um and 0.65 at dy = 20 um -- i.e. 35-47 %
+    LOW, outside a +-15 % validation band, and converging towards the law as
+    dy -> 0 (first-order Richardson estimate ~0.77).  The deficit is the DEEPS
+    blend's own diffusion (1 - beta) dyy/2 dy^2/dt, ~0.5 nu_w at the wall here,
+    which carries part of the sublayer stress (it scales with dy / CFL;
+    profiles/flat_plate_validation.md; removing the blend near walls is
+    unstable with this explicit scheme).  The layer is turbulent: Cf is > 1.6x
+    the laminar law.  The modelled stress over 30 <= y+ <= 100 (Cf_eff) is a
+    diagnostic only."""
+    r40, r20 = turbulent_runs[6], turbulent_runs["6_dy20"]
+    hi40, hi20 = r40["Re_x"] > 7e5, r20["Re_x"] > 7e5
+    assert (r40["Cf"][hi40] / r40["Cf_lam"][hi40]).min() > 1.6
+    mol40 = float((r40["Cf"][hi40] / r40["Cf_turb"][hi40]).mean())
+    mol20 = float((r20["Cf"][hi20] / r20["Cf_turb"][hi20]).mean())
+    eff40 = float((r40["Cf_eff"][hi40] / r40["Cf_turb"][hi40]).mean())
+    msg = "molecular Cf/Cf_turb: dy 40 um %.3f, dy 20 um %.3f; band-averaged modelled stress %.3f" % (mol40, mol20, eff40)
+    assert 0.45 < mol40 < 0.62, msg
+    assert 0.56 < mol20 < 0.76, msg
+    assert mol20 - mol40 > 0.06, msg   # converging towards the correlation as dy -> 0
+    assert eff40 > mol40, msg
 
 
 def test_keps_plate_keeps_the_reference_eddy_viscosity_cap(turbulent_runs):
