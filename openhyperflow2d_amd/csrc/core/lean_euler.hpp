@@ -418,6 +418,9 @@ struct LeanTile {
   int TI, TJ, W, NC, nbi, nbj;
   int TIh;   // columns per cell layer: thread t owns (t / TJ + q * TIh, t % TJ), q < CPT
   int CPT;   // cells per thread
+  // comm-overlap launches: tile columns at the strip's right edge in the edge
+  // part (2 when the last one holds a single column and the halo carries two)
+  int ne = 1;
 };
 
 // Tile height: tj > 0 overrides (clamped to [LEAN_TILE_MIN_TJ, block]);

@@ -18,11 +18,11 @@ struct DevScalars {
   double dt_val[3];                // dt of the step that used the slot (the lean
                                    // mechanism step's fill belongs to the previous one)
   unsigned hot_cnt[3];             // lean mechanism step: reacting cells listed by the step using the slot
-  unsigned pad2;
+  unsigned hot_cnt2[3];            // ... by its interior tiles (comm-overlap steps: a second list)
   // Sharded dt MIN: every workgroup of a step used to atomicMin into ONE word,
   // and device-scope atomics to one address serialise at the memory side
-  // (~10 ns each: 800 workgroups of a small-strip step queued 7 us behind
-  // them, profiles/small_strip_r04.md).  Workgroup b min-reduces into shard
+  // (~10 ns each: the 800 workgroups of a small-strip step queued ~7 us
+  // behind them).  Workgroup b min-reduces into shard
   // b % DT_SHARDS (one 128-byte line each) instead; the value of a slot is
   // MIN(dt_bits[slot], its shards) (dt_get), and folds that publish a
   // global MIN store it into dt_bits[slot] (the shards stay >= it).

@@ -471,7 +471,7 @@ __device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memr
 // (their results feed the halo exchange); 2 the other tiles.  The grid of a
 // part launch has exactly that many workgroups (DeviceSolver comm overlap).
 __device__ inline unsigned tile_of_part(unsigned bl, int part, const LeanTile& T) {
-  if (part == 1) return bl < (unsigned)T.nbj ? bl : (unsigned)((T.nbi - 1) * T.nbj) + (bl - T.nbj);
+  if (part == 1) return bl < (unsigned)T.nbj ? bl : (unsigned)((T.nbi - T.ne) * T.nbj) + (bl - T.nbj);
   if (part == 2) return (unsigned)T.nbj + bl;
   return bl;
 }
@@ -975,8 +975,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void
 // values of the fields in Lc (column first + o / last - o) and stores them
 // into the neighbours' mailboxes; the last workgroup publishes and, fold,
 // folds the peers' dt into dslot (fx_tail); hf2d_p2p_unpack follows.
+// publish = 0: the pushes only (drained); a later hf2d_p2p_finish publishes
+// the step -- the mechanism step pushes its edge tiles' halo before its
+// interior tiles run.
 __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, int last, int ny, int cnt, FusedX X,
-                                                      DevScalars* sc, int dslot, int fold) {
+                                                      DevScalars* sc, int dslot, int fold, int publish) {
   const unsigned long long seq_prev = *X.seq;
   const int pn = (int)((seq_prev + 1) & 1);
   constexpr int PER = 16;
@@ -1006,8 +1009,15 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
     }
   }
   vm_drain();
+  if (!publish) return;
   __syncthreads();
   if (threadIdx.x == 0) fx_tail(X, sc, dslot, seq_prev, fold != 0);
+}
+
+// One workgroup: publish the step whose halo an earlier hf2d_p2p_push
+// (publish = 0) stored, wait for the peers' publication, fold their dt.
+__global__ void hf2d_p2p_finish(FusedX X, DevScalars* sc, int dslot) {
+  if (threadIdx.x == 0) fx_tail(X, sc, dslot, *X.seq, true);
 }
 
 // Ghost columns of the HALO_LNS group from the mailbox of the step the fused
@@ -1075,7 +1085,7 @@ template <bool RES, int TURB, bool STRIP = true>
 __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
-  const unsigned b = xcd_remap(blockIdx.x, gridDim.x);
+  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), a.part, T);
   const LnmLayout L(T.TI, T.TJ, a.nsp - 1);
   // phase trace: wavefront 0 (slots 0..8) and the last wavefront (9, 10) of the workgroup
   unsigned long long* tr = a.tr ? a.tr + (long)b * 12 : nullptr;
@@ -1095,6 +1105,9 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
     sc->time_part += dt_step;
     sc->dt_val[slot] = dt_step;
     sc->hot_cnt[slot_next] = 0;
+    // the interior tiles' list of a comm-overlap step (a later launch of this
+    // step) starts empty whatever ran before (split steps reset hot_cnt only)
+    sc->hot_cnt2[slot] = 0;
     scenario_next(P, sc, slot, slot_next);
   }
   int i, j, c, i0, j0;
@@ -1291,7 +1304,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
         const int lane = threadIdx.x & (WAVE - 1);
         const int leader = __ffsll((long long)ball) - 1;
         unsigned base = 0;
-        if (lane == leader) base = atomicAdd(&sc->hot_cnt[slot], (unsigned)__popcll(ball));
+        if (lane == leader) base = atomicAdd(a.hot_n, (unsigned)__popcll(ball));
         base = __shfl(base, leader, WAVE);
         if (hot) a.hot[base + __popcll(ball & ((1ull << lane) - 1ull))] = (int)idx;
       }
@@ -1346,7 +1359,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void
 __global__ __launch_bounds__(BLOCK) void hf2d_lnm_hot(StepParams P, LnmArrays a, DevScalars* sc, int slot,
                                                        int slot_next, int serial) {
   apply_dt(P, sc, slot);
-  const unsigned n = sc->hot_cnt[slot];
+  const unsigned n = *a.hot_n;
   const long N = a.N;
   double dtl = 1.0;
   int neg = 0, skip = 0;
@@ -3016,7 +3029,7 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     const FusedX X = fused_args();
     const unsigned nbp = (unsigned)std::max(1, (2 * cnt + BLOCK * 16 - 1) / (BLOCK * 16));
     hipLaunchKernelGGL(hf2d_p2p_push, dim3(nbp), dim3(BLOCK), 0, st, L, first, last, ny, cnt, X, m.sc,
-                       dt_slot >= 0 ? dt_slot : 0, dt_slot >= 0 ? 1 : 0);
+                       dt_slot >= 0 ? dt_slot : 0, dt_slot >= 0 ? 1 : 0, 1);
     HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
                        dim3(BLOCK), 0, st, L, l_off - 1, l_off + (gi1 - gi0), ny, cnt, X);
@@ -3537,7 +3550,104 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
     a.tr = m.lnm_trace;
   }
   if (lnm_ti < 1 || lnm_ti > BLOCK / LNM_TILE) lnm_ti = BLOCK / LNM_TILE;
-  const LeanTile T = lnm_tile(P.i1 - P.i0, P.ny, lnm_ti);
+  LeanTile T = lnm_tile(P.i1 - P.i0, P.ny, lnm_ti);
+  T.ne = (P.i1 - P.i0) % T.TI == 1 ? 2 : 1;   // (the halo's second column from the edge part)
+  // RCCL / in-process transports: the tiles of the strip's first and last
+  // tile columns first -- with their kinetics and state kernel, which change
+  // the reacting edge cells' halo values -- then their halo on the comm
+  // stream while the interior tiles and their kinetics run (a second list),
+  // then the dt MIN (as the lean N-S and inviscid tile kernels)
+  // (the decision must be the same on every rank -- the exchange sequence
+  // differs -- so a strip too narrow to split runs all its tiles at once)
+  static const bool split_env = !std::getenv("HF2D_LNM_SPLIT") || std::string(std::getenv("HF2D_LNM_SPLIT")) != "0";
+  lnm_split = split_env && comm_overlap && (m.p2p.on ? p2p_fuse : (m.comm || m.local)) && m.nranks > 1 &&
+              !want_res && cs.cfg.isAdiabaticWall;
+  const bool parts = T.nbi >= 2 + T.ne;
+  // (xGMI mailboxes: the edge halo is pushed before the interior tiles run,
+  // and published with the dt once they are done)
+  ColList Lc{};
+  if (lnm_split && m.p2p.on) {
+    sbuf = 1 - sbuf, pbuf = 1 - pbuf, cbuf = 1 - cbuf, dsbuf = 1 - dsbuf;
+    std::vector<real*> fl;
+    std::vector<unsigned char> fo;
+    halo_fields(CpuSolver::HALO_LNS, fl, fo, false);
+    sbuf = 1 - sbuf, pbuf = 1 - pbuf, cbuf = 1 - cbuf, dsbuf = 1 - dsbuf;
+    if (fl.size() > (size_t)MAX_HALO_FIELDS || (long)fl.size() * h.ny > m.halo_cap)
+      throw std::runtime_error("mechanism halo exceeds the mailbox capacity");
+    Lc.nf = (int)fl.size();
+    for (int k = 0; k < Lc.nf; k++) {
+      Lc.f[k] = fl[k];
+      Lc.o[k] = fo[k];
+    }
+  }
+  if (!lnm_split) {
+    a.hot = m.chem_list;
+    a.hot_n = &m.sc->hot_cnt[slot];
+    a.part = 0;
+    lnm_launch(P, a, T, want_res, slot, slot_next, serial, (unsigned)(T.nbi * T.nbj));
+  } else {
+    if (!m.comm_stream) {
+      HIP_CHECK(hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&m.ev_halo, hipEventDisableTiming));
+    }
+    // edge list first (at most its own cells), the interior list after it
+    const long edge_cells = (1L + T.ne) * T.TI * P.ny;
+    a.hot = m.chem_list;
+    a.hot_n = &m.sc->hot_cnt[slot];
+    a.part = parts ? 1 : 0;
+    lnm_launch(P, a, T, want_res, slot, slot_next, serial, (unsigned)(parts ? (1 + T.ne) * T.nbj : T.nbi * T.nbj));
+    const int cnt = Lc.nf * h.ny;
+    if (m.p2p.on) {
+      hipLaunchKernelGGL(hf2d_p2p_push, dim3((unsigned)std::max(1, (2 * cnt + BLOCK * 16 - 1) / (BLOCK * 16))),
+                         dim3(BLOCK), 0, st, Lc, l_off, l_off + (gi1 - gi0) - 1, h.ny, cnt, fused_args(), m.sc, slot_next,
+                         1, 0);
+      HIP_CHECK(hipGetLastError());
+    } else {
+      HIP_CHECK(hipEventRecord(m.ev_edge, st));
+    }
+    a.hot = m.chem_list + edge_cells;
+    a.hot_n = &m.sc->hot_cnt2[slot];
+    a.part = 2;
+    if (parts) lnm_launch(P, a, T, want_res, slot, slot_next, serial, (unsigned)((T.nbi - 1 - T.ne) * T.nbj));
+    if (m.p2p.on) {
+      hipLaunchKernelGGL(hf2d_p2p_finish, dim3(1), dim3(WAVE), 0, st, fused_args(), m.sc, slot_next);
+      HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
+                         dim3(BLOCK), 0, st, Lc, l_off - 1, l_off + (gi1 - gi0), h.ny, cnt, fused_args());
+      HIP_CHECK(hipGetLastError());
+      ghost_stale = true;
+      p2p_mwg_exchanges++;
+      overlap_steps++;
+    }
+  }
+  sbuf = 1 - sbuf;
+  pbuf = 1 - pbuf;
+  cbuf = 1 - cbuf;
+  dsbuf = 1 - dsbuf;
+  lnm_steps++;
+  if (lnm_split && !m.p2p.on) {   // the new state's halo (post-step buffers), overlapped with the interior
+    if (m.local) {   // in-process group: the host orders the streams (see the inviscid path)
+      HIP_CHECK(hipEventSynchronize(m.ev_edge));
+      exchange(CpuSolver::HALO_LNS, -1, (void*)m.comm_stream);
+      HIP_CHECK(hipStreamSynchronize(m.comm_stream));
+    } else {
+      HIP_CHECK(hipStreamWaitEvent(m.comm_stream, m.ev_edge, 0));
+      exchange(CpuSolver::HALO_LNS, -1, (void*)m.comm_stream);
+      HIP_CHECK(hipEventRecord(m.ev_halo, m.comm_stream));
+      HIP_CHECK(hipStreamWaitEvent(st, m.ev_halo, 0));
+    }
+    exchange_dt(slot_next);
+    overlap_steps++;
+  }
+}
+
+// Tile kernel (the tiles of a.part), kinetics of the cells it listed (a.hot /
+// a.hot_n) in place on the new species, their state kernel.
+void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const LeanTile& T, bool want_res, int slot,
+                              int slot_next, int serial, unsigned ntile) {
+  Impl& m = *impl;
+  hipStream_t st = m.stream;
   const LnmLayout L(T.TI, T.TJ, m.nsp - 1);
   const size_t shmem = (size_t)L.total() * sizeof(real);
   const int strip = P.i1 < P.nx ? 1 : 0;
@@ -3548,8 +3658,7 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
     (void)hipGetLastError();
     attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip] = true;
   }
-  hipLaunchKernelGGL(k, dim3(T.nbi * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
-                     m.partials);
+  hipLaunchKernelGGL(k, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial, m.partials);
   HIP_CHECK(hipGetLastError());
   // kinetics of the listed cells (T^m >= Tchem), in place on the new species
   const MechData& md = *cs.cfg.mech->data_ptr();
@@ -3563,26 +3672,20 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
   mid.mech = m.mech;
   mid.nsp = m.nsp;
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
-  unsigned* cnt = &m.sc->hot_cnt[slot];
   const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : 4);
   if (kind == 1) {
-    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st,
-                          m.chem_list, cnt, true))
+    if (!chem_fast_launch(cs.cfg.mech->name, P, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st, a.hot,
+                          a.hot_n, true))
       throw std::runtime_error("hf2d_chem_fast list launch failed");
     chem_kernel_used = "hf2d_chem_fast";
   } else {
-    if (!chem_rtc_launch(md, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st, m.chem_list, cnt, true))
+    if (!chem_rtc_launch(md, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st, a.hot, a.hot_n, true))
       throw std::runtime_error("hf2d_rtc_chem list launch failed");
     chem_kernel_used = "hf2d_rtc_chem";
   }
   const unsigned nb = (unsigned)std::min<long>((c1 - c0 + BLOCK - 1) / BLOCK, 1024);
   hipLaunchKernelGGL(hf2d_lnm_hot, dim3(nb), dim3(BLOCK), 0, st, P, a, m.sc, slot, slot_next, serial);
   HIP_CHECK(hipGetLastError());
-  sbuf = 1 - sbuf;
-  pbuf = 1 - pbuf;
-  cbuf = 1 - cbuf;
-  dsbuf = 1 - dsbuf;
-  lnm_steps++;
 }
 
 // The lean N-S kernel applies to this step (lean_ns.hpp; eligibility lns_ok)
@@ -3643,6 +3746,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     // point, dispatched in ~15 waves, ran 350 -> 550 us with it)
     P.stagger_wgs = cu_count > 0 ? cu_count : 256;
     P.stagger = ntile <= 4u * (unsigned)P.stagger_wgs && nt == BLOCK ? tile_stagger : 0;
+    // (64-thread tiles, the whole grid resident at once: a linear start ramp
+    // over the grid of 2 / 4 / 7 / 10 us measured 4.7 / 6.4 / 15 / 27 %
+    // slower than none, profiles/r04_start.md)
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
     const FusedX X = fx_step ? fused_args() : FusedX{};
@@ -3766,7 +3872,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       cbuf = 1;
     } else {
       const LnsArrays a = m.lns_arrays(h, sbuf, pbuf, cbuf, dsbuf, abuf);
-      const LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj > 0 ? lean_tj : lns_tile_height(P.ny, BLOCK), 1);
+      LeanTile T = lean_tile_geom(P.i1 - P.i0, P.ny, BLOCK, lean_tj > 0 ? lean_tj : lns_tile_height(P.ny, BLOCK), 1);
+      // (the halo's second column must come from the edge part)
+      T.ne = (P.i1 - P.i0) % T.TI == 1 ? 2 : 1;
       const int ntile = T.nbi * T.nbj;
       const bool t2 = sk_mode == SK_SGT;
       const size_t shmem = (size_t)(t2 ? Lns<SK_SGT>::PLANES : Lns<SK_SGL>::PLANES) * T.NC * sizeof(real);
@@ -3799,8 +3907,11 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
           Lc.o[k] = fo[k];
         }
       }
+      // (the decision must be the same on every rank -- the exchange sequence
+      // differs -- so a strip too narrow to split runs all its tiles at once)
       lns_split = !lns_fx && comm_overlap && !m.p2p.on && (m.comm || m.local) && m.nranks > 1 && !want_res &&
-                  T.nbi >= 3 && cs.cfg.isAdiabaticWall;
+                  cs.cfg.isAdiabaticWall;
+      const bool lparts = T.nbi >= 2 + T.ne;
       if (lns_fx) {
         hipLaunchKernelGGL(kLnsFx[tv][want_res ? 1 : 0], dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
                            slot_next, serial, m.partials, fused_args(), Lc);
@@ -3816,8 +3927,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
           HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
           HIP_CHECK(hipEventCreateWithFlags(&m.ev_halo, hipEventDisableTiming));
         }
-        hipLaunchKernelGGL(lk, dim3(2 * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
-                           m.partials, 1);
+        hipLaunchKernelGGL(lk, dim3(lparts ? (1 + T.ne) * T.nbj : ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
+                           slot_next, serial, m.partials, lparts ? 1 : 0);
       } else {
         hipLaunchKernelGGL(lk, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial,
                            m.partials, 0);
@@ -3833,8 +3944,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
         HIP_CHECK(hipEventRecord(m.ev_edge, st));
         // interior tiles in flight before the exchange is issued; they write
         // neither the edge columns nor the ghost columns
-        hipLaunchKernelGGL(lk, dim3((T.nbi - 2) * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next,
-                           serial, m.partials, 2);
+        if (lparts)
+          hipLaunchKernelGGL(lk, dim3((T.nbi - 1 - T.ne) * T.nbj), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
+                             slot_next, serial, m.partials, 2);
         HIP_CHECK(hipGetLastError());
         if (m.local) {   // in-process group: the host orders the streams (see the inviscid path)
           HIP_CHECK(hipEventSynchronize(m.ev_edge));
@@ -3860,6 +3972,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     fx_pending = true;   // exchanged inside the tile kernel
   } else if (lns_fx) {
     lns_fx = false;   // exchanged inside the lean N-S kernel + unpacked
+  } else if (lnm_split) {
+    lnm_split = false;   // exchanged above, overlapped with the interior tiles
   } else if (lns_split) {
     lns_split = false;   // exchanged above, overlapped with the interior tiles
   } else if ((m.comm || m.local || m.p2p.on) && m.nranks > 1) {

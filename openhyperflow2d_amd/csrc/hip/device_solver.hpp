@@ -12,6 +12,9 @@
 
 namespace hf2d {
 
+struct LnmArrays;
+struct LeanTile;
+
 bool gpu_available();
 
 // In-process stand-in for the RCCL communicator: N DeviceSolvers (one host
@@ -112,6 +115,7 @@ class DeviceSolver : public SolverBase {
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
   bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
+  bool lnm_split = false;   // this lean mechanism step ran edge-first with its halo overlapped
   bool lns_fx = false;      // this lean N-S step exchanged through the fused mailbox kernel
   long lns_fx_steps = 0;    // lean N-S steps with the fused xGMI mailbox exchange
   long p2p_mwg_exchanges = 0;   // mailbox exchanges through hf2d_p2p_push / hf2d_p2p_unpack
@@ -228,6 +232,8 @@ class DeviceSolver : public SolverBase {
   bool lns_entry(const StepParams& P0) const;
   bool lnm_step_ok(const StepParams& P) const;
   void lnm_step(const StepParams& P, bool want_res, int slot, int slot_next, int serial);
+  void lnm_launch(const StepParams& P, const LnmArrays& a, const LeanTile& T, bool want_res, int slot, int slot_next,
+                  int serial, unsigned ntile);
   // mechanism-mode kinetics of cells [k0, k1) (chem_fast / chem_mech / generic)
   void launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb, int slot);
 };

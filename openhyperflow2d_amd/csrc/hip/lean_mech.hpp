@@ -76,6 +76,8 @@ struct LnmArrays {
   const uint8_t* nb = nullptr;
   const uint8_t* gf = nullptr;
   int* hot = nullptr;   // reacting cells of the step (kinetics list)
+  unsigned* hot_n = nullptr;   // ... and their count (DevScalars::hot_cnt / hot_cnt2 of the slot)
+  int part = 0;   // tiles of this launch: 0 all, 1 the strip's edge tile columns, 2 the others (comm overlap)
   unsigned long long* tr = nullptr;   // phase trace (HF2D_LNM_TRACE): 12 clocks per workgroup
 };
 

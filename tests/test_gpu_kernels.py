@@ -141,7 +141,7 @@ def test_lean_bitwise_with_switches(gpu):
 
 
 def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, toggle=False, corrupt=False,
-                   stats=None, setup=None, chunk_hook=None, fields=FIELDS):
+                   stats=None, setup=None, chunk_hook=None, fields=FIELDS, parts=None):
     """Run the strip decomposition as `nranks` DeviceSolvers on ONE GPU, one
     host thread each, halos through the in-process LocalGroup transport (or,
     p2p=True, the device-side mailbox transport: one exchange kernel per step,
@@ -152,7 +152,7 @@ def _virtual_ranks(hf, text, nranks, schedule, lean=True, p2p=False, fuse=True, 
 
     nat = hf.native()
     cases = [nat.Case.from_deck(text, ".", False) for _ in range(nranks)]
-    parts = balanced_columns(np.asarray(cases[0].field("solid")), nranks)
+    parts = parts or balanced_columns(np.asarray(cases[0].field("solid")), nranks)
     group = nat.LocalGroup(nranks)
     solvers = []
     for r, (a, b) in enumerate(parts):
@@ -345,7 +345,7 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     assert min(lean_steps) > 0, stats
     if p2p == "fx":
         assert min(stats["p2p_mwg_exchanges" if deck == "scramjet" else "lns_fx_steps"]) > 0, stats
-    if not p2p and deck != "scramjet":   # in-process transport: edge tiles first, halo overlapped
+    if not p2p:   # in-process transport: edge tiles first, halo overlapped (mechanism: + their kinetics)
         assert min(stats["overlap_steps"]) > 0, stats
     ref = gpu.Simulation(text, "gpu")
     for n, res in schedule:
@@ -353,6 +353,32 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     assert (ref.solver.lnm_steps if deck == "scramjet" else ref.solver.lns_steps) > 0
     assert summ["dt"] == ref.summary()["dt"]
     assert summ["time"] == ref.summary()["time"]
+    for f in fields:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+@pytest.mark.parametrize("deck,p2p", [("resonator", False), ("scramjet", False), ("scramjet", "fx")])
+def test_overlap_with_a_one_column_last_tile(gpu, deck, p2p):
+    """Strips 97 columns wide: the edge-first launches' last tile column holds
+    a single column (97 = 6 x 16 + 1 = 8 x 12 + 1), so the edge part takes the
+    last two tile columns (the halo's second column, LeanTile::ne) -- and a
+    20-column strip, too narrow to split, runs all its tiles at once while its
+    neighbours split (the exchange sequence is the same on every rank)."""
+    fields = list(FIELDS) + ["k", "mu_t"]
+    if deck == "resonator":
+        text = decks.resonator(214, 40, nmax=10 ** 6, nout=10 ** 5)
+    else:
+        text = decks.scramjet(214, 48, nmax=10 ** 6, nout=10 ** 5)
+        fields += ["Y:H2", "Y:OH"]
+    schedule = [(4, True), (13, False), (3, True)]
+    stats = {}
+    got, summ = _virtual_ranks(gpu, text, 3, schedule, lean=True, p2p=bool(p2p), fuse=p2p == "fx", stats=stats,
+                               fields=fields, parts=[(0, 97), (97, 194), (194, 214)])
+    assert min(stats["overlap_steps"][:2]) > 0, stats
+    ref = gpu.Simulation(text, "gpu")
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
     for f in fields:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
