@@ -1020,6 +1020,21 @@ __global__ void hf2d_p2p_finish(FusedX X, DevScalars* sc, int dslot) {
   if (threadIdx.x == 0) fx_tail(X, sc, dslot, *X.seq, true);
 }
 
+// The scalars the host reads (the words before the dt shards, and the shards
+// of the dt slot it reads) into pinned host memory with plain vector stores,
+// queued behind the step's kernels: the host then waits for the stream only,
+// instead of for the stream and a device-to-host copy of the whole block behind
+// it (one copy-engine round trip per sync_scalars, i.e. per run_steps call).
+__global__ __launch_bounds__(WAVE) void hf2d_scalars_out(const DevScalars* sc, DevScalars* host, int slot) {
+  constexpr int NH = (int)(offsetof(DevScalars, dt_sh) / 8);
+  static_assert(offsetof(DevScalars, dt_sh) % 8 == 0 && NH <= WAVE, "DevScalars header is copied in 8-byte words");
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(sc);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(host);
+  const int t = threadIdx.x;
+  if (t < NH) dst[t] = src[t];
+  if (t < DT_SHARDS) host->dt_sh[slot][t][0] = sc->dt_sh[slot][t][0];
+}
+
 // Ghost columns of the HALO_LNS group from the mailbox of the step the fused
 // tail just completed (it waited for every peer's flag): entry f of side s
 // goes to ghost column ghostL - o[f] / ghostR + o[f] (grid-stride, one value
@@ -1806,6 +1821,7 @@ struct DeviceSolver::Impl {
   real* probe_out = nullptr;
   DevScalars* sc = nullptr;
   DevScalars* sc_host = nullptr;   // pinned
+  bool sc_kernel = true;           // sync_scalars: hf2d_scalars_out instead of a copy (HF2D_SC_KERNEL=0: copy)
   ResidualPack* partials = nullptr;
   ResidualPack* res_out = nullptr;
   ResidualPack* res_host = nullptr;   // pinned
@@ -2069,6 +2085,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
   if (const char* e = std::getenv("HF2D_STAGGER")) tile_stagger = std::atoi(e);
+  if (const char* e = std::getenv("HF2D_SC_KERNEL")) impl->sc_kernel = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
@@ -2617,7 +2634,12 @@ void DeviceSolver::sync_scalars() {
   flush_pending();
   p2p_complete();
   Impl& m = *impl;
-  HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
+  if (m.sc_kernel) {
+    hipLaunchKernelGGL(hf2d_scalars_out, dim3(1), dim3(WAVE), 0, m.stream, m.sc, m.sc_host, (int)(nstep % 3));
+    HIP_CHECK(hipGetLastError());
+  } else {
+    HIP_CHECK(hipMemcpyAsync(m.sc_host, m.sc, sizeof(DevScalars), hipMemcpyDeviceToHost, m.stream));
+  }
   HIP_CHECK(hipStreamSynchronize(m.stream));
   const int slot = nstep % 3;
   const unsigned long long db = dt_get_host(*m.sc_host, slot);
@@ -3852,7 +3874,17 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   } else if (lnm_step_ok(P)) {
     if (lean_state) lean_materialize();
     if (lns_state == 0) {
-      // first lean mechanism step: the split step, then T^{n+1} as the stored state
+      // first lean mechanism step: the split step, then T^{n+1} as the stored state.
+      // Its fill F_{n+1} overwrites the level-n state (Cp, k, p) in place; a
+      // materialise right after this step (a download after a one-step call)
+      // re-runs F_{n+1}, which reads the lagged state from the [cbuf] buffers
+      // as after a lean step: keep level n there (without it the re-fill read
+      // stale buffers: with a download after every step the scramjet's dt
+      // left the CPU stepper's at step 4, tools/download_effect.py)
+      const size_t SB = (size_t)h.N * sizeof(real);
+      HIP_CHECK(hipMemcpyAsync(m.CP2, m.CP, SB, hipMemcpyDeviceToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(m.kk2, m.kk, SB, hipMemcpyDeviceToDevice, st));
+      HIP_CHECK(hipMemcpyAsync(m.p2, m.p, SB, hipMemcpyDeviceToDevice, st));
       step_split(P, want_res, slot, slot_next, serial, nblk, true);
       HIP_CHECK(hipMemcpyAsync(m.Tst[0], m.Tg[pbuf], h.N * sizeof(real), hipMemcpyDeviceToDevice, st));
       lns_state = 1;

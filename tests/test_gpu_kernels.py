@@ -310,6 +310,32 @@ def test_compact_state_halo_matches_single_gpu(gpu, deck, p2p):
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
 
+@pytest.mark.parametrize("deck", ["scramjet", "resonator", "step"])
+def test_download_after_every_step_leaves_the_trajectory_unchanged(gpu, deck):
+    """One-step calls with a download (materialise of the lean N-S /
+    mechanism representation) after each: every step is then a re-entry
+    split step followed by a materialise, which must give the same trajectory
+    as the lean steps of the same calls without downloads (bitwise) and the
+    CPU stepper's dt."""
+    gen = {"scramjet": lambda: decks.scramjet(214, 48, nmax=10 ** 6, nout=10 ** 5),
+           "resonator": lambda: decks.resonator(214, 40, nmax=10 ** 6, nout=10 ** 5),
+           "step": lambda: decks.step(214, 80, nmax=10 ** 6, nout=10 ** 5)}[deck]
+    cont = gpu.Simulation(gen(), "gpu")
+    down = gpu.Simulation(gen(), "gpu")
+    cpu = gpu.Simulation(gen(), "cpu")
+    for s in range(8):
+        cont.step(1)
+        down.step(1)
+        cpu.step(1)
+        down.field("rho")
+        assert cont.summary()["dt"] == down.summary()["dt"], s
+        assert abs(down.summary()["dt"] / cpu.summary()["dt"] - 1) < 1e-12, s
+    lean = (lambda sv: sv.lnm_steps) if deck == "scramjet" else (lambda sv: sv.lns_steps)
+    assert lean(cont.solver) > 0 and lean(down.solver) == 0
+    for f in FIELDS:
+        np.testing.assert_array_equal(cont.field(f), down.field(f), err_msg=f)
+
+
 @pytest.mark.parametrize("deck,nranks,p2p", [("step", 3, False), ("resonator", 4, False), ("sst_plate", 3, False),
                                             ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True),
                                             ("resonator", 3, "fx"), ("step", 2, "fx"), ("sst_plate", 3, "fx"),
@@ -490,6 +516,69 @@ def test_p2p_two_processes_ipc(gpu, tmp_path):
         ref.step(n, residual=res)
     assert float(got["dt"]) == ref.summary()["dt"]
     for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def _rccl_proc_worker(rank, world, port, text, schedule, fields, out):
+    import os
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from openhyperflow2d_amd.parallel.dist import DistributedSimulation
+
+    sim = DistributedSimulation(text, "gpu", rank=rank, world=world, device=rank, transport="rccl")
+    assert sim.transport == "rccl", sim.transport
+    for n, res in schedule:
+        sim.step(n, residual=res)
+    got = {f: sim.gather_field(f) for f in fields}
+    ov = [None] * world
+    dist.all_gather_object(ov, int(sim.solver.overlap_steps))
+    if rank == 0:
+        np.savez(out, dt=sim.summary()["dt"], overlap=np.array(ov), **got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("deck", ["resonator", "scramjet"])
+def test_rccl_two_processes_overlap_match_single_gpu(gpu, deck, tmp_path):
+    """Two OS processes on two GPUs over RCCL (the truly asynchronous comm
+    stream: the edge tiles' halo goes out with ncclSend/ncclRecv on the comm
+    stream, ordered after the edge tiles by an event, while the interior tiles
+    run; the dt MIN waits for it) == one GPU bitwise, and the split ran on
+    both ranks.  RCCL refuses two ranks on one device, so this needs >= 2 GPUs
+    (skipped on a one-GPU box; the in-process group covers the same launch
+    order with host-ordered copies in test_lean_ns_strips_match_single_gpu)."""
+    import socket
+
+    import torch
+    import torch.multiprocessing as mp
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs one device per rank")
+    fields = list(FIELDS) + ["k", "mu_t"]
+    if deck == "resonator":
+        text = decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5)
+    else:
+        text = decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5)
+        fields += ["Y:H2", "Y:OH"]
+    schedule = [(4, True), (17, False), (5, True)]
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    out = str(tmp_path / "rccl.npz")
+    mp.start_processes(_rccl_proc_worker, args=(2, port, text, schedule, fields, out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    assert got["overlap"].min() > 0, got["overlap"]
+    ref = gpu.Simulation(text, "gpu")
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert float(got["dt"]) == ref.summary()["dt"]
+    for f in fields:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
 
