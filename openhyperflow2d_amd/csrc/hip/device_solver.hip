@@ -4222,6 +4222,34 @@ std::string DeviceSolver::autotune(int steps) {
   lean_tj = win.tj;
   lean_nt = win.nt;
   lean_wgcu = win.wgcu;
+  // step graphs on or off for the winning geometry: replaying the 6-step
+  // graph costs ~1 us per step more than eager launches on the 2000 x 200
+  // headline grid (28.5 vs 27.5 us/step over 20-step calls, 1x MI355X,
+  // tools/launch_overhead.py) but saves host launch time on small grids
+  if (use_graph) {
+    double g_us[2] = {1e30, 1e30};
+    for (int g : {1, 0}) {
+      use_graph = g == 1;
+      graph.reset();
+      try {
+        run_steps(12);
+        synchronize();
+        for (int rep = 0; rep < 2; rep++) {
+          const auto t0 = std::chrono::steady_clock::now();
+          run_steps(steps);
+          synchronize();
+          g_us[g] = std::min(g_us[g],
+                             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / steps * 1e6);
+        }
+      } catch (const std::exception& e) {
+        log += std::string("stopped: ") + e.what() + "; ";
+        break;
+      }
+    }
+    use_graph = g_us[1] <= g_us[0];
+    std::snprintf(b, sizeof b, "graphs on %.2f us, off %.2f us; ", g_us[1], g_us[0]);
+    log += b;
+  }
   graph.reset();
   dt = s_dt;
   dt_running = s_dtr;
@@ -4237,8 +4265,8 @@ std::string DeviceSolver::autotune(int steps) {
   upload();   // device scalars from the restored host state
   graph_launches = 0;
   lns_steps = lnm_steps = 0;   // (the tuning steps do not count as the run's)
-  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d wgcu=%d (%.2f us/step)", win.nt, win.cpt, win.tj, win.wgcu,
-                best);
+  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d wgcu=%d graphs=%d (%.2f us/step)", win.nt, win.cpt, win.tj,
+                win.wgcu, (int)use_graph, best);
   return log + b;
 }
 

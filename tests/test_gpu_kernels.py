@@ -484,6 +484,7 @@ def _p2p_proc_worker(rank, world, port, text, schedule, out):
     sim = DistributedSimulation(text, "gpu", rank=rank, world=world, device=0, transport="p2p")
     assert sim.transport == "p2p", sim.transport
     sim.solver.p2p_fuse = True   # fused exchange across processes (IPC-mapped mailboxes)
+    sim.solver.use_graph = True  # (the autotune may have turned step graphs off for this grid)
     for n, res in schedule:
         sim.step(n, residual=res)
     fields = {f: sim.gather_field(f) for f in FIELDS}
@@ -607,6 +608,7 @@ def test_step_graphs_bitwise(gpu, physics):
     text = decks.wedge15(300, 60, navier_stokes=ns, turbulence=4 if ns else 0, nmax=10 ** 6, nout=10 ** 5)
     a = gpu.Simulation(text, "gpu")
     b = gpu.Simulation(text, "gpu")
+    a.solver.use_graph = True   # (the autotune picks graphs on / off by speed)
     b.solver.use_graph = False
     for n, res in [(40, False), (13, True), (61, False)]:
         a.step(n, residual=res)
