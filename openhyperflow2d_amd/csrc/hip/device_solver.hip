@@ -3358,9 +3358,14 @@ void DeviceSolver::flush_pending() {
 }
 
 uint64_t DeviceSolver::mode_signature() const {
+  // (the ping-pong parities too: a captured window bakes in the buffer
+  // pointers of its first step, and a materialise + re-entry (split) step
+  // flips only some of them, so a window cached before a download must not
+  // replay after it -- it did, and the lean mechanism run then stepped on
+  // the previous level's buffers from the first replayed window on)
   const int fields[] = {lean_state, (int)lean, (int)fused, (int)lean_tile, (int)(lean_sg && lean_sg_ok), lean_cpt,
                         lean_tj, lean_nt, lean_wgcu, (int)(p2p_fuse && impl->p2p.on), (int)(sgl && sgl_ok), lns_state,
-                        (int)lean_ns, (int)lean_mech};
+                        (int)lean_ns, (int)lean_mech, sbuf, abuf, dsbuf, pbuf, cbuf};
   uint64_t h = 0;
   for (int f : fields) h = h * 1000003ull + (uint64_t)(f + 1);
   return h;

@@ -336,6 +336,34 @@ def test_download_after_every_step_leaves_the_trajectory_unchanged(gpu, deck):
         np.testing.assert_array_equal(cont.field(f), down.field(f), err_msg=f)
 
 
+@pytest.mark.parametrize("deck", ["scramjet", "resonator", "wedge"])
+def test_graph_windows_after_a_download_replay_the_right_buffers(gpu, deck):
+    """Step graphs on, a download between calls: the materialise + re-entry
+    step shifts the ping-pong parities, so a 6-step window captured before
+    the download must not replay after it with the old buffer pointers (it
+    did: the lean mechanism run then read the previous level's buffers).
+    Equal bitwise to the same calls without downloads and to eager launches."""
+    gen = {"scramjet": lambda: decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5),
+           "resonator": lambda: decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5),
+           "wedge": lambda: decks.wedge15(300, 60, nmax=10 ** 6, nout=10 ** 5)}[deck]
+    runs = [gpu.Simulation(gen(), "gpu") for _ in range(3)]
+    for r in runs:
+        r.solver.use_graph = True
+    runs[2].solver.use_graph = False
+    for n in (24, 11, 24, 13, 24):
+        for k, r in enumerate(runs):
+            r.step(n)
+            if k == 0:
+                r.solver.download()   # materialise; the next call re-enters
+    assert runs[0].solver.graph_launches > 0 and runs[1].solver.graph_launches > 0
+    dt = [r.summary()["dt"] for r in runs]
+    assert dt[0] == dt[1] == dt[2], dt
+    fields = FIELDS + (["Y:H2", "Y:OH", "mu_t"] if deck == "scramjet" else ["mu_t"] if deck == "resonator" else [])
+    for f in fields:
+        np.testing.assert_array_equal(runs[0].field(f), runs[1].field(f), err_msg=f)
+        np.testing.assert_array_equal(runs[0].field(f), runs[2].field(f), err_msg=f)
+
+
 @pytest.mark.parametrize("deck,nranks,p2p", [("step", 3, False), ("resonator", 4, False), ("sst_plate", 3, False),
                                             ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True),
                                             ("resonator", 3, "fx"), ("step", 2, "fx"), ("sst_plate", 3, "fx"),
