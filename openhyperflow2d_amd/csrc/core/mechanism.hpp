@@ -36,7 +36,15 @@ constexpr int MECH_NT = 97;       // transport table: 200 K .. 5000 K, 50 K step
 constexpr real MECH_TT0 = 200.0, MECH_TDT = 50.0;
 constexpr real MECH_RU = 8.314462618;
 constexpr real MECH_PATM = 101325.0;
-constexpr real MECH_TMIN = 100.0, MECH_TMAX = 6000.0;   // Newton clamp
+// Newton clamp.  Below MECH_TLO (the lower limit of the NASA-7 fits, 200 K
+// for the GRI / Li et al. data) every species is extrapolated at constant cp
+// -- cp(T) = cp(TLO), h(T) = h(TLO) + cp(TLO) (T - TLO), s(T) = s(TLO) +
+// cp(TLO) ln(T / TLO) -- instead of running the polynomial outside its fit;
+// the recovery then holds down to MECH_TMIN (reaching it flags the state as
+// unphysical).  The under-expanded fuel jet of the scramjet deck cools to
+// ~105 K in its barrel (profiles/scramjet_long_r05.md), so the former 100 K
+// floor stopped that run after 12-14k steps.
+constexpr real MECH_TMIN = 20.0, MECH_TMAX = 6000.0, MECH_TLO = 200.0;
 
 struct MechReaction {
   int nrs = 0, nps = 0;            // distinct reactant / product species (<= 3 each)
@@ -110,20 +118,25 @@ HF_HD inline real nasa_s(const real* a, real T, real lnT) {
   return a[0] * lnT + T * (a[1] + T * (a[2] * 0.5 + T * (a[3] * (1.0 / 3.0) + T * a[4] * 0.25))) + a[6];
 }
 
-// e (J/kg, formation included), cv, R_mix, cp of mass fractions Y at T.
+// e (J/kg, formation included), cv, R_mix, cp of mass fractions Y at T
+// (below MECH_TLO: evaluated at TLO, e extended linearly with the mixture cv
+// -- the constant-cp extrapolation of every species; bitwise the polynomial
+// for T >= TLO).
 template <int NSB>
 HF_HD inline void mech_mix_thermo(const MechData& m, const real* Y, real T, real* e, real* cv, real* Rm, real* cp) {
   real se = 0, scv = 0, sR = 0;
+  const real Te = T < MECH_TLO ? MECH_TLO : T;
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
     if (s >= m.ns) break;
-    const Nasa7 c = mech_coef_v(m, s, T);
+    const Nasa7 c = mech_coef_v(m, s, Te);
     const real* a = c.a;
     const real R = m.Rs[s];
-    se += Y[s] * R * (nasa_hT(a, T) - T);
-    scv += Y[s] * R * (nasa_cp(a, T) - 1.0);
+    se += Y[s] * R * (nasa_hT(a, Te) - Te);
+    scv += Y[s] * R * (nasa_cp(a, Te) - 1.0);
     sR += Y[s] * R;
   }
+  if (T < MECH_TLO) se += scv * (T - MECH_TLO);
   *e = se;
   *cv = scv;
   *Rm = sR;
@@ -185,8 +198,11 @@ HF_HD inline void mech_transport(const MechData& m, const real* Y, real T, real*
 
 // Species absolute enthalpy h_s(T) (J/kg) for the enthalpy-diffusion heat flux.
 HF_HD inline real mech_h_species(const MechData& m, int s, real T) {
-  const Nasa7 c = mech_coef_v(m, s, T);
-  return m.Rs[s] * nasa_hT(c.a, T);
+  const real Te = T < MECH_TLO ? MECH_TLO : T;
+  const Nasa7 c = mech_coef_v(m, s, Te);
+  real hT = nasa_hT(c.a, Te);
+  if (T < MECH_TLO) hT += nasa_cp(c.a, MECH_TLO) * (T - MECH_TLO);   // constant cp below TLO
+  return m.Rs[s] * hT;
 }
 
 // ---------------------------------------------------------------------------
@@ -200,13 +216,23 @@ struct MechRate {
 };
 
 // g[s] = h_s/(R T) - s_s/R of every species at T (for equilibrium constants)
+// (below MECH_TLO with the constant-cp extrapolation: h/RT = (h(TLO)/R +
+// cp/R (T - TLO)) / T, s/R = s(TLO)/R + cp/R ln(T / TLO))
 template <int NSB>
 HF_HD inline void mech_gibbs(const MechData& m, real T, real lnT, real* g) {
+  const bool lo = T < MECH_TLO;
+  const real Te = lo ? MECH_TLO : T;
+  const real lnTe = lo ? std::log(MECH_TLO) : lnT;
 #pragma unroll
   for (int s = 0; s < NSB; s++) {
     if (s >= m.ns) break;
-    const Nasa7 c = mech_coef_v(m, s, T);
-    g[s] = nasa_h(c.a, T) - nasa_s(c.a, T, lnT);
+    const Nasa7 c = mech_coef_v(m, s, Te);
+    if (lo) {
+      const real cpR = nasa_cp(c.a, Te);
+      g[s] = (nasa_hT(c.a, Te) + cpR * (T - Te)) / T - (nasa_s(c.a, Te, lnTe) + cpR * (lnT - lnTe));
+    } else {
+      g[s] = nasa_h(c.a, T) - nasa_s(c.a, T, lnT);
+    }
   }
 }
 

@@ -24,7 +24,7 @@
 namespace hf2d {
 namespace chemk {
 
-constexpr double RU = 8.314462618, PATM = 101325.0, TMIN = 100.0, TMAX = 6000.0;   // mechanism.hpp MECH_*
+constexpr double RU = 8.314462618, PATM = 101325.0, TMIN = 20.0, TMAX = 6000.0, TLO = 200.0;   // mechanism.hpp MECH_*
 
 template <int... Is>
 struct IntSeq {};
@@ -73,9 +73,11 @@ __device__ __forceinline__ const double* coef(int s, double T) {
 }
 
 // e, cv of the concentrations c at T (per unit mass: divided by rho)
+// (below TLO: constant-cp extrapolation, as mech_mix_thermo)
 template <class M>
-__device__ __forceinline__ void mix_e_cv(const double* c, double rho, double T, double* e, double* cv) {
+__device__ __forceinline__ void mix_e_cv(const double* c, double rho, double Tin, double* e, double* cv) {
   double se = 0.0, scv = 0.0;
+  const double T = Tin < TLO ? TLO : Tin;
 #pragma unroll
   for (int s = 0; s < M::NS; s++) {
     const double* a = coef<M>(s, T);
@@ -86,6 +88,7 @@ __device__ __forceinline__ void mix_e_cv(const double* c, double rho, double T, 
     se += c[s] * (T * (hRT - 1.0));
     scv += c[s] * (cpR - 1.0);
   }
+  if (Tin < TLO) se += scv * (Tin - TLO);
   *e = se * RU / rho;
   *cv = scv * RU / rho;
 }
@@ -263,6 +266,15 @@ __device__ void chem_cell(double rho, double e, double* y, double* Tio, double d
     double g[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++) {
+      if (T < TLO) {   // constant-cp extrapolation (mechanism.hpp mech_gibbs)
+        const double Te = TLO, lnTe = log(TLO);
+        const double* a = coef<M>(s, Te);
+        const double cpR = a[0] + Te * (a[1] + Te * (a[2] + Te * (a[3] + Te * a[4])));
+        const double hT = Te * (a[0] + Te * (a[1] * 0.5 + Te * (a[2] * (1.0 / 3.0) + Te * (a[3] * 0.25 + Te * a[4] * 0.2)))) + a[5];
+        const double sR = a[0] * lnTe + Te * (a[1] + Te * (a[2] * 0.5 + Te * (a[3] * (1.0 / 3.0) + Te * a[4] * 0.25))) + a[6];
+        g[s] = (hT + cpR * (T - Te)) / T - (sR + cpR * (lnT - lnTe));
+        continue;
+      }
       const double* a = coef<M>(s, T);
       const double hRT = a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) +
                          a[5] / T;

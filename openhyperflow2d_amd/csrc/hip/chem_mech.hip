@@ -48,8 +48,10 @@ __device__ __forceinline__ const double* nasa(const ChemMechDev& m, int s, doubl
 }
 
 // specific internal energy and cv of the concentrations of one cell at T
-__device__ void cell_e_cv(const ChemMechDev& m, const double* c, double rho, double T, double* e, double* cv) {
+// (below MECH_TLO: constant-cp extrapolation, as mech_mix_thermo)
+__device__ void cell_e_cv(const ChemMechDev& m, const double* c, double rho, double Tin, double* e, double* cv) {
   double se = 0.0, scv = 0.0;
+  const double T = Tin < MECH_TLO ? MECH_TLO : Tin;
   for (int s = 0; s < m.ns; s++) {
     const double* a = nasa(m, s, T);
     const double cpR = a[0] + T * (a[1] + T * (a[2] + T * (a[3] + T * a[4])));
@@ -57,6 +59,7 @@ __device__ void cell_e_cv(const ChemMechDev& m, const double* c, double rho, dou
     se += c[s] * (T * (hRT - 1.0));
     scv += c[s] * (cpR - 1.0);
   }
+  if (Tin < MECH_TLO) se += scv * (Tin - MECH_TLO);
   *e = se * MECH_RU / rho;
   *cv = scv * MECH_RU / rho;
 }
@@ -143,7 +146,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void hf
       for (int i = 0; i < 4; i++) {
         const int s = quad + 4 * i;
         double gv = 0.0;
-        if (s < m.ns) {
+        if (s < m.ns && T < MECH_TLO) {   // constant-cp extrapolation (mechanism.hpp mech_gibbs)
+          const double Te = MECH_TLO, lnTe = log(MECH_TLO);
+          const double* a = nasa(m, s, Te);
+          const double cpR = a[0] + Te * (a[1] + Te * (a[2] + Te * (a[3] + Te * a[4])));
+          const double hT =
+              Te * (a[0] + Te * (a[1] * 0.5 + Te * (a[2] * (1.0 / 3.0) + Te * (a[3] * 0.25 + Te * a[4] * 0.2)))) + a[5];
+          const double sR =
+              a[0] * lnTe + Te * (a[1] + Te * (a[2] * 0.5 + Te * (a[3] * (1.0 / 3.0) + Te * a[4] * 0.25))) + a[6];
+          gv = (hT + cpR * (T - Te)) / T - (sR + cpR * (lnT - lnTe));
+        } else if (s < m.ns) {
           const double* a = nasa(m, s, T);
           const double hRT =
               a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) + a[5] / T;

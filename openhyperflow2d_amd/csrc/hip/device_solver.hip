@@ -3618,8 +3618,11 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
       HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&m.ev_halo, hipEventDisableTiming));
     }
-    // edge list first (at most its own cells), the interior list after it
-    const long edge_cells = (1L + T.ne) * T.TI * P.ny;
+    // edge list first (at most its own cells), the interior list after it:
+    // tile column 0 (TI columns), ne - 1 full columns and the last, partial
+    // one of w - (nbi - 1) TI columns -- the list holds exactly N entries
+    const long wl = (long)(P.i1 - P.i0) - (long)(T.nbi - 1) * T.TI;
+    const long edge_cells = ((long)T.ne * T.TI + wl) * P.ny;
     a.hot = m.chem_list;
     a.hot_n = &m.sc->hot_cnt[slot];
     a.part = parts ? 1 : 0;

@@ -445,23 +445,45 @@ def nasa_coeffs(mech: Mechanism, T: np.ndarray) -> np.ndarray:
     return np.where(sel, lo, hi)
 
 
-def cp_R(mech, T):
+# Below T_LO (the lower limit of the NASA-7 fits) every species is
+# extrapolated at constant cp (the solver's MECH_TLO rule, core/mechanism.hpp).
+T_LO = 200.0
+
+
+def _cp_R_poly(mech, T):
     a = nasa_coeffs(mech, T)
     T = np.asarray(T, dtype=np.float64)[..., None]
     return a[..., 0] + T * (a[..., 1] + T * (a[..., 2] + T * (a[..., 3] + T * a[..., 4])))
 
 
-def h_RT(mech, T):
+def _h_RT_poly(mech, T):
     a = nasa_coeffs(mech, T)
     T = np.asarray(T, dtype=np.float64)[..., None]
     return a[..., 0] + T * (a[..., 1] / 2 + T * (a[..., 2] / 3 + T * (a[..., 3] / 4 + T * a[..., 4] / 5))) + a[..., 5] / T
 
 
-def s_R(mech, T):
+def _s_R_poly(mech, T):
     a = nasa_coeffs(mech, T)
     T = np.asarray(T, dtype=np.float64)[..., None]
     return (a[..., 0] * np.log(T) + T * (a[..., 1] + T * (a[..., 2] / 2 + T * (a[..., 3] / 3 + T * a[..., 4] / 4)))
             + a[..., 6])
+
+
+def cp_R(mech, T):
+    return _cp_R_poly(mech, np.maximum(np.asarray(T, dtype=np.float64), T_LO))
+
+
+def h_RT(mech, T):
+    T = np.asarray(T, dtype=np.float64)
+    Te = np.maximum(T, T_LO)
+    h = _h_RT_poly(mech, Te) * Te[..., None] + _cp_R_poly(mech, Te) * (T - Te)[..., None]
+    return h / T[..., None]
+
+
+def s_R(mech, T):
+    T = np.asarray(T, dtype=np.float64)
+    Te = np.maximum(T, T_LO)
+    return _s_R_poly(mech, Te) + _cp_R_poly(mech, Te) * np.log(T / Te)[..., None]
 
 
 def mixture_e(mech, Y, T):

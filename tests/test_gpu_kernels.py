@@ -411,23 +411,33 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
 
-@pytest.mark.parametrize("deck,p2p", [("resonator", False), ("scramjet", False), ("scramjet", "fx")])
+@pytest.mark.parametrize("deck,p2p", [("resonator", False), ("scramjet", False), ("scramjet", "fx"),
+                                      ("scramjet_hot", False), ("scramjet_hot", "fx")])
 def test_overlap_with_a_one_column_last_tile(gpu, deck, p2p):
     """Strips 97 columns wide: the edge-first launches' last tile column holds
     a single column (97 = 6 x 16 + 1 = 8 x 12 + 1), so the edge part takes the
     last two tile columns (the halo's second column, LeanTile::ne) -- and a
     20-column strip, too narrow to split, runs all its tiles at once while its
-    neighbours split (the exchange sequence is the same on every rank)."""
+    neighbours split (the exchange sequence is the same on every rank).
+    'scramjet_hot': ChemTmin 200 K (every active cell on the kinetics lists)
+    with 90-column strips, whose last tile column holds 10 columns: the
+    interior list starts after the edge part's real cell count, not after
+    (1 + ne) full tile columns (which overran the list by 6 columns)."""
     fields = list(FIELDS) + ["k", "mu_t"]
+    parts = [(0, 97), (97, 194), (194, 214)]
     if deck == "resonator":
         text = decks.resonator(214, 40, nmax=10 ** 6, nout=10 ** 5)
+    elif deck == "scramjet_hot":
+        text = decks.with_mechanism(decks.scramjet(214, 48, nmax=10 ** 6, nout=10 ** 5), tmin=200.0)
+        fields += ["Y:H2", "Y:OH"]
+        parts = [(0, 90), (90, 180), (180, 214)]
     else:
         text = decks.scramjet(214, 48, nmax=10 ** 6, nout=10 ** 5)
         fields += ["Y:H2", "Y:OH"]
     schedule = [(4, True), (13, False), (3, True)]
     stats = {}
     got, summ = _virtual_ranks(gpu, text, 3, schedule, lean=True, p2p=bool(p2p), fuse=p2p == "fx", stats=stats,
-                               fields=fields, parts=[(0, 97), (97, 194), (194, 214)])
+                               fields=fields, parts=parts)
     assert min(stats["overlap_steps"][:2]) > 0, stats
     ref = gpu.Simulation(text, "gpu")
     for n, res in schedule:

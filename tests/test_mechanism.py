@@ -69,6 +69,28 @@ def test_native_thermo_matches_numpy(native):
         assert d["mu"] == pytest.approx(mu, rel=2e-3)   # 50 K uniform table vs exact
 
 
+def test_thermo_below_the_fit_range_extrapolates_at_constant_cp(native):
+    """Below T_LO = 200 K (the NASA-7 fits' lower limit) every species runs at
+    constant cp: e is linear in T with the cv of 200 K, continuous at 200 K,
+    the Newton recovers T down to the 20 K floor (the under-expanded fuel jet
+    of the scramjet deck cools to ~105 K), and the NumPy oracle agrees."""
+    m = M.h2_air_li2004()
+    Y = np.array([0.5, 0.1, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0])
+    Y[-1] = 1 - Y.sum()
+    ref = native.mech_thermo_host("h2_air_li2004", list(Y), 200.0)
+    for T in (199.999, 150.0, 105.0, 60.0, 25.0):
+        d = native.mech_thermo_host("h2_air_li2004", list(Y), T)
+        assert d["cv"] == ref["cv"]
+        assert d["e"] == pytest.approx(ref["e"] + ref["cv"] * (T - 200.0), rel=1e-13)
+        assert d["e"] == pytest.approx(M.mixture_e(m, Y, T), rel=1e-12)
+        assert d["cv"] == pytest.approx(M.mixture_cv(m, Y, T), rel=1e-13)
+        assert d["T_from_e"] == pytest.approx(T, rel=1e-10)
+    # continuity of the oracle's h and s at T_LO (the Gibbs energies of the kinetics)
+    for f in (M.h_RT, M.s_R, M.cp_R):
+        a, b = f(m, np.array(200.0)), f(m, np.array(200.0 - 1e-7))
+        np.testing.assert_allclose(a, b, rtol=1e-8)
+
+
 def _states(m, n, seed=1):
     rng = np.random.default_rng(seed)
     Y = rng.random((m.ns, n)) * np.array([0.03, 0.2, 0.1, 1e-3, 1e-3, 3e-3, 1e-4, 1e-5, 0.0])[:, None]
