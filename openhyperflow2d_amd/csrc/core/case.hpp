@@ -56,6 +56,12 @@ struct Config {
   // new key: k-omega SST wall omega = 60 nu / (beta1 d1^2) with d1 = SSTWallDistance *
   // min(dx, dy): 1.0 (default) is Menter's distance of the first cell off the wall node
   real SSTWallDistance = 1.0;
+  // new key: lagged time step.  0 (default, the reference):
+  // step n+1 uses dt = MIN over every rank's cells of the local dt of step n.
+  // 1: step n+1 uses the MIN of step n-1, so a strip only waits for its two
+  // neighbours' halos before its next step and the all-rank MIN has a whole
+  // step to arrive (the first two steps use the initial dt).
+  int LaggedDt = 0;
   // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
   // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
   int ThreadBlockSize = 0;

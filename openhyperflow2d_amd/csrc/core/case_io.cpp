@@ -119,6 +119,7 @@ void config_io(IO& io, C& c) {
   io.pod(c.CFL);
   io.pod(c.ViscousCFL);
   io.pod(c.SSTWallDistance);
+  io.pod(c.LaggedDt);
   io.pod(c.ThreadBlockSize);
   io.table(c.CFL_Scenario);
   io.table(c.beta_Scenario);

@@ -311,6 +311,7 @@ StepParams SolverBase::make_params(long it) const {
   P.bff = C.bff;
   P.alternate_rms = C.isAlternateRMS;
   P.sm = C.ProblemType;
+  P.lag_dt = (C.LaggedDt && C.semantics == Semantics::MPI) ? 1 : 0;
   P.chem_model = C.chem_model;
   P.species = &C.species;
   FillParams f = C.fill_params();
@@ -358,6 +359,10 @@ StepResult SolverBase::advance(bool want_res) {
   if (cs.cfg.semantics == Semantics::SERIAL) {
     dt_running = std::min(dt_running, dtm);
     dt = dt_running;
+  } else if (P.lag_dt) {   // step n + 1 takes the MIN of step n - 1; this one's waits a step
+    if (!(dt_lag > 0)) dt_lag = P.dt;
+    dt = dt_lag;
+    dt_lag = dtm;
   } else {
     dt = dtm;
   }

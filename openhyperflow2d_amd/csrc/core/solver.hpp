@@ -114,6 +114,9 @@ class SolverBase {
   Comm local_comm;
   real dt = 0;               // dt used by the next step
   real dt_running = 1.0;     // serial semantics: never reset
+  // Config::LaggedDt: the MIN of the last step's local dts, used by the step
+  // after next (<= 0: not yet set -- the next step's dt)
+  real dt_lag = -1.0;
   long iter = 0;             // iteration inside the current cycle
   long last_iter = 0;        // completed iterations of previous cycles
   bool ckpt_written = false; // a cycle-end checkpoint of this run exists

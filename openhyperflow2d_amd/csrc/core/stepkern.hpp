@@ -128,6 +128,9 @@ struct StepParams {
   // of the 100 MHz clock before staging, so the dispatch rounds of a
   // co-resident grid load their tiles one after another (speed only)
   int stagger = 0, stagger_wgs = 256;
+  // Config::LaggedDt: the step's dt is the all-rank MIN of two steps back
+  // (device: DevScalars::dt_lag; host: SolverBase::dt_lag)
+  int lag_dt = 0;
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

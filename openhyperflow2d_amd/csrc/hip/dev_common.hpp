@@ -19,6 +19,11 @@ struct DevScalars {
                                    // mechanism step's fill belongs to the previous one)
   unsigned hot_cnt[3];             // lean mechanism step: reacting cells listed by the step using the slot
   unsigned hot_cnt2[3];            // ... by its interior tiles (comm-overlap steps: a second list)
+  // Lagged dt (StepParams::lag_dt): dt_lag[slot] is the dt of the step that
+  // reads the slot -- the all-rank MIN of two steps back.  The first kernel
+  // of step n (lag_head) moves MIN(slot n) -- the previous step's MIN, folded
+  // over the ranks -- to dt_lag[slot of n + 1] before it overwrites the word.
+  unsigned long long dt_lag[3];
   // Sharded dt MIN: every workgroup of a step used to atomicMin into ONE word,
   // and device-scope atomics to one address serialise at the memory side
   // (~10 ns each: the 800 workgroups of a small-strip step queued ~7 us
@@ -77,8 +82,22 @@ __host__ inline void dt_set_host(DevScalars& s, int slot, unsigned long long b) 
   for (int k = 0; k < DT_SHARDS; k++) s.dt_sh[slot][k][0] = b;
 }
 
+// dt of the step reading the slot
+__device__ inline double dt_cur(const StepParams& P, const DevScalars* sc, int slot) {
+  return P.lag_dt ? bits_to_d(sc->dt_lag[slot]) : dt_get(sc, slot);
+}
+// first kernel of a lagged step, one thread, before the slot's word is
+// overwritten with this step's dt: the previous step's MIN goes to the next
+// step's lag word (fold: the MIN over the other ranks, if it is still pending)
+__device__ inline void lag_head(const StepParams& P, DevScalars* sc, int slot, int slot_next, double fold = 1.0) {
+  if (P.lag_dt) {
+    const double m = dt_get(sc, slot);
+    sc->dt_lag[slot_next] = d_to_bits(fold < m ? fold : m);
+  }
+}
+
 __device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
-  const double dt = dt_get(sc, slot);
+  const double dt = dt_cur(P, sc, slot);
   P.dt = dt;
   P.dtdx = dt / P.dx;
   P.dtdy = dt / P.dy;

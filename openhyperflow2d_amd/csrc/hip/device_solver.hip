@@ -122,6 +122,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_predict(StepParams P, SoA in, SoA 
     // step's fill is min-reducing, which other blocks may already be
     // writing) and accumulate physical time.
     dt_reset(sc, slot_reset(slot));
+    lag_head(P, sc, slot, slot_next);
     sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     sc->dt_val[slot] = P.dt;
@@ -235,6 +236,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_fused_euler(StepParams P, SoA in, 
   const long g = (long)blockIdx.x * BLOCK + threadIdx.x;
   if (g == 0) {
     dt_reset(sc, slot_reset(slot));
+    lag_head(P, sc, slot, slot_next);
     sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
@@ -280,6 +282,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_euler(StepParams P, LeanSoA L
   const long g = (long)b * BLOCK + threadIdx.x;
   if (g == 0) {
     dt_reset(sc, slot_reset(slot));
+    lag_head(P, sc, slot, slot_next);
     sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
@@ -378,6 +381,10 @@ struct FusedX {
   unsigned* done;            // workgroups finished in this step: per dt shard, then the shards (FX_DONE_STRIDE apart)
   long cap;
   int rank, nranks, sides, on;
+  // lagged dt: the tail waits for the two neighbours' flags only and leaves
+  // the dt MIN to the next step's first workgroup (lean_tile_body) or to
+  // hf2d_p2p_complete
+  int defer;
 };
 
 __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, DevScalars* sc) {
@@ -436,6 +443,7 @@ __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slo
   bool ok = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
   for (int q = 0; q < X.nranks && ok; q++) {
     if (q == X.rank) continue;
+    if (X.defer && q != X.rank - 1 && q != X.rank + 1) continue;   // (halo senders only)
     long spins = 0;
     while (__hip_atomic_load(&X.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sn) {
       __builtin_amdgcn_s_sleep(1);
@@ -451,7 +459,8 @@ __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slo
     if (ok) (void)p2p_acquire(&X.my_flags[q]);
     if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
   }
-  if (fold) __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (fold && !X.defer)
+    __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   *X.seq = sn;
 }
 
@@ -515,6 +524,16 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     dt_reset(sc, slot_reset(slot));
+    // lagged dt with the fold deferred (X.defer): the previous step's tail
+    // waited for the two neighbours only; the other ranks' dt of that step
+    // is folded here, one step later, by this one thread
+    double fold = 1.0;
+    if (FX && X.defer && P.lag_dt && seq_prev > 0 && p2p_wait_all(X, seq_prev, sc)) {
+      const int pp = (int)(seq_prev & 1);
+      for (int q = 0; q < X.nranks; q++)
+        if (q != X.rank) fold = fmin(fold, p2p_load(X.my_dtr + pp * X.nranks + q));
+    }
+    lag_head(P, sc, slot, slot_next, fold);
     sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     scenario_next(P, sc, slot, slot_next);
@@ -764,6 +783,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     dt_reset(sc, slot_reset(slot));
+    lag_head(P, sc, slot, slot_next);
     sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
     sc->time_part += P.dt;
     sc->dt_val[slot] = P.dt;
@@ -1113,9 +1133,10 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   apply_dt(P, sc, slot);
   const real dt_now = P.dt;
   P.dt = sc->dt_val[slot_reset(slot)];
-  const real dt_step = dt_get(sc, slot);
+  const real dt_step = dt_cur(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     dt_reset(sc, slot_reset(slot));
+    lag_head(P, sc, slot, slot_next);
     sc->dt_bits[slot] = d_to_bits(dt_step);   // folded (the kinetics read the word)
     sc->time_part += dt_step;
     sc->dt_val[slot] = dt_step;
@@ -2408,6 +2429,15 @@ void DeviceSolver::upload() {
   dt_set_host(s0, 0, b0);
   dt_set_host(s0, 1, b1);
   dt_set_host(s0, 2, b1);
+  if (make_params(last_iter + iter).lag_dt) {
+    // lagged dt: the first step runs with dt; slot 0's MIN stands for the
+    // previous step's (the host's dt_lag, or dt before any step)
+    s0.dt_lag[0] = b0;
+    const double dl = dt_lag > 0 ? dt_lag : dt;
+    unsigned long long bl;
+    std::memcpy(&bl, &dl, 8);
+    dt_set_host(s0, 0, bl);
+  }
   s0.time_part = 0.0;
   s0.iter[0] = s0.iter[1] = s0.iter[2] = (double)(last_iter + iter);
   {
@@ -2643,7 +2673,12 @@ void DeviceSolver::sync_scalars() {
   HIP_CHECK(hipStreamSynchronize(m.stream));
   const int slot = nstep % 3;
   const unsigned long long db = dt_get_host(*m.sc_host, slot);
-  std::memcpy(&dt, &db, 8);
+  if (make_params(last_iter + iter).lag_dt) {   // next step's dt, and the MIN it hands on
+    std::memcpy(&dt, &m.sc_host->dt_lag[slot], 8);
+    std::memcpy(&dt_lag, &db, 8);
+  } else {
+    std::memcpy(&dt, &db, 8);
+  }
   cur_time_part = m.sc_host->time_part - time_offset;
   last_dev_time = m.sc_host->time_part;
   const int err = comm->allreduce_max_int(m.sc_host->neg_T);
@@ -3781,7 +3816,11 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     // slower than none, profiles/r04_start.md)
     // multi-GPU: exchange fused into the tile kernel (no separate exchange launch)
     fx_step = m.p2p.on && p2p_fuse && !lean_has_cauchy_x;
-    const FusedX X = fx_step ? fused_args() : FusedX{};
+    FusedX X = fx_step ? fused_args() : FusedX{};
+    // lagged dt: the fused tail waits for the two neighbours only; the dt
+    // MIN follows in the next fused step's first workgroup or in
+    // hf2d_p2p_complete before any other consumer (fx_pending)
+    X.defer = fx_step && P.lag_dt ? 1 : 0;
     // RCCL / in-process transports: edge tiles first, their halo on the comm
     // stream while the interior tiles compute, then the dt MIN
     // (the decision must be the same on every rank -- the exchange sequence

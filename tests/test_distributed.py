@@ -55,6 +55,10 @@ CASES = {
     # mechanism mode (species block + operator-split kinetics + SST)
     "scramjet_mech": (lambda: decks.with_mechanism(decks.scramjet(120, 40, nmax=10 ** 6, nout=10 ** 5), substeps=2,
                                                    tmin=250.0), 4),
+    # lagged dt (LaggedDt = 1): step n + 1 runs with the all-rank MIN of step n - 1
+    "wedge15_euler_lag": (lambda: decks.set_key(decks.wedge15(90, 30, nmax=10 ** 6, nout=10 ** 5), "LaggedDt", 1), 5),
+    "wedge15_ns_keps_lag": (lambda: decks.set_key(decks.wedge15(90, 30, navier_stokes=True, turbulence=4,
+                                                                nmax=10 ** 6, nout=10 ** 5), "LaggedDt", 1), 4),
 }
 
 
@@ -81,10 +85,10 @@ def test_two_strips_match_single_rank(hf, case, lean, tmp_path):
 
 
 @pytest.mark.parametrize("world", [4, 8])
-@pytest.mark.parametrize("case", ["wedge15_euler", "wedge15_ns_keps", "scramjet_mech"])
+@pytest.mark.parametrize("case", ["wedge15_euler", "wedge15_ns_keps", "scramjet_mech", "wedge15_euler_lag"])
 def test_many_strips_match_single_rank(hf, case, world, tmp_path):
     """4 and 8 gloo ranks (strips of 11..30 columns): bit-identical to one rank."""
-    _strips_vs_single(hf, case, case == "wedge15_euler", tmp_path, world)
+    _strips_vs_single(hf, case, case.startswith("wedge15_euler"), tmp_path, world)
 
 
 def _run_worker(rank, world, port, text, outdir, lean=False):
@@ -199,3 +203,24 @@ def test_fault_on_one_rank_stops_every_rank(hf, tmp_path):
     import json
 
     assert json.loads((tmp_path / "Wedge15_90x30.hf2d.meta").read_text())["iteration"] == 20
+
+
+def test_lagged_dt_takes_the_min_of_two_steps_back(hf):
+    """LaggedDt = 1: the first two steps run with the initial dt, step n + 1
+    with the MIN of step n - 1 (here: the standard run's dt after its first
+    step, whose state both runs share), and the trajectories then differ."""
+    text = decks.wedge15(60, 20, nmax=10 ** 6, nout=10 ** 5)
+    std = hf.Simulation(text, "cpu")
+    lag = hf.Simulation(decks.set_key(text, "LaggedDt", 1), "cpu")
+    d0 = std.summary()["dt"]
+    assert lag.summary()["dt"] == d0
+    std.step(1)
+    lag.step(1)
+    f0 = std.summary()["dt"]
+    assert f0 != d0
+    assert lag.summary()["dt"] == d0
+    np.testing.assert_array_equal(lag.field("rho"), std.field("rho"))
+    std.step(1)
+    lag.step(1)
+    assert lag.summary()["dt"] == f0
+    assert not np.array_equal(lag.field("rho"), std.field("rho"))

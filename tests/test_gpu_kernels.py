@@ -847,3 +847,58 @@ def test_tile_stagger_is_timing_only(gpu, monkeypatch, stagger):
     assert s.summary()["dt"] == ref.summary()["dt"]
     for f in FIELDS:
         np.testing.assert_array_equal(s.field(f), ref.field(f), err_msg=f)
+
+
+def _lagged(text):
+    return decks.set_key(text, "LaggedDt", 1)
+
+
+@pytest.mark.parametrize("deck", ["wedge", "resonator", "scramjet_transport"])
+def test_lagged_dt_gpu_equals_cpu(gpu, deck):
+    """LaggedDt = 1 (step n + 1 runs with the MIN of step n - 1): the device
+    slots (DevScalars::dt_lag, lag_head in every step's first kernel) give the
+    CPU stepper's dt sequence and fields bit for bit, across residual steps,
+    downloads and graph windows -- lean tile, lean N-S and lean mechanism
+    kernels (kinetics off: ChemTmin above every temperature)."""
+    if deck == "wedge":
+        text = decks.wedge15(200, 40, nmax=10 ** 6, nout=10 ** 5)
+    elif deck == "resonator":
+        text = decks.resonator(214, 40, nmax=10 ** 6, nout=10 ** 5)
+    else:
+        text = decks.with_mechanism(decks.scramjet(150, 48, nmax=10 ** 6, nout=10 ** 5), tmin=1e9)
+    text = _lagged(text)
+    g = gpu.Simulation(text, "gpu")
+    c = gpu.Simulation(text, "cpu")
+    for n, res in [(1, False), (1, True), (9, False), (4, True), (20, False)]:
+        g.step(n, residual=res)
+        c.step(n, residual=res)
+        assert g.summary()["dt"] == c.summary()["dt"], n
+    assert g.summary()["time"] == c.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(g.field(f), c.field(f), err_msg=f)
+    std = gpu.Simulation(decks.set_key(text, "LaggedDt", 0), "gpu")
+    std.step(35)
+    assert std.summary()["dt"] != g.summary()["dt"]
+
+
+@pytest.mark.parametrize("deck,nranks,p2p", [("wedge", 4, "fx"), ("wedge", 3, False), ("resonator", 3, "fx")])
+def test_lagged_dt_strips_match_single_gpu(gpu, deck, nranks, p2p):
+    """Lagged dt on strips: with the fused mailbox exchange the tail of a
+    step waits for its two neighbours only and the next step's first
+    workgroup folds the other ranks' dt (hf2d_p2p_complete before any other
+    consumer); N strips == one GPU bit for bit."""
+    if deck == "wedge":
+        text = _lagged(decks.wedge15(300, 60, nmax=10 ** 6, nout=10 ** 5))
+    else:
+        text = _lagged(decks.resonator(300, 40, nmax=10 ** 6, nout=10 ** 5))
+    schedule = [(4, True), (17, False), (5, True), (14, False)]
+    stats = {}
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=bool(p2p), fuse=p2p == "fx",
+                               stats=stats)
+    ref = gpu.Simulation(text, "gpu")
+    for n, res in schedule:
+        ref.step(n, residual=res)
+    assert summ["dt"] == ref.summary()["dt"]
+    assert summ["time"] == ref.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
