@@ -710,6 +710,7 @@ PYBIND11_MODULE(_hf2d, m) {
            py::arg("gi1") = -1, py::keep_alive<1, 2>())
       .def_static("nccl_unique_id", []() { return py::bytes(DeviceSolver::nccl_unique_id()); })
       .def("init_comm", [](DeviceSolver& s, py::bytes uid, int r, int n) { s.init_comm(std::string(uid), r, n); })
+      .def("p2p_loopback", &DeviceSolver::p2p_loopback, py::arg("rank"), py::arg("nranks"))
       .def("p2p_export", [](DeviceSolver& s, int r, int n) { return py::bytes(s.p2p_export(r, n)); },
            py::arg("rank"), py::arg("nranks"))
       .def("p2p_import",

@@ -230,6 +230,7 @@ class Case {
                                                          bool use_checkpoint, int nparts);
   FactsPart facts_part() const;
   void merge_facts(const std::vector<FactsPart>& parts);
+  CaseFacts fold_facts(const std::vector<FactsPart>& parts) const;   // (merge_facts without storing)
 
   // Individual pre-processing steps (public for tests).
   void fill_node(CellRecord& n, int is_mu_t, int is_init) const;
@@ -255,7 +256,14 @@ class Case {
   // record (i, j) as the geometry steps left it: resident, or read from the
   // preloaded checkpoint (windowed restart), or nullptr
   const CellRecord* far_record(int i, int j);
-  std::vector<std::pair<long, CellRecord>> far_cache;
+  struct FarRec {
+    long key;
+    CellRecord r;
+    bool reset;   // scan_area's turbulence reset applied
+  };
+  std::vector<FarRec> far_cache;
+  bool far_turb_reset = false;   // scan_area reset the turbulence state: far records get it too
+  void turb_reset_record(CellRecord& n, u64 tt) const;
   void load_and_preprocess(InputDeck& deck, const std::string& workdir, bool use_checkpoint, bool flags_only = false);
   void preprocess(InputDeck& d, const std::string& workdir, bool use_checkpoint);
 };

@@ -67,7 +67,9 @@ FactsPart Case::facts_part() const {
   return f;
 }
 
-void Case::merge_facts(const std::vector<FactsPart>& parts) {
+void Case::merge_facts(const std::vector<FactsPart>& parts) { facts = fold_facts(parts); }
+
+CaseFacts Case::fold_facts(const std::vector<FactsPart>& parts) const {
   CaseFacts f;
   const Config& C = cfg;
   f.single_gas = true;
@@ -116,7 +118,7 @@ void Case::merge_facts(const std::vector<FactsPart>& parts) {
     }
   }
   f.valid = true;
-  facts = f;
+  return f;
 }
 
 std::string FactsPart::pack() const {
@@ -156,11 +158,8 @@ static const CaseFacts& whole_facts(const Case& cs, CaseFacts& tmp) {
     if (!cs.facts.valid) throw std::runtime_error("eligibility of a strip Case without the merged whole-field facts");
     return cs.facts;
   }
-  Case& m = const_cast<Case&>(cs);
-  const CaseFacts keep = m.facts;
-  m.merge_facts({cs.facts_part()});
-  tmp = m.facts;
-  m.facts = keep;
+  // (folded into a local: the Case is not touched, so threads may share it)
+  tmp = cs.fold_facts({cs.facts_part()});
   return tmp;
 }
 

@@ -479,16 +479,27 @@ void Case::fill_node(CellRecord& n, int is_mu_t, int is_init) const {
   hf2d::fill_node(n, P);
 }
 
+// (a record of another strip's column, read from the checkpoint: it gets
+// every per-record change the whole-field pre-processing made to it by the
+// time of the call -- scan_area's turbulence reset)
 const CellRecord* Case::far_record(int i, int j) {
   if (J.resident(i)) return &J.at(i, j);
   if (!preloaded) return nullptr;
   const long key = (long)i * J.ny + j;
-  for (auto& e : far_cache)
-    if (e.first == key) return &e.second;
-  CellRecord r;
-  if (!read_hf2d_record(swap_path, J.nx, J.ny, i, j, r)) throw std::runtime_error("cannot read record of " + swap_path);
-  far_cache.push_back({key, r});
-  return &far_cache.back().second;
+  FarRec* e = nullptr;
+  for (auto& f : far_cache)
+    if (f.key == key) e = &f;
+  if (!e) {
+    CellRecord r;
+    if (!read_hf2d_record(swap_path, J.nx, J.ny, i, j, r)) throw std::runtime_error("cannot read record of " + swap_path);
+    far_cache.push_back({key, r, false});
+    e = &far_cache.back();
+  }
+  if (far_turb_reset && !e->reset) {
+    turb_reset_record(e->r, J.tt(i, j));
+    e->reset = true;
+  }
+  return &e->r;
 }
 
 Case Case::from_deck_window(InputDeck deck, const std::string& workdir, bool use_checkpoint, int a, int b,
@@ -499,7 +510,7 @@ Case Case::from_deck_window(InputDeck deck, const std::string& workdir, bool use
   cs.log = log;
   cs.load_and_preprocess(deck, workdir, use_checkpoint);
   cs.J.drop_flags();
-  std::vector<std::pair<long, CellRecord>>().swap(cs.far_cache);
+  std::vector<FarRec>().swap(cs.far_cache);
   cs.win_a = cs.win_b = -1;
   return cs;
 }
@@ -1334,6 +1345,15 @@ int Case::set_non_reflected_bc() {
   return nr;
 }
 
+// scan_area's turbulence reset of one record (tt: its new TurbType word)
+void Case::turb_reset_record(CellRecord& n, u64 tt) const {
+  n.TurbType = tt;
+  n.dkdx = n.dkdy = n.depsdx = n.depsdy = 0.0;
+  n.S[I_K] = n.S[I_EPS] = n.Src[I_K] = n.Src[I_EPS] = 0.0;
+  n.mu_t = n.lam_t = 0.0;
+  fill_node(n, 0, 1);
+}
+
 // ScanArea: mark active cells, optional turbulence-model reset and the
 // active-cell-balanced column partition.
 void Case::scan_area(int num_parts) {
@@ -1351,13 +1371,10 @@ void Case::scan_area(int num_parts) {
           if ((tt & m) == m) tt = (tt ^ m) & tt;
         tt |= TM;
         if (!J.resident(i)) continue;
-        CellRecord& n = J.at(i, j);
-        n.dkdx = n.dkdy = n.depsdx = n.depsdy = 0.0;
-        n.S[I_K] = n.S[I_EPS] = n.Src[I_K] = n.Src[I_EPS] = 0.0;
-        n.mu_t = n.lam_t = 0.0;
-        fill_node(n, 0, 1);
+        turb_reset_record(J.at(i, j), tt);
       }
     cfg.isTurbulenceReset = 0;
+    far_turb_reset = true;
   }
   subdomains = partition_columns(num_parts);
 }

@@ -1865,6 +1865,14 @@ struct DeviceSolver::Impl {
     std::vector<void*> opened;            // IPC mappings to close
     unsigned long long** d_flags = nullptr;
     double** d_dtr = nullptr;
+    bool loop = false;                    // p2p_loopback: the neighbours' mailboxes are this rank's own
+    // mailbox the edge pushes of `side` land in (0: the left neighbour's,
+    // whose right side this rank is); loopback: this rank's own mailbox of
+    // that side, so the ghost columns take the strip's own edge values
+    real* push_base(int side, int rank, long cap) const {
+      if (loop) return (real*)(base + off_recv) + (side == 0 ? -cap : cap);
+      return (real*)(peer_base[side == 0 ? rank - 1 : rank + 1] + off_recv);
+    }
   } p2p;
 
   LeanSoA lean_view(const HostArrays& h, int sb, int ab, int db, int pb, bool fromg) const {
@@ -2876,6 +2884,37 @@ std::string DeviceSolver::p2p_export(int rank, int nranks) {
   return std::string((const char*)&d, sizeof d);
 }
 
+// One-GPU stand-in for the multi-GPU mailbox exchange (timing only,
+// tools/exchange_loopback.py): this strip plays rank `rank` of `nranks`,
+// every peer has already published its step (flags at the maximum, dt 1.0),
+// and the neighbours' mailboxes are this rank's own (Impl::P2P::push_base:
+// the left edge push lands in the left-ghost mailbox, zero-gradient ghosts).
+// A step then does every store, publication, poll and ghost staging of a
+// real exchange, without a second strip on the GPU and without waiting --
+// what remains is the exchange's own cost on this device (the xGMI link
+// latency is not in it).
+void DeviceSolver::p2p_loopback(int rank, int nranks) {
+  if (nranks < 2 || rank < 0 || rank >= nranks) throw std::runtime_error("p2p_loopback: bad rank/nranks");
+  (void)p2p_export(rank, nranks);
+  HIP_CHECK(hipSetDevice(dev));
+  Impl& m = *impl;
+  Impl::P2P& p = m.p2p;
+  p.peer_base.assign(nranks, p.base);
+  std::vector<unsigned long long> flags(nranks, ~0ull);
+  flags[rank] = 0;
+  std::vector<double> dtr(2 * (size_t)nranks, 1.0);
+  HIP_CHECK(hipMemcpy(p.base, flags.data(), nranks * sizeof(unsigned long long), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(p.base + p.off_dtr, dtr.data(), dtr.size() * sizeof(double), hipMemcpyHostToDevice));
+  std::vector<unsigned long long*> fl(nranks, (unsigned long long*)p.base);
+  std::vector<double*> dr(nranks, (double*)(p.base + p.off_dtr));
+  p.d_flags = m.mem.alloc<unsigned long long*>(nranks);
+  p.d_dtr = m.mem.alloc<double*>(nranks);
+  HIP_CHECK(hipMemcpy(p.d_flags, fl.data(), nranks * sizeof(void*), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(p.d_dtr, dr.data(), nranks * sizeof(void*), hipMemcpyHostToDevice));
+  p.loop = true;
+  p.on = true;
+}
+
 void DeviceSolver::p2p_import(const std::vector<std::string>& descs) {
   HIP_CHECK(hipSetDevice(dev));
   Impl& m = *impl;
@@ -3107,8 +3146,8 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     a.cnt = cnt;
     a.sides = sides;
     a.cap = m.halo_cap;
-    a.peer_recv_l = has_left ? (real*)(p.peer_base[m.rank - 1] + p.off_recv) : nullptr;
-    a.peer_recv_r = has_right ? (real*)(p.peer_base[m.rank + 1] + p.off_recv) : nullptr;
+    a.peer_recv_l = has_left ? p.push_base(0, m.rank, m.halo_cap) : nullptr;
+    a.peer_recv_r = has_right ? p.push_base(1, m.rank, m.halo_cap) : nullptr;
     a.my_recv = (real*)(p.base + p.off_recv);
     a.peer_flags = p.d_flags;
     a.peer_dtr = p.d_dtr;
@@ -3314,8 +3353,8 @@ FusedX DeviceSolver::fused_args() const {
   const Impl::P2P& p = m.p2p;
   const bool has_left = gi0 > 0, has_right = gi1 < cs.J.nx;
   FusedX X{};
-  X.peer_recv_l = has_left ? (real*)(p.peer_base[m.rank - 1] + p.off_recv) : nullptr;
-  X.peer_recv_r = has_right ? (real*)(p.peer_base[m.rank + 1] + p.off_recv) : nullptr;
+  X.peer_recv_l = has_left ? p.push_base(0, m.rank, m.halo_cap) : nullptr;
+  X.peer_recv_r = has_right ? p.push_base(1, m.rank, m.halo_cap) : nullptr;
   X.my_recv = (const real*)(p.base + p.off_recv);
   X.peer_flags = p.d_flags;
   X.peer_dtr = p.d_dtr;

@@ -95,6 +95,9 @@ class DeviceSolver : public SolverBase {
   // the per-step halo + dt exchange is one device kernel (no RCCL, no host).
   std::string p2p_export(int rank, int nranks);
   void p2p_import(const std::vector<std::string>& descs);
+  // timing stand-in: rank `rank` of `nranks` with every peer ready and the
+  // neighbours' mailboxes looped back into this rank's own (device_solver.hip)
+  void p2p_loopback(int rank, int nranks);
   bool p2p_active() const;
   bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
   bool fx_step = false, fx_pending = false;

@@ -87,11 +87,13 @@ def test_merged_facts_name_the_first_failing_cell(hf, tmp_path):
         _check_windows(nat, text, str(tmp_path), 5)
 
 
-@pytest.mark.parametrize("mech", [False, True])
-def test_windowed_restart_reads_the_rank_slab(hf, mech, tmp_path):
+@pytest.mark.parametrize("mech,reset", [(False, False), (True, False), (False, True)])
+def test_windowed_restart_reads_the_rank_slab(hf, mech, reset, tmp_path):
     """A restart of a strip rank reads its own slab of the .hf2d (and of the
     species sidecar), plus the flag words of the other columns: the records
-    equal the whole-field restart's columns."""
+    equal the whole-field restart's columns.  reset: the restart runs with
+    isTurbulenceReset = 1, so the wall records another strip owns (read for
+    y+) must get scan_area's turbulence reset too."""
     if mech:
         text = decks.scramjet(96, 32, nmax=6, nout=3)
     else:
@@ -99,5 +101,7 @@ def test_windowed_restart_reads_the_rank_slab(hf, mech, tmp_path):
     sim = hf.Simulation(text, "cpu", workdir=str(tmp_path))
     sim.run(max_cycles=1, outdir=str(tmp_path), verbose=False)
     assert any(p.suffix == ".hf2d" for p in tmp_path.iterdir())
+    if reset:
+        text = decks.set_key(decks.set_key(text, "isTurbulenceReset", 1), "TurbulenceModel", 6)
     full, strips = _check_windows(hf.native(), text, str(tmp_path), 3, use_checkpoint=True)
     assert full.field("rho").any() and all(c.global_time == full.global_time for c in strips)
