@@ -62,6 +62,13 @@ struct Config {
   // neighbours' halos before its next step and the all-rank MIN has a whole
   // step to arrive (the first two steps use the initial dt).
   int LaggedDt = 0;
+  // new key: near-wall blend (0 = off, the reference).  N > 0: in the first N
+  // cells off a no-slip wall the DEEPS blend of the TANGENTIAL momentum leaves
+  // out the wall-normal neighbours (the blend's (1 - beta) dyy/2 dy^2/dt
+  // diffusion across the viscous sublayer carries part of the wall stress
+  // otherwise; profiles/flat_plate_validation.md).  The streamwise blend,
+  // and every other equation's, are unchanged.
+  int WallBlendCells = 0;
   // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
   // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
   int ThreadBlockSize = 0;
@@ -179,6 +186,9 @@ class Case {
   Field J;
   std::vector<GasFlow> flows, flows2d;
   std::vector<std::pair<int, int>> wall_nodes;     // (i, j)
+  // per wall node: directions into the flow (WD_* bits: the neighbour there
+  // is gas, the opposite one solid or outside the grid); WallBlendCells
+  std::vector<uint8_t> wall_dirs;
   std::vector<std::pair<int, int>> subdomains;     // ScanArea [start, end) pairs
   real dt0 = 1.0;
   real global_time = 0.0;

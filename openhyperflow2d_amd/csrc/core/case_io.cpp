@@ -120,6 +120,7 @@ void config_io(IO& io, C& c) {
   io.pod(c.ViscousCFL);
   io.pod(c.SSTWallDistance);
   io.pod(c.LaggedDt);
+  io.pod(c.WallBlendCells);
   io.pod(c.ThreadBlockSize);
   io.table(c.CFL_Scenario);
   io.table(c.beta_Scenario);
@@ -207,6 +208,7 @@ std::string Case::pack_strip_header(int a, int b) const {
   w.vec(flows);
   w.vec(flows2d);
   w.vec(pairs_flat(wall_nodes));
+  w.vec(wall_dirs);
   w.vec(pairs_flat(subdomains));
   w.pod(dt0);
   w.pod(global_time);
@@ -294,6 +296,7 @@ Case Case::unpack_strip_header(const char* data, size_t size, std::ostream* log,
   std::vector<int> flat;
   r.vec(flat);
   cs.wall_nodes = pairs_of(flat);
+  r.vec(cs.wall_dirs);
   r.vec(flat);
   cs.subdomains = pairs_of(flat);
   r.pod(cs.dt0);

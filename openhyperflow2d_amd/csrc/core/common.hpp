@@ -96,6 +96,8 @@ enum : u64 {
   NT_FC_TIME_DEPEND = NT_FC | CT_TIME_DEPEND,
   NT_FARFIELD = NT_FC | CT_NONREFLECTED,
 };
+// wall node directions into the flow (Case::wall_dirs, Config::WallBlendCells)
+enum : uint8_t { WD_XP = 1, WD_XM = 2, WD_YP = 4, WD_YM = 8 };
 
 // Turbulence condition bits (TurbType word).
 enum : u64 {

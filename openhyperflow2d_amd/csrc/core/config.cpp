@@ -27,6 +27,7 @@ void Config::load_globals(InputDeck& d) {
   ViscousCFL = d.get_float_or("ViscousCFL", 0.0);
   SSTWallDistance = d.get_float_or("SSTWallDistance", 1.0);
   LaggedDt = d.get_int_or("LaggedDt", 0) ? 1 : 0;
+  WallBlendCells = std::max(0, d.get_int_or("WallBlendCells", 0));
   ThreadBlockSize = d.get_int_or("ThreadBlockSize", 0);
   NSaveStep = d.get_int("NSaveStep");
   Nmax = d.get_int("Nmax");

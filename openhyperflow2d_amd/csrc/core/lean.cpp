@@ -248,7 +248,7 @@ std::vector<uint8_t> lean_flags(const HostArrays& h, int sm) {
 
 namespace hf2d {
 
-void compute_generic_flags(const Case& cs, HostArrays& h) {
+void compute_generic_flags(const Case& cs, HostArrays& h, int gx0) {
   const long N = h.N;
   const std::vector<uint8_t> lb = lean_flags(h, cs.cfg.ProblemType);
   // (mechanism mode: the kinetics are operator-split, no species Src)
@@ -269,6 +269,27 @@ void compute_generic_flags(const Case& cs, HostArrays& h) {
     const bool wall_gas = !has_all(CT, CT_SOLID) && (has_all(CT, CT_WALL_NO_SLIP) || has_all(CT, CT_WALL_LAW));
     if (wall_gas || nonzero(h.SrcAdd, idx, 0, NEQ)) g |= GF_SRCADD;
     h.gf[idx] = g;
+  }
+  // WallBlendCells: the first N cells off every no-slip wall node along its
+  // directions into the flow (the global wall list: decomposition independent)
+  const int nwb = cs.cfg.WallBlendCells;
+  if (nwb > 0 && cs.cfg.ProblemType == SM_NS && cs.wall_dirs.size() == cs.wall_nodes.size()) {
+    static const int di[4] = {1, -1, 0, 0}, dj[4] = {0, 0, 1, -1};
+    static const uint8_t bit[4] = {WD_XP, WD_XM, WD_YP, WD_YM};
+    for (size_t w = 0; w < cs.wall_nodes.size(); w++) {
+      for (int d = 0; d < 4; d++) {
+        if (!(cs.wall_dirs[w] & bit[d])) continue;
+        for (int n = 1; n <= nwb; n++) {
+          const int gi = cs.wall_nodes[w].first + n * di[d], j = cs.wall_nodes[w].second + n * dj[d];
+          const int li = gi - gx0;
+          if (j < 0 || j >= h.ny || gi < 0 || gi >= cs.J.nx) break;
+          if (li < 0 || li >= h.nx) continue;   // (another strip's column)
+          const long idx = (long)li * h.ny + j;
+          if (has_all(h.CT[idx], CT_SOLID)) break;
+          h.gf[idx] |= d < 2 ? GF_WBX : GF_WBY;
+        }
+      }
+    }
   }
 }
 

@@ -1176,9 +1176,20 @@ void Case::set_wall_nodes() {
 // GetWallNodes: list of wall-flagged gas cells in j-major scan order.
 void Case::collect_wall_nodes() {
   wall_nodes.clear();
+  wall_dirs.clear();
+  auto solid_or_out = [&](int i, int j) { return !J.in(i, j) || J.is(i, j, CT_SOLID); };
+  auto gas = [&](int i, int j) { return J.in(i, j) && !J.is(i, j, CT_SOLID); };
   for (int j = 0; j < J.ny; j++)
     for (int i = 0; i < J.nx; i++)
-      if (!J.is(i, j, CT_SOLID) && (J.is(i, j, CT_WALL_LAW) || J.is(i, j, CT_WALL_NO_SLIP))) wall_nodes.push_back({i, j});
+      if (!J.is(i, j, CT_SOLID) && (J.is(i, j, CT_WALL_LAW) || J.is(i, j, CT_WALL_NO_SLIP))) {
+        wall_nodes.push_back({i, j});
+        uint8_t d = 0;
+        if (gas(i + 1, j) && solid_or_out(i - 1, j)) d |= WD_XP;
+        if (gas(i - 1, j) && solid_or_out(i + 1, j)) d |= WD_XM;
+        if (gas(i, j + 1) && solid_or_out(i, j - 1)) d |= WD_YP;
+        if (gas(i, j - 1) && solid_or_out(i, j + 1)) d |= WD_YM;
+        wall_dirs.push_back(d);
+      }
 }
 
 // SetMinDistanceToWall2D (deeps2d_core.cpp:4783-4832) scans every wall node

@@ -312,6 +312,7 @@ StepParams SolverBase::make_params(long it) const {
   P.alternate_rms = C.isAlternateRMS;
   P.sm = C.ProblemType;
   P.lag_dt = (C.LaggedDt && C.semantics == Semantics::MPI) ? 1 : 0;
+  P.wall_blend = C.WallBlendCells > 0 ? 1 : 0;
   P.chem_model = C.chem_model;
   P.species = &C.species;
   FillParams f = C.fill_params();
@@ -787,7 +788,7 @@ void CpuSolver::upload() {
   h.from_field(cs.J, gi0 - l_off);
   h.wall_slots(cs, gi0 - l_off, gi0, gi1);
   h.mech_from_case(cs, gi0 - l_off);
-  compute_generic_flags(cs, h);
+  compute_generic_flags(cs, h, gi0 - l_off);
   sbuf = 0;
   dsbuf = 0;
   pbuf = 0;

@@ -182,7 +182,7 @@ int sk_eligible(const Case& cs, std::string* why);   // SK_* mode of the split k
 bool lean_any_cauchy_x(const Case& cs);
 bool mech_species_cauchy(const Case& cs);   // some node applies d2(rhoY)/dx2 or /dy2 = 0
 // per-cell GF_* flags of the generic stepper (from the uploaded host arrays)
-void compute_generic_flags(const Case& cs, HostArrays& h);
+void compute_generic_flags(const Case& cs, HostArrays& h, int gx0);
 std::vector<uint8_t> lean_flags(const HostArrays& h, int sm);
 
 class CpuSolver : public SolverBase {

@@ -35,7 +35,11 @@ enum : uint8_t { NB_XL = 1, NB_XR = 2, NB_YU = 4, NB_YD = 8 };
 //   GF_SRCADD              SrcAdd may be non-zero (wall nodes)
 // Skipped loads are replaced by the +0 the arrays provably hold, skipped
 // stores would rewrite unchanged values, so results are bit-identical.
-enum : uint8_t { GF_DX_OUT = 1, GF_DY_OUT = 2, GF_SRC = 4, GF_SRCADD = 8 };
+//   GF_WBX / GF_WBY        Config::WallBlendCells: within that many cells of an
+//                          x- / y-normal no-slip wall (predict_core drops the
+//                          wall-normal neighbours from the tangential
+//                          momentum's blend; read only with StepParams::wall_blend)
+enum : uint8_t { GF_DX_OUT = 1, GF_DY_OUT = 2, GF_SRC = 4, GF_SRCADD = 8, GF_WBX = 16, GF_WBY = 32 };
 
 // Raw SoA view.  Equation arrays are [k * N + idx], idx = i * ny + j
 // (x-major, matching the .hf2d file; a column is contiguous).
@@ -131,6 +135,7 @@ struct StepParams {
   // Config::LaggedDt: the step's dt is the all-rank MIN of two steps back
   // (device: DevScalars::dt_lag; host: SolverBase::dt_lag)
   int lag_dt = 0;
+  int wall_blend = 0;   // Config::WallBlendCells > 0: predictor accessors' gf carries GF_WBX / GF_WBY
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.
@@ -232,6 +237,12 @@ HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, rea
 // Cauchy bit, not frozen in pass 2, all four neighbours present, not
 // non-reflecting).  The flags then fold to constants; the arithmetic is the
 // same, so the result is bit-identical to the general path.
+// predictor accessors with per-cell GF_* flags (a data member gf)
+template <class IO, class = void>
+struct io_has_gf : std::false_type {};
+template <class IO>
+struct io_has_gf<IO, std::void_t<decltype(std::declval<const IO&>().gf + 0)>> : std::true_type {};
+
 template <bool RES, class IO, bool PLAIN = false>
 HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int n1, int n2, int n3, int n4, int gi,
                                int j, ResidualPack& rp) {
@@ -300,8 +311,16 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
     }
     if (f.dx2) dXX = (io.dxL(kk) + io.dxR(kk)) * 0.5;
     if (f.dy2) dYY = (io.dyU(kk) + io.dyD(kk)) * 0.5;
-    const real SL = n1 ? io.SL(kk) : s, SR = n2 ? io.SR(kk) : s;
-    const real SU = n3 ? io.SU(kk) : s, SD = n4 ? io.SD(kk) : s;
+    real SL = n1 ? io.SL(kk) : s, SR = n2 ? io.SR(kk) : s;
+    real SU = n3 ? io.SU(kk) : s, SD = n4 ? io.SD(kk) : s;
+    if constexpr (io_has_gf<IO>::value) {
+      // Config::WallBlendCells: the tangential momentum's blend leaves out
+      // the wall-normal neighbours near a no-slip wall
+      if (!PLAIN && P.wall_blend) {
+        if (k == I_RHOU && (io.gf & GF_WBY)) SU = SD = s;
+        if (k == I_RHOV && (io.gf & GF_WBX)) SL = SR = s;
+      }
+    }
     const real beta = io.beta(kk);
     const real _beta = 1. - beta;
     real snew;

@@ -2284,7 +2284,7 @@ void DeviceSolver::upload() {
   cp(m.CT, h.CT.data(), N * sizeof(u64));
   cp(m.TT, h.TT.data(), N * sizeof(u64));
   cp(m.nb, h.nb.data(), N);
-  compute_generic_flags(cs, h);
+  compute_generic_flags(cs, h, gi0 - l_off);
   cp(m.gf, h.gf.data(), N);
   chem_fast_ok = cs.cfg.mech_mode() && chem_fast_available(cs.cfg.mech->name) &&
                  mech_is_builtin(*cs.cfg.mech, cs.cfg.mech->name);

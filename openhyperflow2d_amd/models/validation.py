@@ -47,6 +47,31 @@ def van_driest_ii(re_x, mach: float, Te: float, Tw, r: float = 0.89, gamma: floa
     return 0.0592 * (frx * re_x) ** -0.2 / fc
 
 
+def _vd2_factors(mach: float, Te: float, Tw, r: float = 0.89, gamma: float = 1.4):
+    """(F_c, F_theta = mu_e / mu_w) of the van Driest II transformation."""
+    Tw = np.asarray(Tw, dtype=np.float64)
+    m = 0.5 * (gamma - 1.0) * mach * mach
+    taw_te = 1.0 + r * m
+    a = np.sqrt(r * m * Te / Tw)
+    b = taw_te * Te / Tw - 1.0
+    den = np.sqrt(4.0 * a * a + b * b)
+    fc = (taw_te - 1.0) / (np.arcsin((2.0 * a * a - b) / den) + np.arcsin(b / den)) ** 2
+    mu_w = np.array([sutherland(t) for t in np.atleast_1d(Tw)]).reshape(Tw.shape)
+    return fc, sutherland(Te) / mu_w
+
+
+def van_driest_ii_theta(re_theta, mach: float, Te: float, Tw, r: float = 0.89, gamma: float = 1.4):
+    """Turbulent Cf against the momentum-thickness Reynolds number: van Driest
+    II with the Karman-Schoenherr law, Cf = Cf_KS(F_theta Re_theta) / F_c,
+    1 / Cf_KS = 17.08 (log10 Re)^2 + 25.11 log10 Re + 6.012.  Unlike the Re_x
+    forms it does not assume a layer turbulent from the leading edge: the
+    local state of the layer (theta) carries its history, so a delayed
+    transition (the virtual origin of the turbulent layer) drops out."""
+    fc, ft = _vd2_factors(mach, Te, Tw, r, gamma)
+    lg = np.log10(ft * np.asarray(re_theta, dtype=np.float64))
+    return 1.0 / (17.08 * lg * lg + 25.11 * lg + 6.012) / fc
+
+
 def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
     """Cf, Re_x and the correlations along the plate of a flat_plate run."""
     case = sim.case
@@ -90,8 +115,18 @@ def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
             tau_eff[q] = float(np.mean([(mu[ii, j] + mut[ii, j]) * (U[ii, j + 1] - U[ii, j - 1]) / (2 * dy)
                                         for j in band]))
     cf_eff = np.sign(cf) * tau_eff / (0.5 * rhoe * Ue * Ue)
+    # momentum thickness theta = int rho U / (rho_e U_e) (1 - U / U_e) dy over
+    # the layer (up to the first node at 0.995 U_e, the inflow edge state)
+    theta = np.zeros(len(i))
+    for q, ii in enumerate(i):
+        ru = rho[ii] * U[ii] / (rhoe * Ue) * (1.0 - U[ii] / Ue)
+        top = np.nonzero(U[ii, 1:] >= 0.995 * Ue)[0]
+        jt = int(top[0]) + 1 if len(top) else ny - 1
+        theta[q] = float(np.sum(ru[:jt + 1]) * dy)
+    re_theta = rhoe * Ue * theta / mue
     return {"x": x, "Re_x": rex, "Cf": cf, "Cf_eff": cf_eff, "Cf_lam": lam, "Cf_turb": turb,
-            "Cf_turb_vd2": van_driest_ii(rex, Me, Te, Tw), "Mach": np.full_like(x, Me), "Tw": Tw}
+            "Cf_turb_vd2": van_driest_ii(rex, Me, Te, Tw), "theta": theta, "Re_theta": re_theta,
+            "Cf_vd2_theta": van_driest_ii_theta(re_theta, Me, Te, Tw), "Mach": np.full_like(x, Me), "Tw": Tw}
 
 
 def langley_phi(mc: float) -> float:

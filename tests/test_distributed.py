@@ -57,6 +57,9 @@ CASES = {
                                                    tmin=250.0), 4),
     # lagged dt (LaggedDt = 1): step n + 1 runs with the all-rank MIN of step n - 1
     "wedge15_euler_lag": (lambda: decks.set_key(decks.wedge15(90, 30, nmax=10 ** 6, nout=10 ** 5), "LaggedDt", 1), 5),
+    # near-wall blend of the tangential momentum (WallBlendCells): flags from the global wall list
+    "plate_wallblend": (lambda: decks.set_key(decks.flat_plate(90, 30, dx=1e-3, dy=4e-5, p=1e4, turbulence=6,
+                                                               nmax=10 ** 6, nout=10 ** 5), "WallBlendCells", 6), 4),
     "wedge15_ns_keps_lag": (lambda: decks.set_key(decks.wedge15(90, 30, navier_stokes=True, turbulence=4,
                                                                 nmax=10 ** 6, nout=10 ** 5), "LaggedDt", 1), 4),
 }
@@ -224,3 +227,25 @@ def test_lagged_dt_takes_the_min_of_two_steps_back(hf):
     lag.step(1)
     assert lag.summary()["dt"] == f0
     assert not np.array_equal(lag.field("rho"), std.field("rho"))
+
+
+def test_wall_blend_changes_only_the_tangential_momentum_near_walls(hf):
+    """WallBlendCells = N: after one step the plate run differs from the
+    reference scheme only in rho U of the N cells above the no-slip plate
+    (the wall-normal neighbours leave the tangential momentum's blend there);
+    N = 0 is the reference scheme bit for bit."""
+    base = decks.flat_plate(60, 40, dx=1e-3, dy=4e-5, p=1e4, turbulence=6, nmax=10 ** 6, nout=10 ** 5)
+    ref = hf.Simulation(base, "cpu")
+    off = hf.Simulation(decks.set_key(base, "WallBlendCells", 0), "cpu")
+    on = hf.Simulation(decks.set_key(base, "WallBlendCells", 5), "cpu")
+    for s in (ref, off, on):
+        s.step(1)
+    for f in ("S0", "S1", "S2", "S3"):
+        np.testing.assert_array_equal(off.field(f), ref.field(f), err_msg=f)
+    for f in ("S0", "S2", "S3"):
+        np.testing.assert_array_equal(on.field(f), ref.field(f), err_msg=f)
+    d = np.argwhere(on.field("S1") != ref.field("S1"))
+    assert len(d) > 0
+    assert set(d[:, 1].tolist()) <= set(range(1, 6)), sorted(set(d[:, 1].tolist()))
+    i_le = int(round(0.2 * 60))
+    assert d[:, 0].min() >= i_le - 1

@@ -28,6 +28,7 @@ ap.add_argument("--beta0", type=float, default=None, help="DEEPS blending factor
 ap.add_argument("--bff", type=int, default=None, help="blending-factor function (deck default 4)")
 ap.add_argument("--max-steps", type=int, default=10 ** 9)
 ap.add_argument("--sst-d1", type=float, default=None, help="SSTWallDistance (wall omega distance / dy; default 1.0, the Menter first-cell distance)")
+ap.add_argument("--wall-blend", type=int, default=0, help="WallBlendCells (near-wall blend of the tangential momentum)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
@@ -42,6 +43,8 @@ if a.beta0 is not None:
     text = decks.set_table(text, "beta_Scenario", [(0.0, a.beta0), (1.0e9, a.beta0)])
 if a.bff is not None:
     text = decks.set_key(text, "BFF", a.bff)
+if a.wall_blend:
+    text = decks.set_key(text, "WallBlendCells", a.wall_blend)
 if a.sst_d1 is not None:
     text = decks.set_key(text, "SSTWallDistance", a.sst_d1)
 sim = hf.Simulation(text, a.backend)
@@ -53,12 +56,15 @@ while sim.summary()["time"] < t_end and steps < a.max_steps:
     sim.step(2000)
     steps += 2000
 r = validation.plate_cf(sim, x_le)
-print("model %d grid %dx%d dy=%g cfl=%s beta0=%s: %d steps, t=%.3g s (%.1f s wall), lean N-S steps %s" % (
-    a.model, a.nx, a.ny, a.dy, a.cfl, a.beta0, steps, sim.summary()["time"], time.time() - t0,
+print("wall blend %d  model %d grid %dx%d dy=%g cfl=%s beta0=%s: %d steps, t=%.3g s (%.1f s wall), lean N-S steps %s" % (
+    a.wall_blend, a.model, a.nx, a.ny, a.dy, a.cfl, a.beta0, steps, sim.summary()["time"], time.time() - t0,
     getattr(sim.solver, "lns_steps", None)))
 print("Mach_e %.2f  Tw/Te %.2f..%.2f" % (r["Mach"][0], r["Tw"].min() / 288.9, r["Tw"].max() / 288.9))
 for q in (0.1, 0.25, 0.5, 0.75, 0.9):
     k = int(q * (len(r["x"]) - 1))
+    print("Re_x %9.3g  Re_theta %7.0f  Cf/vdII(Re_theta): molecular %.3f  effective %.3f  |  Cf/vdII(Re_x) "
+          "molecular %.3f" % (r["Re_x"][k], r["Re_theta"][k], r["Cf"][k] / r["Cf_vd2_theta"][k],
+                              r["Cf_eff"][k] / r["Cf_vd2_theta"][k], r["Cf"][k] / r["Cf_turb_vd2"][k]))
     print("Re_x %9.3g  Cf %.4e  Cf/lam %.3f  Cf/turb %.3f  effective (max near-wall stress) Cf/lam %.3f Cf/turb %.3f"
           "  Cf/vdII %.3f" % (
               r["Re_x"][k], r["Cf"][k], r["Cf"][k] / r["Cf_lam"][k], r["Cf"][k] / r["Cf_turb"][k],
