@@ -24,6 +24,7 @@ namespace hf2d {
 using real = double;
 using u64 = std::uint64_t;
 
+
 // ---------------------------------------------------------------------------
 // Species / equation layout (NUM_COMPONENTS = 3 additional species + inert).
 // ---------------------------------------------------------------------------

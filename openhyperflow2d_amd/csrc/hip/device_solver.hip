@@ -387,81 +387,107 @@ struct FusedX {
   int defer;
 };
 
-__device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, DevScalars* sc) {
-  if (__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) return false;
-  for (int q = 0; q < x.nranks; q++) {
-    if (q == x.rank) continue;
+// Peer waits and publications are spread over the lanes of one wavefront:
+// lane q polls / publishes to peer q (q < nranks <= 64 per pass), so a step
+// costs one round trip to the fine-grained mailbox per phase instead of one
+// per peer (the single-thread loops cost ~12 us per step on an 8-rank strip,
+// tools/exchange_loopback.py, profiles/exchange_loopback_r05.md).
+__device__ inline double wave_min(double v) {
+#pragma unroll
+  for (int off = 1; off < WAVE; off <<= 1) v = fmin(v, __shfl_xor(v, off, WAVE));
+  return v;
+}
+// Every lane of the calling wavefront: wait (bounded) for the flags of the
+// peers q with need(q) to reach target (acquire), and return the MIN of
+// their dt of parity par (fold) -- or 1.0 without fold.  False through *ok
+// after a timeout (neg_T bit 2) or an earlier one.
+template <class Need>
+__device__ inline double p2p_wait_wave(const FusedX& x, unsigned long long target, DevScalars* sc, Need need,
+                                       bool fold, int par, bool* ok) {
+  const int lane = (int)(threadIdx.x & (WAVE - 1));
+  bool good = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
+  double d = 1.0;
+  for (int q = lane; q < x.nranks && good; q += WAVE) {
+    if (q == x.rank || !need(q)) continue;
     long spins = 0;
-    while (__hip_atomic_load(&x.my_flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
-      // every workgroup of the step polls: back off harder than the
-      // single-workgroup exchange kernel so the pollers do not flood HBM
-      __builtin_amdgcn_s_sleep(16);
-      if (++spins > P2P_SPIN_LIMIT / 8) {
+    while (__hip_atomic_load(&x.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > P2P_SPIN_LIMIT) {
         atomicOr(&sc->neg_T, 2);
-        return false;
+        good = false;
+        break;
       }
     }
+    // acquire the peer's publication: its dt and mailbox stores (released by
+    // its vmcnt drain before the flag) are visible to every load ordered
+    // after this one, here and in later kernels
+    if (good) (void)p2p_acquire(&x.my_flags[q]);
+    if (good && fold) d = fmin(d, p2p_load(x.my_dtr + par * x.nranks + q));
   }
-  return true;
+  *ok = __ballot(!good) == 0;
+  return wave_min(d);
+}
+__device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, DevScalars* sc) {
+  bool ok;
+  (void)p2p_wait_wave(x, target, sc, [](int) { return true; }, false, 0, &ok);
+  return ok;
 }
 
-// Tail of a step kernel with the exchange fused in (thread 0 of every
+// Tail of a step kernel with the exchange fused in (wavefront 0 of every
 // workgroup, after the workgroup's mailbox stores and dt MIN): the last
 // workgroup to finish publishes this rank's step (its dt to every peer, then
 // flag seq_prev + 1), waits (bounded) for every peer's flag of the same step
-// and folds their dt into the slot the next step reads.
+// -- the two neighbours' only with X.defer -- and folds their dt into the
+// slot the next step reads.
 __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
                                         unsigned long long seq_prev, bool fold = true) {
-  // the workgroup barrier drained every wave's mailbox stores; drain the dt
-  // atomic before counting this workgroup as done
+  const int lane = (int)(threadIdx.x & (WAVE - 1));
+  // the workgroup barrier drained every wave's mailbox stores; drain lane
+  // 0's dt atomic before counting this workgroup as done
   vm_drain();
   // completion count in two levels (one counter per dt shard, then one for
   // the shards): a single counter serialises every workgroup's returning
   // atomic at the memory side
-  const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
-  const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
-  unsigned* cs = X.done + sh * FX_DONE_STRIDE;
-  unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
-  bool last = false;
-  if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
-    __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
-      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = true;
-    }
-  }
-  if (!last) return;
-  // last workgroup: publish this rank's step, then fold the peers'
-  const unsigned long long sn = seq_prev + 1;
-  const int pn = (int)(sn & 1);
-  double d = dt_get_fresh(sc, slot_next);
-  for (int q = 0; q < X.nranks; q++)
-    if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
-  vm_drain();
-  for (int q = 0; q < X.nranks; q++)
-    if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  bool ok = !(__hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2);
-  for (int q = 0; q < X.nranks && ok; q++) {
-    if (q == X.rank) continue;
-    if (X.defer && q != X.rank - 1 && q != X.rank + 1) continue;   // (halo senders only)
-    long spins = 0;
-    while (__hip_atomic_load(&X.my_flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < sn) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > P2P_SPIN_LIMIT) {
-        atomicOr(&sc->neg_T, 2);
-        ok = false;
-        break;
+  int last = 0;
+  if (lane == 0) {
+    const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
+    const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
+    unsigned* cs = X.done + sh * FX_DONE_STRIDE;
+    unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
+    if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
+      __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+        __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
       }
     }
-    // acquire the peer's publication: its dt and mailbox stores (released
-    // by its vmcnt drain before the flag) are visible to every load ordered
-    // after this one, here and in later kernels
-    if (ok) (void)p2p_acquire(&X.my_flags[q]);
-    if (ok) d = fmin(d, p2p_load(X.my_dtr + pn * X.nranks + q));
   }
-  if (fold && !X.defer)
-    __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  *X.seq = sn;
+  if (!__shfl(last, 0, WAVE)) return;
+  // last workgroup: this rank's dt (word + shards, one per lane), published
+  // to every peer (one peer per lane), then the flags, then the peers'
+  const unsigned long long sn = seq_prev + 1;
+  const int pn = (int)(sn & 1);
+  unsigned long long b = ~0ull;
+  if (lane < DT_SHARDS)
+    b = __hip_atomic_load(&sc->dt_sh[slot_next][lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == DT_SHARDS) b = __hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double d = wave_min(b == ~0ull ? 1.0 : bits_to_d(b));
+  for (int q = lane; q < X.nranks; q += WAVE)
+    if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
+  vm_drain();   // (the wavefront's stores: every lane's)
+  for (int q = lane; q < X.nranks; q += WAVE)
+    if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const bool defer = X.defer != 0;
+  const int r = X.rank;
+  bool ok;
+  const double peers = p2p_wait_wave(X, sn, sc, [=](int q) { return !defer || q == r - 1 || q == r + 1; },
+                                     fold && !defer, pn, &ok);
+  d = fmin(d, peers);
+  if (lane == 0) {
+    if (fold && !defer && ok)
+      __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *X.seq = sn;
+  }
 }
 
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
@@ -522,21 +548,22 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
   apply_dt(P, sc, slot);
-  if (b == 0 && threadIdx.x == 0) {
-    dt_reset(sc, slot_reset(slot));
+  if (b == 0 && threadIdx.x < WAVE) {
     // lagged dt with the fold deferred (X.defer): the previous step's tail
     // waited for the two neighbours only; the other ranks' dt of that step
-    // is folded here, one step later, by this one thread
+    // is folded here, one step later, by this wavefront (one peer per lane)
     double fold = 1.0;
-    if (FX && X.defer && P.lag_dt && seq_prev > 0 && p2p_wait_all(X, seq_prev, sc)) {
-      const int pp = (int)(seq_prev & 1);
-      for (int q = 0; q < X.nranks; q++)
-        if (q != X.rank) fold = fmin(fold, p2p_load(X.my_dtr + pp * X.nranks + q));
+    if (FX && X.defer && P.lag_dt && seq_prev > 0) {
+      bool ok;
+      fold = p2p_wait_wave(X, seq_prev, sc, [](int) { return true; }, true, (int)(seq_prev & 1), &ok);
     }
-    lag_head(P, sc, slot, slot_next, fold);
-    sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
-    sc->time_part += P.dt;
-    scenario_next(P, sc, slot, slot_next);
+    if (threadIdx.x == 0) {
+      dt_reset(sc, slot_reset(slot));
+      lag_head(P, sc, slot, slot_next, fold);
+      sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
+      sc->time_part += P.dt;
+      scenario_next(P, sc, slot, slot_next);
+    }
   }
   int i[CPT], j[CPT], c[CPT], i0, j0;
   bool mine[CPT];
@@ -558,11 +585,20 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     const long N = L.N;
     constexpr int NS = SG ? 4 : 4 + NCOMP;
     constexpr int FU = SG ? 4 : 10;
+    const int sii = NT / T.W, sq = NT - sii * T.W;
+    int ii = (int)threadIdx.x / T.W - 1, q = (int)threadIdx.x - (ii + 1) * T.W;
     for (int c = threadIdx.x; c < T.NC; c += NT) {
-      const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
+      const int jj = q - 1;
       const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
       const int gi = i0 + ii, gj = j0 + jj;
-      if ((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
+      const bool ok = !((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny);
+      ii += sii;
+      q += sq;
+      if (q >= T.W) {
+        q -= T.W;
+        ii++;
+      }
+      if (!ok) continue;
       const bool gl = (X.sides & 1) && gi == P.i0 - 1, gr = (X.sides & 2) && gi == P.i1;
       if (gl || gr) {
         const real* mb = gl ? mbL : mbR;
@@ -647,8 +683,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       o[6] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
       o[7] = blockIdx.x;
     }
-    if (FX) fx_tail(X, sc, slot_next, seq_prev);
   }
+  if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
 }
 
 // No occupancy attribute on the default kernel: the backend's own register
@@ -707,7 +743,10 @@ __global__ __launch_bounds__(P2P_THREADS) void hf2d_p2p_complete(ColList Lc, int
   const unsigned long long sq = *X.seq;
   if (sq == 0) return;
   __shared__ int ok;
-  if (threadIdx.x == 0) ok = p2p_wait_all(X, sq, sc) ? 1 : 0;
+  if (threadIdx.x < WAVE) {
+    const bool w = p2p_wait_all(X, sq, sc);
+    if (threadIdx.x == 0) ok = w ? 1 : 0;
+  }
   __syncthreads();
   if (!ok) return;
   const int pp = (int)(sq & 1);
@@ -964,8 +1003,8 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     for (int q = 1; q < BLOCK / WAVE; q++) m = fmin(m, sdt[q]);
     if (serial) m = fmin(m, P.dt);
     dt_min(sc, slot_next, m);
-    if (FX) fx_tail(X, sc, slot_next, seq_prev);
   }
+  if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
 }
 
 template <bool RES, int MODE, int TURB = 2>
@@ -1031,13 +1070,13 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
   vm_drain();
   if (!publish) return;
   __syncthreads();
-  if (threadIdx.x == 0) fx_tail(X, sc, dslot, seq_prev, fold != 0);
+  if (threadIdx.x < WAVE) fx_tail(X, sc, dslot, seq_prev, fold != 0);
 }
 
 // One workgroup: publish the step whose halo an earlier hf2d_p2p_push
 // (publish = 0) stored, wait for the peers' publication, fold their dt.
 __global__ void hf2d_p2p_finish(FusedX X, DevScalars* sc, int dslot) {
-  if (threadIdx.x == 0) fx_tail(X, sc, dslot, *X.seq, true);
+  fx_tail(X, sc, dslot, *X.seq, true);   // (one wavefront)
 }
 
 // The scalars the host reads (the words before the dt shards, and the shards
@@ -4228,7 +4267,7 @@ std::string DeviceSolver::autotune(int steps) {
   if (nstep != 0 || iter != 0) return "";
   if (ns ? !(lean_ns && lns_ok) : !(lean_ok && lean_tile)) return "";
   flush_pending();
-  const real s_dt = dt, s_dtr = dt_running, s_cur = cur_time_part, s_gt = cs.global_time;
+  const real s_dt = dt, s_dtr = dt_running, s_cur = cur_time_part, s_gt = cs.global_time, s_lag = dt_lag;
   const long s_iter = iter, s_last = last_iter;
   const int s_cycle = cycle;
   const bool s_src = isSrcAdd, s_out = step_outputs;
@@ -4339,6 +4378,7 @@ std::string DeviceSolver::autotune(int steps) {
   graph.reset();
   dt = s_dt;
   dt_running = s_dtr;
+  dt_lag = s_lag;
   cur_time_part = s_cur;
   cs.global_time = s_gt;
   iter = s_iter;
