@@ -746,6 +746,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("grad_every", &DeviceSolver::grad_every)
       .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
       .def_readwrite("comm_overlap", &DeviceSolver::comm_overlap)
+      .def_readwrite("lnm_overlap", &DeviceSolver::lnm_overlap)
       .def_readwrite("lean_ns", &DeviceSolver::lean_ns)
       .def_readwrite("lns_occ", &DeviceSolver::lns_occ)
       .def_readonly("lns_ok", &DeviceSolver::lns_ok)

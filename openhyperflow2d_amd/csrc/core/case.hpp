@@ -69,6 +69,10 @@ struct Config {
   // otherwise; profiles/flat_plate_validation.md).  The streamwise blend,
   // and every other equation's, are unchanged.
   int WallBlendCells = 0;
+  // ... keeping this fraction of the wall-normal neighbours' weight (0: none;
+  // removing it altogether leaves the wide-stencil viscous term without
+  // odd-even damping: the SST plate went unstable within 2000 steps)
+  real WallBlendFactor = 0.0;
   // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
   // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
   int ThreadBlockSize = 0;

@@ -121,6 +121,7 @@ void config_io(IO& io, C& c) {
   io.pod(c.SSTWallDistance);
   io.pod(c.LaggedDt);
   io.pod(c.WallBlendCells);
+  io.pod(c.WallBlendFactor);
   io.pod(c.ThreadBlockSize);
   io.table(c.CFL_Scenario);
   io.table(c.beta_Scenario);

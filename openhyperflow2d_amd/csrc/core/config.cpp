@@ -28,6 +28,7 @@ void Config::load_globals(InputDeck& d) {
   SSTWallDistance = d.get_float_or("SSTWallDistance", 1.0);
   LaggedDt = d.get_int_or("LaggedDt", 0) ? 1 : 0;
   WallBlendCells = std::max(0, d.get_int_or("WallBlendCells", 0));
+  WallBlendFactor = std::min(1.0, std::max(0.0, (double)d.get_float_or("WallBlendFactor", 0.0)));
   ThreadBlockSize = d.get_int_or("ThreadBlockSize", 0);
   NSaveStep = d.get_int("NSaveStep");
   Nmax = d.get_int("Nmax");

@@ -313,6 +313,7 @@ StepParams SolverBase::make_params(long it) const {
   P.sm = C.ProblemType;
   P.lag_dt = (C.LaggedDt && C.semantics == Semantics::MPI) ? 1 : 0;
   P.wall_blend = C.WallBlendCells > 0 ? 1 : 0;
+  P.wall_blend_f = C.WallBlendFactor;
   P.chem_model = C.chem_model;
   P.species = &C.species;
   FillParams f = C.fill_params();

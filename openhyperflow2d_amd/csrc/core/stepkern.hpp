@@ -136,6 +136,7 @@ struct StepParams {
   // (device: DevScalars::dt_lag; host: SolverBase::dt_lag)
   int lag_dt = 0;
   int wall_blend = 0;   // Config::WallBlendCells > 0: predictor accessors' gf carries GF_WBX / GF_WBY
+  real wall_blend_f = 0;   // Config::WallBlendFactor
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.
@@ -317,8 +318,15 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
       // Config::WallBlendCells: the tangential momentum's blend leaves out
       // the wall-normal neighbours near a no-slip wall
       if (!PLAIN && P.wall_blend) {
-        if (k == I_RHOU && (io.gf & GF_WBY)) SU = SD = s;
-        if (k == I_RHOV && (io.gf & GF_WBX)) SL = SR = s;
+        const real f = P.wall_blend_f;
+        if (k == I_RHOU && (io.gf & GF_WBY)) {
+          SU = s + f * (SU - s);
+          SD = s + f * (SD - s);
+        }
+        if (k == I_RHOV && (io.gf & GF_WBX)) {
+          SL = s + f * (SL - s);
+          SR = s + f * (SR - s);
+        }
       }
     }
     const real beta = io.beta(kk);

@@ -385,6 +385,10 @@ struct FusedX {
   // the dt MIN to the next step's first workgroup (lean_tile_body) or to
   // hf2d_p2p_complete
   int defer;
+  // cost attribution of the fused exchange (HF2D_FX_SKIP, timing only, wrong
+  // results): bit 0 no tail, bit 1 no edge pushes, bit 2 ghosts staged from
+  // the state arrays instead of the mailbox
+  int skip;
 };
 
 // Peer waits and publications are spread over the lanes of one wavefront:
@@ -574,7 +578,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     mine[q] = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i[q], &j[q], &c[q], &i0, &j0, q);
     if (mine[q]) lean_load_own<TileIO<SG>::NE>(L, (long)i[q] * P.ny + j[q], own[q]);
   }
-  if (!FX || seq_prev == 0 || (i0 - 1 > P.i0 - 1 && i0 + T.TI < P.i1)) {
+  if (!FX || seq_prev == 0 || (X.skip & 4) || (i0 - 1 > P.i0 - 1 && i0 + T.TI < P.i1)) {
     lean_tile_stage<SG>(P, L, T, i0, j0, lds, threadIdx.x, NT);
   } else {
     // edge tile: the ghost column comes from the mailbox of parity seq_prev
@@ -585,20 +589,11 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     const long N = L.N;
     constexpr int NS = SG ? 4 : 4 + NCOMP;
     constexpr int FU = SG ? 4 : 10;
-    const int sii = NT / T.W, sq = NT - sii * T.W;
-    int ii = (int)threadIdx.x / T.W - 1, q = (int)threadIdx.x - (ii + 1) * T.W;
     for (int c = threadIdx.x; c < T.NC; c += NT) {
-      const int jj = q - 1;
+      const int ii = c / T.W - 1, jj = c - (ii + 1) * T.W - 1;
       const bool xh = ii < 0 || ii >= T.TI, yh = jj < 0 || jj >= T.TJ;
       const int gi = i0 + ii, gj = j0 + jj;
-      const bool ok = !((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny);
-      ii += sii;
-      q += sq;
-      if (q >= T.W) {
-        q -= T.W;
-        ii++;
-      }
-      if (!ok) continue;
+      if ((xh && yh) || gi < 0 || gi >= P.nx || gj < 0 || gj >= P.ny) continue;
       const bool gl = (X.sides & 1) && gi == P.i0 - 1, gr = (X.sides & 2) && gi == P.i1;
       if (gl || gr) {
         const real* mb = gl ? mbL : mbR;
@@ -634,7 +629,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       dtl = fmin(dtl, lean_cell<RES, OUT>(P, L, io, own[q], i[q], j[q], r, &neg));
       if (FX) {
         const bool pl = (X.sides & 1) && i[q] == P.i0, pr = (X.sides & 2) && i[q] == P.i1 - 1;
-        if (pl || pr) {   // new lean state of an edge cell -> the neighbour's mailbox of parity seq_prev + 1
+        if ((pl || pr) && !(X.skip & 2)) {   // new lean state of an edge cell -> the neighbour's mailbox of parity seq_prev + 1
           constexpr int NF = SG ? LEAN_TILE_FIELDS_SG : LEAN_TILE_FIELDS;
           constexpr int NS = SG ? 4 : 4 + NCOMP;
           const int pn = (int)((seq_prev + 1) & 1);
@@ -684,7 +679,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       o[7] = blockIdx.x;
     }
   }
-  if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
+  if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev);
 }
 
 // No occupancy attribute on the default kernel: the backend's own register
@@ -3406,6 +3401,8 @@ FusedX DeviceSolver::fused_args() const {
   X.nranks = m.nranks;
   X.sides = (has_left ? 1 : 0) | (has_right ? 2 : 0);
   X.on = 1;
+  static const int skip = std::getenv("HF2D_FX_SKIP") ? std::atoi(std::getenv("HF2D_FX_SKIP")) : 0;
+  X.skip = m.p2p.loop ? skip : 0;   // (loopback timing runs only)
   return X;
 }
 
@@ -3699,8 +3696,13 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
   // then the dt MIN (as the lean N-S and inviscid tile kernels)
   // (the decision must be the same on every rank -- the exchange sequence
   // differs -- so a strip too narrow to split runs all its tiles at once)
-  static const bool split_env = !std::getenv("HF2D_LNM_SPLIT") || std::string(std::getenv("HF2D_LNM_SPLIT")) != "0";
-  lnm_split = split_env && comm_overlap && (m.p2p.on ? p2p_fuse : (m.comm || m.local)) && m.nranks > 1 &&
+  // Opt-in (lnm_overlap / HF2D_LNM_SPLIT=1): the edge part is one
+  // workgroup round of ~50 tiles on an otherwise idle GPU before the interior
+  // starts, so on the mailbox transport the split step measured 109 us of
+  // exchange cost against 17 us for all tiles + push / unpack
+  // (tools/exchange_loopback.py, scramjet 8 ranks, profiles/exchange_loopback_r05.md)
+  static const bool split_env = std::getenv("HF2D_LNM_SPLIT") && std::string(std::getenv("HF2D_LNM_SPLIT")) == "1";
+  lnm_split = (split_env || lnm_overlap) && comm_overlap && (m.p2p.on ? p2p_fuse : (m.comm || m.local)) && m.nranks > 1 &&
               !want_res && cs.cfg.isAdiabaticWall;
   const bool parts = T.nbi >= 2 + T.ne;
   // (xGMI mailboxes: the edge halo is pushed before the interior tiles run,

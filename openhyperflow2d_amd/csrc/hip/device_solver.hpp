@@ -117,6 +117,7 @@ class DeviceSolver : public SolverBase {
   // RCCL / in-process transports: halo of the edge tiles on a comm stream while
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
+  bool lnm_overlap = false;   // mechanism step: edge tiles first, halo overlapped with the interior (opt-in)
   bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
   bool lnm_split = false;   // this lean mechanism step ran edge-first with its halo overlapped
   bool lns_fx = false;      // this lean N-S step exchanged through the fused mailbox kernel

@@ -29,6 +29,7 @@ ap.add_argument("--bff", type=int, default=None, help="blending-factor function 
 ap.add_argument("--max-steps", type=int, default=10 ** 9)
 ap.add_argument("--sst-d1", type=float, default=None, help="SSTWallDistance (wall omega distance / dy; default 1.0, the Menter first-cell distance)")
 ap.add_argument("--wall-blend", type=int, default=0, help="WallBlendCells (near-wall blend of the tangential momentum)")
+ap.add_argument("--wall-blend-factor", type=float, default=0.0, help="WallBlendFactor")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
@@ -45,6 +46,7 @@ if a.bff is not None:
     text = decks.set_key(text, "BFF", a.bff)
 if a.wall_blend:
     text = decks.set_key(text, "WallBlendCells", a.wall_blend)
+    text = decks.set_key(text, "WallBlendFactor", a.wall_blend_factor)
 if a.sst_d1 is not None:
     text = decks.set_key(text, "SSTWallDistance", a.sst_d1)
 sim = hf.Simulation(text, a.backend)
@@ -56,8 +58,8 @@ while sim.summary()["time"] < t_end and steps < a.max_steps:
     sim.step(2000)
     steps += 2000
 r = validation.plate_cf(sim, x_le)
-print("wall blend %d  model %d grid %dx%d dy=%g cfl=%s beta0=%s: %d steps, t=%.3g s (%.1f s wall), lean N-S steps %s" % (
-    a.wall_blend, a.model, a.nx, a.ny, a.dy, a.cfl, a.beta0, steps, sim.summary()["time"], time.time() - t0,
+print("wall blend %d (factor %g)  model %d grid %dx%d dy=%g cfl=%s beta0=%s: %d steps, t=%.3g s (%.1f s wall), lean N-S steps %s" % (
+    a.wall_blend, a.wall_blend_factor, a.model, a.nx, a.ny, a.dy, a.cfl, a.beta0, steps, sim.summary()["time"], time.time() - t0,
     getattr(sim.solver, "lns_steps", None)))
 print("Mach_e %.2f  Tw/Te %.2f..%.2f" % (r["Mach"][0], r["Tw"].min() / 288.9, r["Tw"].max() / 288.9))
 for q in (0.1, 0.25, 0.5, 0.75, 0.9):
