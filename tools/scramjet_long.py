@@ -85,7 +85,7 @@ def main():
         done += a.chunk
         T = np.asarray(sim.field("T"))
         act = T[T > 0]
-        print("step %6d dt %.4e  T %.1f .. %.1f  hot %.1f %%  lean steps %d  (%.0f s)" % (
+        print("step %6d dt %.17g  T %.1f .. %.1f  hot %.1f %%  lean steps %d  (%.0f s)" % (
             done, sim.summary()["dt"], act.min(), act.max(), 100 * (T >= tchem).mean(), sim.solver.lnm_steps,
             time.time() - t0), flush=True)
         cold = coldest(sim, T)
