@@ -151,7 +151,8 @@ PYBIND11_MODULE(_hf2d, m) {
       [](const std::string& mech, py::array_t<double, py::array::c_style | py::array::forcecast> rhoY,
          py::array_t<double, py::array::c_style | py::array::forcecast> rho,
          py::array_t<double, py::array::c_style | py::array::forcecast> e,
-         py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub, int repeats) {
+         py::array_t<double, py::array::c_style | py::array::forcecast> T, double dt, int nsub, int repeats,
+         bool valu) {
         auto mi = mech.find('\n') == std::string::npos ? load_mechanism(mech) : parse_mechanism(mech);
         const long n = (long)rho.size();
         if (rhoY.ndim() != 2 || rhoY.shape(0) != mi->data.ns || rhoY.shape(1) != n || e.size() != n || T.size() != n)
@@ -164,12 +165,12 @@ PYBIND11_MODULE(_hf2d, m) {
         {
           py::gil_scoped_release nogil;
           ms = chem_mech_run_host(mi->data, y.mutable_data(), rho.data(), e.data(), Tout.mutable_data(), n, dt, nsub,
-                                  repeats);
+                                  repeats, valu);
         }
         return py::make_tuple(y, Tout, ms);
       },
       py::arg("mech"), py::arg("rhoY"), py::arg("rho"), py::arg("e"), py::arg("T"), py::arg("dt"), py::arg("nsub") = 1,
-      py::arg("repeats") = 1);
+      py::arg("repeats") = 1, py::arg("valu") = false);
   m.attr("CHEM_MECH_MAX_REACTIONS") = chem_mech_max_reactions();
   m.def("request_stop", &request_stop, "ask a running driver to finish the cycle, write outputs and return");
   m.def("stop_requested", &stop_requested);

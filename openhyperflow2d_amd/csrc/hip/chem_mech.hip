@@ -433,8 +433,28 @@ std::unique_ptr<ChemMechPack> chem_mech_pack(const MechData& md) {
   return pk;
 }
 
+// Runtime-data VALU form of the operator: one cell per lane, the host
+// integrator's template (core/mechanism.hpp mech_chem_cell) over the
+// MechData block in device memory.  Like hf2d_chem_mech, and unlike the
+// compiled chem_fast / hiprtc kernels, every stoichiometric coefficient, rate
+// parameter and efficiency is read at run time, so the two measure the
+// matrix cores against the vector ALUs on the same work.
+__global__ __launch_bounds__(64) void hf2d_chem_rt_valu(const MechData* md, MechCells q, double dt, int nsub) {
+  const long cell = q.c0 + (long)blockIdx.x * 64 + threadIdx.x;
+  if (cell >= q.c1) return;
+  const int ns = md->ns;
+  double rhoY[MECH_MAXSP];
+  for (int s = 0; s < ns; s++) rhoY[s] = q.Yin[(long)s * q.N + cell];
+  const double rho = q.S[cell];
+  const double e = q.S[3 * q.N + cell] / rho;   // (at rest: the standalone operator's states)
+  double T = q.Tprev[cell];
+  mech_chem_cell<MECH_MAXSP>(*md, rho, e, rhoY, &T, dt, nsub);
+  for (int s = 0; s < ns; s++) q.Yout[(long)s * q.N + cell] = rhoY[s];
+  q.Tout[cell] = T;
+}
+
 double chem_mech_run_host(const MechData& md, double* rhoY, const double* rho, const double* e, double* T, long n,
-                          double dt, int nsub, int repeats) {
+                          double dt, int nsub, int repeats, bool valu) {
   if (n < 1 || nsub < 1) throw std::runtime_error("chem_mech: need n >= 1 and nsub >= 1");
   for (long i = 0; i < n; i++)
     if (!(T[i] > 0.0) || !(rho[i] > 0.0)) throw std::runtime_error("chem_mech: T and rho must be > 0 and finite");
@@ -477,9 +497,24 @@ double chem_mech_run_host(const MechData& md, double* rhoY, const double* rho, c
   ck(hipEventCreate(&e0), "event");
   ck(hipEventCreate(&e1), "event");
   float total = 0.f;
+  struct DevMech {
+    MechData* p = nullptr;
+    ~DevMech() {
+      if (p) (void)hipFree(p);
+    }
+  } dm;
+  if (valu) {
+    ck(hipMalloc(&dm.p, sizeof(MechData)), "malloc");
+    ck(hipMemcpy(dm.p, &md, sizeof(MechData), hipMemcpyHostToDevice), "h2d");
+  }
   for (int it = 0; it < std::max(repeats, 1); it++) {
     ck(hipEventRecord(e0, 0), "record");
-    ck((hipError_t)chem_mech_launch(pk->dev, q, dt, nsub, 0), "launch");
+    if (valu) {
+      hipLaunchKernelGGL(hf2d_chem_rt_valu, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, 0, dm.p, q, dt, nsub);
+      ck(hipGetLastError(), "launch");
+    } else {
+      ck((hipError_t)chem_mech_launch(pk->dev, q, dt, nsub, 0), "launch");
+    }
     ck(hipEventRecord(e1, 0), "record");
     ck(hipEventSynchronize(e1), "sync");
     float ms = 0.f;

@@ -59,7 +59,10 @@ int chem_mech_launch(const ChemMechDev& m, const MechCells& q, double dt, int ns
 
 // Standalone operator: rhoY [ns][n] and T updated in place at constant (rho, e).
 // Returns the mean kernel time in ms over `repeats` runs from the same input.
+// valu: the same operator on the vector ALUs from the same runtime data
+// (hf2d_chem_rt_valu: core/mechanism.hpp mech_chem_cell, one cell per lane) --
+// the equal-terms baseline of the MFMA kernel (PARITY.md, K12).
 double chem_mech_run_host(const MechData& md, double* rhoY, const double* rho, const double* e, double* T, long n,
-                          double dt, int nsub, int repeats);
+                          double dt, int nsub, int repeats, bool valu = false);
 
 }  // namespace hf2d

@@ -50,9 +50,10 @@ def mech_step_gpu(mech: Mechanism, rhoY: np.ndarray, rho: np.ndarray, e: np.ndar
             np.ascontiguousarray(T, dtype=np.float64), float(dt), int(nsub), int(repeats))
     if kernel == "fast":
         return m.chem_fast_run(mech.name, *args)
-    if kernel != "mfma":
-        raise ValueError("kernel must be 'fast' or 'mfma'")
-    return m.chem_mech_run(mech.to_text(), *args)
+    if kernel not in ("mfma", "valu"):
+        raise ValueError("kernel must be 'fast', 'mfma' or 'valu'")
+    # 'valu': the runtime-data VALU form of the MFMA kernel's operator (equal terms)
+    return m.chem_mech_run(mech.to_text(), *args, valu=kernel == "valu")
 
 
 def demo_state(mech: Mechanism, ncell: int, seed: int = 0, T_range=(1000.0, 2600.0)):

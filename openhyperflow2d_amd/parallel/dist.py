@@ -3,8 +3,10 @@
 GPU ranks: torch.distributed only bootstraps.  By default every rank exports
 an IPC descriptor of its fine-grained xGMI mailbox, the descriptors are
 all-gathered once, and afterwards each step's exchange (halo columns to the
-strip neighbours + every rank's dt, MIN-folded on device) is ONE device kernel
-per rank (DeviceSolver p2p transport, hf2d_p2p_xchg).  ``transport="rccl"``
+strip neighbours + every rank's dt, MIN-folded on device) runs on the device:
+fused into the inviscid and lean N-S tile kernels (edge cells push, the last
+workgroup's wavefront publishes and waits), or as hf2d_p2p_push / unpack
+after the mechanism step (DeviceSolver p2p transport).  ``transport="rccl"``
 (or HF2D_TRANSPORT=rccl) instead issues pack + grouped ncclSend/ncclRecv +
 unpack on the solver stream.  Either way the inner loop never returns to
 Python and is captured in step graphs.
@@ -161,11 +163,11 @@ class DistributedSimulation:
         if self._all_ok(ok, nccl):
             self.transport = "p2p"
             self.p2p_validated = True
-            # the exchange is folded into the lean tile kernel (one kernel per
-            # step, the last workgroup publishes and waits); HF2D_P2P_FUSE=0
-            # selects tile kernel + hf2d_p2p_xchg.  One-GPU proxy
-            # (tools/p2p_probe.py --tail): 18.6 vs 21.7 us/step for a 250-column
-            # strip (profiles/p2p_fused_virtual2_kernels.md)
+            # the exchange is folded into the tile kernels (the last workgroup
+            # publishes and waits, one peer per lane); HF2D_P2P_FUSE=0 selects a
+            # separate exchange kernel.  Device-side cost per step without a
+            # second strip on the GPU: tools/exchange_loopback.py
+            # (profiles/exchange_loopback_r05.md)
             s.p2p_fuse = os.environ.get("HF2D_P2P_FUSE", "1") == "1"
         else:
             if not nccl:

@@ -1,6 +1,7 @@
 """K12 kinetics benchmark: one kinetics call on a scramjet-sized field (6000x400 =
 2.4 M cells, the built-in 9-species / 21-step Li et al. H2/air mechanism) with the
-compiled VALU kernel and the runtime-mechanism MFMA kernel, each checked on a cell
+compiled VALU kernel, the runtime-mechanism MFMA kernel and the same runtime-data
+operator on the vector ALUs (the MFMA kernel's equal-terms baseline), each checked on a cell
 subset against the NumPy FP64 oracle.  Prints one JSON line per kernel."""
 import argparse
 import json
@@ -24,7 +25,7 @@ def main():
     a = ap.parse_args()
     m = mech.Mechanism.load(a.mech) if a.mech else mech.h2_air_li2004()
     bad = False
-    for k in (["fast", "mfma"] if not a.mech else ["mfma"]):
+    for k in (["fast", "mfma", "valu"] if not a.mech else ["mfma", "valu"]):
         res = ch.benchmark(m, a.nx * a.ny, a.dt, a.nsub, a.repeats, kernel=k)
         print(json.dumps(res), flush=True)
         bad = bad or not res["incr_err_vs_numpy_fp64"] < 1e-8
