@@ -4007,7 +4007,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
       // re-runs F_{n+1}, which reads the lagged state from the [cbuf] buffers
       // as after a lean step: keep level n there (without it the re-fill read
       // stale buffers: with a download after every step the scramjet's dt
-      // left the CPU stepper's at step 4, tools/download_effect.py)
+      // left the CPU stepper's at step 4; test_download_after_every_step_leaves_the_trajectory_unchanged)
       const size_t SB = (size_t)h.N * sizeof(real);
       HIP_CHECK(hipMemcpyAsync(m.CP2, m.CP, SB, hipMemcpyDeviceToDevice, st));
       HIP_CHECK(hipMemcpyAsync(m.kk2, m.kk, SB, hipMemcpyDeviceToDevice, st));

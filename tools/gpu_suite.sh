@@ -34,10 +34,10 @@ run_configs() {
   done
 }
 run_strips() {
-  for w in 250 500; do
-    timeout -k 10 240 python tools/p2p_probe.py --nx $((w + 10)) --tail 10 --autotune --steps 2000 --warmup 200 \
-      > gpurun_out/p2p_tail$w.log 2>&1 &&
-    timeout -k 10 240 python bench.py --nx $w --steps 2000 --warmup 200 > gpurun_out/bench_nx$w.log 2>&1 || return 1
+  # one strip of the 8 / 4-rank headline split alone and with the mailbox exchange (loopback)
+  for n in 8 4; do
+    timeout -k 10 240 python tools/exchange_loopback.py --config wedge15 --ranks $n >> gpurun_out/loopback.jsonl \
+      2> gpurun_out/loopback_$n.err || return 1
   done
 }
 run_prof() {
