@@ -238,11 +238,14 @@ HF_HD inline real blend_beta(int bff, real beta_min, real beta_old, real DD, rea
 // Cauchy bit, not frozen in pass 2, all four neighbours present, not
 // non-reflecting).  The flags then fold to constants; the arithmetic is the
 // same, so the result is bit-identical to the general path.
-// predictor accessors with per-cell GF_* flags (a data member gf)
+// predictor accessors that carry the Config::WallBlendCells flags (a static
+// member kWallBlend): only the split path's SoAPredictIO, so the lean N-S /
+// mechanism tile kernels compile the blend out (the device solver sends a
+// WallBlendCells deck down the split path)
 template <class IO, class = void>
-struct io_has_gf : std::false_type {};
+struct io_wall_blend : std::false_type {};
 template <class IO>
-struct io_has_gf<IO, std::void_t<decltype(std::declval<const IO&>().gf + 0)>> : std::true_type {};
+struct io_wall_blend<IO, std::void_t<decltype(IO::kWallBlend)>> : std::bool_constant<IO::kWallBlend> {};
 
 template <bool RES, class IO, bool PLAIN = false>
 HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int n1, int n2, int n3, int n4, int gi,
@@ -314,10 +317,10 @@ HF_HD inline void predict_core(const StepParams& P, IO& io, u64 CT, u64 TT, int 
     if (f.dy2) dYY = (io.dyU(kk) + io.dyD(kk)) * 0.5;
     real SL = n1 ? io.SL(kk) : s, SR = n2 ? io.SR(kk) : s;
     real SU = n3 ? io.SU(kk) : s, SD = n4 ? io.SD(kk) : s;
-    if constexpr (io_has_gf<IO>::value) {
+    if constexpr (io_wall_blend<IO>::value) {
       // Config::WallBlendCells: the tangential momentum's blend leaves out
       // the wall-normal neighbours near a no-slip wall
-      if (!PLAIN && P.wall_blend) {
+      if (!PLAIN && __builtin_expect(P.wall_blend != 0, 0)) {
         const real f = P.wall_blend_f;
         if (k == I_RHOU && (io.gf & GF_WBY)) {
           SU = s + f * (SU - s);
@@ -390,6 +393,7 @@ HF_HD constexpr bool sk_live(int mode, int k) {
 template <int MODE = SK_GENERIC>
 struct SoAPredictIO {
   static constexpr int NE = MODE == SK_SGL ? 4 : NEQ;
+  static constexpr bool kWallBlend = true;
   static constexpr bool skip(int k) { return !sk_live(MODE, k); }
   HF_HD static constexpr int eq(int k) { return k; }
   const SoA& in;

@@ -88,7 +88,7 @@ __device__ __forceinline__ void mix_e_cv(const double* c, double rho, double Tin
     se += c[s] * (T * (hRT - 1.0));
     scv += c[s] * (cpR - 1.0);
   }
-  if (Tin < TLO) se += scv * (Tin - TLO);
+  se += scv * (Tin - T);   // (+0 for Tin >= TLO)
   *e = se * RU / rho;
   *cv = scv * RU / rho;
 }

@@ -59,7 +59,7 @@ __device__ void cell_e_cv(const ChemMechDev& m, const double* c, double rho, dou
     se += c[s] * (T * (hRT - 1.0));
     scv += c[s] * (cpR - 1.0);
   }
-  if (Tin < MECH_TLO) se += scv * (Tin - MECH_TLO);
+  se += scv * (Tin - T);   // (+0 for Tin >= MECH_TLO)
   *e = se * MECH_RU / rho;
   *cv = scv * MECH_RU / rho;
 }

@@ -84,7 +84,7 @@ __host__ inline void dt_set_host(DevScalars& s, int slot, unsigned long long b) 
 
 // dt of the step reading the slot
 __device__ inline double dt_cur(const StepParams& P, const DevScalars* sc, int slot) {
-  return P.lag_dt ? bits_to_d(sc->dt_lag[slot]) : dt_get(sc, slot);
+  return __builtin_expect(P.lag_dt != 0, 0) ? bits_to_d(sc->dt_lag[slot]) : dt_get(sc, slot);
 }
 // first kernel of a lagged step, one thread, before the slot's word is
 // overwritten with this step's dt: the previous step's MIN goes to the next

@@ -443,7 +443,8 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
 // flag seq_prev + 1), waits (bounded) for every peer's flag of the same step
 // -- the two neighbours' only with X.defer -- and folds their dt into the
 // slot the next step reads.
-__device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
+// Returns true (every lane) in the last workgroup, after the wait.
+__device__ __forceinline__ bool fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
                                         unsigned long long seq_prev, bool fold = true) {
   const int lane = (int)(threadIdx.x & (WAVE - 1));
   // the workgroup barrier drained every wave's mailbox stores; drain lane
@@ -466,7 +467,7 @@ __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slo
       }
     }
   }
-  if (!__shfl(last, 0, WAVE)) return;
+  if (!__shfl(last, 0, WAVE)) return false;
   // last workgroup: this rank's dt (word + shards, one per lane), published
   // to every peer (one peer per lane), then the flags, then the peers'
   const unsigned long long sn = seq_prev + 1;
@@ -492,7 +493,9 @@ __device__ __forceinline__ void fx_tail(const FusedX& X, DevScalars* sc, int slo
       __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *X.seq = sn;
   }
+  return true;
 }
+
 
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
 // In-kernel phase trace (TR): thread 0 of every workgroup records the
@@ -999,6 +1002,9 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     if (serial) m = fmin(m, P.dt);
     dt_min(sc, slot_next, m);
   }
+  // (unpacking the peers' halo in this last workgroup instead of a separate
+  // hf2d_p2p_unpack launch measured 2x the exchange cost: one workgroup's
+  // serial rounds of uncached mailbox loads, profiles/exchange_loopback_r05.md)
   if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
 }
 
@@ -2348,6 +2354,7 @@ void DeviceSolver::upload() {
     u64 models = 0;
     if (sk_mode != SK_SGL && sk_mode != SK_SGT) no("not single-gas N-S");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
+    else if (cs.cfg.WallBlendCells > 0) no("WallBlendCells (split path only)");
     else if ((gi0 > 0 && l_off < 2) || (gi1 < cs.J.nx && h.nx - l_off - (gi1 - gi0) < 2)) no("one ghost column");
     else if (sk_mode == SK_SGT && cs.cfg.ViscousCFL > 0) no("viscous CFL with eddy viscosity");
     else
@@ -2400,6 +2407,7 @@ void DeviceSolver::upload() {
     else if (cs.cfg.ProblemType != SM_NS) no("not Navier-Stokes");
     else if (m.nsp > LNM_NSB || m.nsp < 2) no("species count outside the kernel's block");
     else if (!cs.cfg.isAdiabaticWall) no("wall heat transfer");
+    else if (cs.cfg.WallBlendCells > 0) no("WallBlendCells (split path only)");
     else if ((gi0 > 0 && l_off < 2) || (gi1 < cs.J.nx && h.nx - l_off - (gi1 - gi0) < 2)) no("one ghost column");
     else if (cs.cfg.ViscousCFL > 0) no("viscous CFL");
     else if (h.ny < LNM_TILE) no("grid lower than one tile");
@@ -4267,7 +4275,10 @@ std::string DeviceSolver::autotune(int steps) {
   // heuristic height, 87 us at 16 rows)
   const bool ns = cs.cfg.ProblemType == SM_NS;
   if (nstep != 0 || iter != 0) return "";
-  if (ns ? !(lean_ns && lns_ok) : !(lean_ok && lean_tile)) return "";
+  // mechanism mode: the lean mechanism tile's width (16 x 16: the ring is a
+  // second fill on one wavefront; 12 x 16: one fill per thread)
+  const bool mech = ns && lean_mech && lnm_ok && cs.cfg.mech_mode();
+  if (ns ? !((lean_ns && lns_ok) || mech) : !(lean_ok && lean_tile)) return "";
   flush_pending();
   const real s_dt = dt, s_dtr = dt_running, s_cur = cur_time_part, s_gt = cs.global_time, s_lag = dt_lag;
   const long s_iter = iter, s_last = last_iter;
@@ -4281,9 +4292,12 @@ std::string DeviceSolver::autotune(int steps) {
   std::vector<Cand> cands;
   for (int cpt : {2, 1}) {
     if (ns && cpt == 2) continue;
+    if (mech) break;
     for (int tj : {0, 10, 12, 14, 16, 20, 25, 32, 40, 50, 64})
       if ((tj == 0 || tj <= h.ny) && (ns ? tj <= 40 : (tj == 0 || tj >= 16))) cands.push_back({cpt, tj, BLOCK});
   }
+  if (mech)   // (Cand::tj carries the tile width here)
+    for (int ti : {LNM_TILE, 12}) cands.push_back({1, ti, BLOCK});
   // small workgroups (single-gas inviscid): the geometries of the narrow
   // strips of a multi-GPU run, where 256-thread tiles leave CUs idle
   if (!ns && lean_sg && lean_sg_ok)
@@ -4292,7 +4306,7 @@ std::string DeviceSolver::autotune(int steps) {
         for (int tj : {0, 8, 16, 32, 64})
           if (tj <= nt && (tj == 0 || tj <= h.ny)) cands.push_back({cpt, tj, nt});
   double best = 1e30;
-  Cand win{lean_cpt, lean_tj, lean_nt, lean_wgcu};
+  Cand win = mech ? Cand{1, lnm_ti, BLOCK} : Cand{lean_cpt, lean_tj, lean_nt, lean_wgcu};
   char b[160];
   std::string log;
   // same work per candidate whatever the grid (~50 M cell-steps): big grids get fewer steps
@@ -4305,10 +4319,14 @@ std::string DeviceSolver::autotune(int steps) {
   bool stage2 = ns;
   for (size_t ci = 0; ci < cands.size(); ci++) {
     const Cand c = cands[ci];
-    lean_cpt = c.cpt;
-    lean_tj = c.tj;
-    lean_nt = c.nt;
-    lean_wgcu = c.wgcu;
+    if (mech) {
+      lnm_ti = c.tj;
+    } else {
+      lean_cpt = c.cpt;
+      lean_tj = c.tj;
+      lean_nt = c.nt;
+      lean_wgcu = c.wgcu;
+    }
     graph.reset();   // the state just keeps marching; it is restored once at the end
     double us = 1e30;
     try {
@@ -4324,7 +4342,9 @@ std::string DeviceSolver::autotune(int steps) {
       log += std::string("stopped: ") + e.what() + "; ";
       break;
     }
-    if (c.wgcu)
+    if (mech)
+      std::snprintf(b, sizeof b, "lnm ti=%d %.2f us; ", c.tj, us);
+    else if (c.wgcu)
       std::snprintf(b, sizeof b, "wgcu=%d %.2f us; ", c.wgcu, us);
     else if (c.nt == BLOCK)
       std::snprintf(b, sizeof b, "cpt=%d tj=%d %.2f us; ", c.cpt, c.tj, us);
@@ -4345,10 +4365,14 @@ std::string DeviceSolver::autotune(int steps) {
       }
     }
   }
-  lean_cpt = win.cpt;
-  lean_tj = win.tj;
-  lean_nt = win.nt;
-  lean_wgcu = win.wgcu;
+  if (mech) {
+    lnm_ti = win.tj;
+  } else {
+    lean_cpt = win.cpt;
+    lean_tj = win.tj;
+    lean_nt = win.nt;
+    lean_wgcu = win.wgcu;
+  }
   // step graphs on or off for the winning geometry: replaying the 6-step
   // graph costs ~1 us per step more than eager launches on the 2000 x 200
   // headline grid (28.5 vs 27.5 us/step over 20-step calls, 1x MI355X,
@@ -4393,8 +4417,11 @@ std::string DeviceSolver::autotune(int steps) {
   upload();   // device scalars from the restored host state
   graph_launches = 0;
   lns_steps = lnm_steps = 0;   // (the tuning steps do not count as the run's)
-  std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d wgcu=%d graphs=%d (%.2f us/step)", win.nt, win.cpt, win.tj,
-                win.wgcu, (int)use_graph, best);
+  if (mech)
+    std::snprintf(b, sizeof b, "best lnm ti=%d graphs=%d (%.2f us/step)", win.tj, (int)use_graph, best);
+  else
+    std::snprintf(b, sizeof b, "best nt=%d cpt=%d tj=%d wgcu=%d graphs=%d (%.2f us/step)", win.nt, win.cpt, win.tj,
+                  win.wgcu, (int)use_graph, best);
   return log + b;
 }
 

@@ -124,9 +124,24 @@ def plate_cf(sim, x_le_frac: float) -> Dict[str, np.ndarray]:
         jt = int(top[0]) + 1 if len(top) else ny - 1
         theta[q] = float(np.sum(ru[:jt + 1]) * dy)
     re_theta = rhoe * Ue * theta / mue
-    return {"x": x, "Re_x": rex, "Cf": cf, "Cf_eff": cf_eff, "Cf_lam": lam, "Cf_turb": turb,
+    # the DEEPS blend's own diffusion across the first cell off the wall,
+    # (1 - beta) dyy/2 dy^2/dt with the rho U blending factor there, against
+    # the molecular nu_w: the near-wall error driver of the molecular Cf
+    beta1 = np.asarray(sim.field("beta1"))
+    dyy = dx / (dx + dy)
+    d_num = (1.0 - beta1[i, 1]) * dyy * 0.5 * dy * dy / sim.summary()["dt"]
+    blend_nu = d_num / (mu[i, 0] / rho[i, 0])
+    return {"x": x, "Re_x": rex, "Cf": cf, "Cf_eff": cf_eff, "Cf_lam": lam, "Cf_turb": turb, "blend_nu": blend_nu,
             "Cf_turb_vd2": van_driest_ii(rex, Me, Te, Tw), "theta": theta, "Re_theta": re_theta,
             "Cf_vd2_theta": van_driest_ii_theta(re_theta, Me, Te, Tw), "Mach": np.full_like(x, Me), "Tw": Tw}
+
+
+def extrapolate_to_zero(xs, ys):
+    """Value at x = 0 of the polynomial (degree len - 1, at most 2) through
+    the points (x, y): the zero-blend-diffusion limit of a grid sequence."""
+    xs = np.asarray(xs, dtype=np.float64)
+    ys = np.asarray(ys, dtype=np.float64)
+    return float(np.polyval(np.polyfit(xs, ys, min(len(xs) - 1, 2)), 0.0))
 
 
 def langley_phi(mc: float) -> float:
