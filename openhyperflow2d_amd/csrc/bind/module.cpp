@@ -552,6 +552,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("download", [](SolverBase& s) { s.download(s.cs.J); })
       .def("upload", &SolverBase::upload)
       .def("sync", &SolverBase::sync_scalars)
+      .def("poison_cell", &SolverBase::poison_cell, py::arg("gi"), py::arg("j"),
+           "test hook: a negative energy in cell (gi, j) (the next step reports Tg < 0)")
       .def("summary", &summary_dict)
       .def_readwrite("dt", &SolverBase::dt)
       .def_readonly("iter", &SolverBase::iter)
@@ -748,6 +750,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("chem_compact", &DeviceSolver::chem_compact)
       .def_readwrite("comm_overlap", &DeviceSolver::comm_overlap)
       .def_readwrite("lnm_overlap", &DeviceSolver::lnm_overlap)
+      .def_readwrite("host_tail", &DeviceSolver::host_tail)
       .def_readwrite("lean_ns", &DeviceSolver::lean_ns)
       .def_readwrite("lns_occ", &DeviceSolver::lns_occ)
       .def_readonly("lns_ok", &DeviceSolver::lns_ok)

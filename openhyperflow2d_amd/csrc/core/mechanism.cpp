@@ -136,7 +136,6 @@ std::shared_ptr<MechInfo> parse_mechanism(const std::string& text) {
       m.a[s][0][k] = v[4 + k];
       m.a[s][1][k] = v[11 + k];
     }
-    m.cplo[s] = nasa_cp(mech_coef(m, s, MECH_TLO), MECH_TLO);
     const auto l = lj.count(info->species[s]) ? lj[info->species[s]] : std::make_pair(3.5, 100.0);
     for (int t = 0; t < MECH_NT; t++) {
       const double T = MECH_TT0 + MECH_TDT * t;

@@ -70,7 +70,6 @@ struct MechData {
   real Rs[MECH_MAXSP] = {};        // RU / W
   real Tmid[MECH_MAXSP] = {};
   real a[MECH_MAXSP][2][7] = {};   // NASA-7 [low, high]
-  real cplo[MECH_MAXSP] = {};      // cp/R at MECH_TLO (the constant cp below it)
   real mu_tab[MECH_MAXSP][MECH_NT] = {};
   real lam_tab[MECH_MAXSP][MECH_NT] = {};
   real slot[4][MECH_MAXSP] = {};   // reference (fuel, ox, cp, air) -> species mass fractions
@@ -202,8 +201,9 @@ HF_HD inline real mech_h_species(const MechData& m, int s, real T) {
   const real Te = T < MECH_TLO ? MECH_TLO : T;
   const Nasa7 c = mech_coef_v(m, s, Te);
   // constant cp below TLO, branch-free (+0 above it): a branch here made the
-  // lean mechanism tile kernel 7 % slower
-  return m.Rs[s] * (nasa_hT(c.a, Te) + m.cplo[s] * (T - Te));
+  // lean mechanism tile kernel 7 % slower; cp(TLO) from the coefficients in
+  // registers (a per-species table load cost the tile kernel 2 VGPR spills)
+  return m.Rs[s] * (nasa_hT(c.a, Te) + nasa_cp(c.a, Te) * (T - Te));
 }
 
 // ---------------------------------------------------------------------------

@@ -137,6 +137,11 @@ struct StepParams {
   int lag_dt = 0;
   int wall_blend = 0;   // Config::WallBlendCells > 0: predictor accessors' gf carries GF_WBX / GF_WBY
   real wall_blend_f = 0;   // Config::WallBlendFactor
+  // device solver, single GPU: the last step of a host call publishes its
+  // scalars (dt, error flag, time) into the pinned host mirror itself
+  // (hip/device_solver.hip host_tail; nullptr: hf2d_scalars_out does it)
+  void* host_sc = nullptr;
+  unsigned* host_done = nullptr;
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

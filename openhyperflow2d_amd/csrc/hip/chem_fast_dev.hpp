@@ -264,22 +264,26 @@ __device__ void chem_cell(double rho, double e, double* y, double* Tio, double d
     const double lnT = log(T), invT = 1.0 / T;
     const double lnP0RT = log(PATM / (RU * T));
     double g[NS];
+    {
+      // below TLO the constant-cp extrapolation of mechanism.hpp mech_gibbs,
+      // branch-free: at Te = max(T, TLO) the polynomial terms, then with
+      // r = Te / T and dl = lnT - lnTe
+      //   g = hRT(Te) r + cp/R (1 - r) - s/R(Te) - cp/R dl,
+      // which for T >= TLO (r = 1, dl = 0; no contraction) is hRT - s/R bit
+      // for bit.  (A branch to a separate low-T loop cost this kernel 50
+      // registers and 18 % of its time.)
+      const bool lo = T < TLO;
+      const double Te = lo ? TLO : T, lnTe = lo ? log(TLO) : lnT;
+      const double r = lo ? TLO * invT : 1.0, dl = lnT - lnTe;
 #pragma unroll
-    for (int s = 0; s < NS; s++) {
-      if (T < TLO) {   // constant-cp extrapolation (mechanism.hpp mech_gibbs)
-        const double Te = TLO, lnTe = log(TLO);
+      for (int s = 0; s < NS; s++) {
         const double* a = coef<M>(s, Te);
-        const double cpR = a[0] + Te * (a[1] + Te * (a[2] + Te * (a[3] + Te * a[4])));
-        const double hT = Te * (a[0] + Te * (a[1] * 0.5 + Te * (a[2] * (1.0 / 3.0) + Te * (a[3] * 0.25 + Te * a[4] * 0.2)))) + a[5];
+        const double hRT = a[0] + Te * (a[1] * 0.5 + Te * (a[2] * (1.0 / 3.0) + Te * (a[3] * 0.25 + Te * a[4] * 0.2))) +
+                           a[5] / Te;
         const double sR = a[0] * lnTe + Te * (a[1] + Te * (a[2] * 0.5 + Te * (a[3] * (1.0 / 3.0) + Te * a[4] * 0.25))) + a[6];
-        g[s] = (hT + cpR * (T - Te)) / T - (sR + cpR * (lnT - lnTe));
-        continue;
+        const double cpR = a[0] + Te * (a[1] + Te * (a[2] + Te * (a[3] + Te * a[4])));
+        g[s] = hRT * r + cpR * (1.0 - r) - sR - cpR * dl;
       }
-      const double* a = coef<M>(s, T);
-      const double hRT = a[0] + T * (a[1] * 0.5 + T * (a[2] * (1.0 / 3.0) + T * (a[3] * 0.25 + T * a[4] * 0.2))) +
-                         a[5] / T;
-      const double sR = a[0] * lnT + T * (a[1] + T * (a[2] * 0.5 + T * (a[3] * (1.0 / 3.0) + T * a[4] * 0.25))) + a[6];
-      g[s] = hRT - sR;
     }
     double A[NS][NS + 1];
 #pragma unroll

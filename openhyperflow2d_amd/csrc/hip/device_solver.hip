@@ -497,6 +497,45 @@ __device__ __forceinline__ bool fx_tail(const FusedX& X, DevScalars* sc, int slo
 }
 
 
+// Single-GPU last step of a host call (StepParams::host_sc): the last
+// workgroup to finish copies the slot's dt (word + shards) and the error flag
+// into the pinned host mirror (workgroup 0's head wrote time_part / dt_lag
+// there), so DeviceSolver::sync_scalars only waits for the stream: no
+// hf2d_scalars_out launch and its completion round trip (13 us of an idle
+// step(0) call, tools/call_overhead.py).  Completion count as fx_tail.
+__device__ __forceinline__ void host_mirror_tail(const StepParams& P, DevScalars* sc, int slot_next) {
+  const int lane = (int)(threadIdx.x & (WAVE - 1));
+  vm_drain();   // lane 0's dt atomic
+  int last = 0;
+  if (lane == 0) {
+    const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
+    const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
+    unsigned* cs = P.host_done + sh * FX_DONE_STRIDE;
+    unsigned* ct = P.host_done + DT_SHARDS * FX_DONE_STRIDE;
+    if (__hip_atomic_fetch_add(cs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pop - 1) {
+      __hip_atomic_store(cs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+        __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
+      }
+    }
+  }
+  if (!__shfl(last, 0, WAVE)) return;
+  DevScalars* h = static_cast<DevScalars*>(P.host_sc);
+  if (lane < DT_SHARDS)
+    h->dt_sh[slot_next][lane][0] =
+        __hip_atomic_load(&sc->dt_sh[slot_next][lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == DT_SHARDS)
+    h->dt_bits[slot_next] = __hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == DT_SHARDS + 1) h->neg_T = __hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// (workgroup 0's head, thread 0, after its updates of the slot words)
+__device__ __forceinline__ void host_mirror_head(const StepParams& P, const DevScalars* sc, int slot_next) {
+  DevScalars* h = static_cast<DevScalars*>(P.host_sc);
+  h->time_part = sc->time_part;
+  h->dt_lag[slot_next] = sc->dt_lag[slot_next];
+}
+
 // LDS-tiled lean step (lean_euler.hpp: lean_tile_stage / TileIO).
 // In-kernel phase trace (TR): thread 0 of every workgroup records the
 // 100 MHz s_memrealtime clock at entry, after the LDS staging barrier, when
@@ -570,6 +609,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       sc->dt_bits[slot] = d_to_bits(P.dt);   // folded (later kernels of the step read the word)
       sc->time_part += P.dt;
       scenario_next(P, sc, slot, slot_next);
+      if (OUT && !RES && !FX && P.host_sc) host_mirror_head(P, sc, slot_next);
     }
   }
   int i[CPT], j[CPT], c[CPT], i0, j0;
@@ -663,7 +703,10 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   for (int off = 1; off < WAVE; off <<= 1) dtl = fmin(dtl, __shfl_xor(dtl, off, WAVE));
   __shared__ double sdt[NT / WAVE];
   if ((threadIdx.x & (WAVE - 1)) == 0) sdt[threadIdx.x / WAVE] = dtl;
-  if (neg) atomicOr(&sc->neg_T, 1);
+  if (neg) {
+    atomicOr(&sc->neg_T, 1);
+    if (OUT && !RES && !FX && P.host_sc) vm_drain();   // (done before host_mirror_tail's count)
+  }
   __syncthreads();
   if (TR) tr[3] = rt_clock();
   if (threadIdx.x == 0) {
@@ -683,6 +726,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     }
   }
   if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev);
+  if (OUT && !RES && !FX && !TR && P.host_sc && threadIdx.x < WAVE) host_mirror_tail(P, sc, slot_next);
 }
 
 // No occupancy attribute on the default kernel: the backend's own register
@@ -1883,6 +1927,11 @@ struct DeviceSolver::Impl {
   DevScalars* sc = nullptr;
   DevScalars* sc_host = nullptr;   // pinned
   bool sc_kernel = true;           // sync_scalars: hf2d_scalars_out instead of a copy (HF2D_SC_KERNEL=0: copy)
+  // single GPU: the last (output) lean tile step of a host call wrote the
+  // scalars into sc_host itself (DeviceSolver::host_tail); sync_scalars then
+  // only waits
+  bool sc_mirrored = false;
+  unsigned* host_done = nullptr;   // host_tail's completion counters
   ResidualPack* partials = nullptr;
   ResidualPack* res_out = nullptr;
   ResidualPack* res_host = nullptr;   // pinned
@@ -2155,6 +2204,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
   if (const char* e = std::getenv("HF2D_STAGGER")) tile_stagger = std::atoi(e);
   if (const char* e = std::getenv("HF2D_SC_KERNEL")) impl->sc_kernel = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_HOST_TAIL")) host_tail = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
@@ -2227,6 +2277,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   m.scen = m.mem.alloc<ScenarioTables>(1);
   m.sc = m.mem.alloc<DevScalars>(1);
   HIP_CHECK(hipHostMalloc((void**)&m.sc_host, sizeof(DevScalars), hipHostMallocDefault));
+  m.host_done = m.mem.alloc<unsigned>((DT_SHARDS + 1) * FX_DONE_STRIDE);
   {
     // any tile shape (lean_tj) covers >= LEAN_TILE_MIN_TJ cells per workgroup
     const long nb_tile = (long)(gi1 - gi0 + 1) * ((h.ny + LEAN_TILE_MIN_TJ - 1) / LEAN_TILE_MIN_TJ);
@@ -2501,6 +2552,7 @@ void DeviceSolver::upload() {
   last_dev_time = 0.0;
   *m.sc_host = s0;
   cp(m.sc, m.sc_host, sizeof(DevScalars));
+  m.sc_mirrored = false;
   HIP_CHECK(hipStreamSynchronize(st));
   nstep = 0;
   abuf = 0;
@@ -2714,7 +2766,9 @@ void DeviceSolver::sync_scalars() {
   flush_pending();
   p2p_complete();
   Impl& m = *impl;
-  if (m.sc_kernel) {
+  if (m.sc_mirrored) {
+    // the last step wrote the mirror (host_tail)
+  } else if (m.sc_kernel) {
     hipLaunchKernelGGL(hf2d_scalars_out, dim3(1), dim3(WAVE), 0, m.stream, m.sc, m.sc_host, (int)(nstep % 3));
     HIP_CHECK(hipGetLastError());
   } else {
@@ -3508,6 +3562,7 @@ StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
 
 void DeviceSolver::run_graph() {
   Impl& m = *impl;
+  m.sc_mirrored = false;
   const uint64_t mode = mode_signature();
   const uint64_t sig = graph_signature(pending[0], mode);
   bool same = true;
@@ -3853,6 +3908,7 @@ bool DeviceSolver::lns_step_ok(const StepParams& P) const {
 
 StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   Impl& m = *impl;
+  m.sc_mirrored = false;
   StepParams P = P0;
   P.nx = h.nx;
   P.ny = h.ny;
@@ -3967,15 +4023,25 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     else if (fx_step)
       hipLaunchKernelGGL(nt == BLOCK ? kTileFx[sg][cpt - 1][var] : kTileFxNt[nts][cpt - 1][var], dim3(ntile),
                          dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials, X);
-    else if (nt != BLOCK)
-      hipLaunchKernelGGL(kTileNt[nts][cpt - 1][var], dim3(ntile), dim3(nt), shmem, st, P, L, T, m.sc, slot,
-                         slot_next, serial, m.partials, 0);
-    else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace)
+    else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace && nt == BLOCK)
       hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                          m.sc, slot, slot_next, serial, m.partials);
-    else
-      hipLaunchKernelGGL(kTile[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
-                         slot_next, serial, m.partials, 0);
+    else {
+      // single GPU, last step of the host call: the scalars go to the host
+      // mirror from the kernel's own tail (host_tail)
+      const bool mirror = var == 1 && !tile_trace && host_tail && m.nranks == 1 && !m.local && !m.p2p.on;
+      if (mirror) {
+        P.host_sc = m.sc_host;
+        P.host_done = m.host_done;
+      }
+      if (nt != BLOCK)
+        hipLaunchKernelGGL(kTileNt[nts][cpt - 1][var], dim3(ntile), dim3(nt), shmem, st, P, L, T, m.sc, slot,
+                           slot_next, serial, m.partials, 0);
+      else
+        hipLaunchKernelGGL(kTile[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
+                           slot_next, serial, m.partials, 0);
+      m.sc_mirrored = mirror;
+    }
     HIP_CHECK(hipGetLastError());
     nres = ntile;
     nres_waves = nt / WAVE;

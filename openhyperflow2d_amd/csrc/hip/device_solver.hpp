@@ -117,6 +117,10 @@ class DeviceSolver : public SolverBase {
   // RCCL / in-process transports: halo of the edge tiles on a comm stream while
   // the interior tiles compute, then the dt MIN (lean tile steps)
   bool comm_overlap = true;
+  // single GPU: the last lean tile step of a host call writes dt / time /
+  // the error flag into the pinned host mirror from its own tail, instead of
+  // a separate read-back kernel after it (HF2D_HOST_TAIL=0: off)
+  bool host_tail = true;
   bool lnm_overlap = false;   // mechanism step: edge tiles first, halo overlapped with the interior (opt-in)
   bool lns_split = false;   // this lean N-S step ran edge-first with its halo overlapped
   bool lnm_split = false;   // this lean mechanism step ran edge-first with its halo overlapped

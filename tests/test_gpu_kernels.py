@@ -116,6 +116,31 @@ def test_small_workgroup_tiles_bitwise(gpu, nt, cpt, tj):
         np.testing.assert_array_equal(s.field(f), ref.field(f), err_msg=f)
 
 
+@pytest.mark.parametrize("nt", [256, 128])
+def test_host_tail_scalars_equal_the_read_back_kernel(gpu, nt):
+    """Single GPU: the last lean tile step of a host call writes dt, time and
+    the error flag into the pinned host mirror from its own tail
+    (DeviceSolver.host_tail) -- the same values, call for call, as the
+    separate read-back kernel; a Tg < 0 in that last step is still reported."""
+    text = decks.wedge15(300, 64, nmax=10 ** 6, nout=10 ** 5)
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    for s in (a, b):
+        s.solver.lean_nt, s.solver.lean_cpt, s.solver.lean_tj = nt, 1, 0
+    b.solver.host_tail = False
+    assert a.solver.host_tail
+    for n, res in [(1, False), (2, False), (7, False), (1, True), (20, False), (3, True), (5, False)]:
+        a.step(n, residual=res)
+        b.step(n, residual=res)
+        sa, sb = a.summary(), b.summary()
+        assert sa["dt"] == sb["dt"] and sa["time"] == sb["time"], (n, res)
+    for f in FIELDS:
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
+    a.solver.poison_cell(150, 30)
+    with pytest.raises(RuntimeError, match="Tg < 0"):
+        a.step(1)
+
+
 def test_lean_bitwise_with_switches(gpu):
     """Lean GPU steps interleaved with downloads and generic steps stay
     bit-identical to the generic CPU stepper (dt, residuals, fields)."""
