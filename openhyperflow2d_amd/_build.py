@@ -78,6 +78,11 @@ def _ninja_file() -> str:
         "  deps = gcc",
         "rule link_gxx_asan",
         "  command = g++ -fsanitize=address,undefined $in -o $out",
+        # FP32 build option of the CPU CLI (the reference's FP_OPTS = -DFP=float)
+        "rule gxx_fp32",
+        "  command = g++ -O2 -std=c++17 -fPIC -DHF2D_FP32 -I" + CSRC + " -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
     ]
     lines.append("rule embed")
     lines.append(f"  command = $python {os.path.abspath(__file__)} --embed $out $in")
@@ -110,8 +115,24 @@ def _ninja_file() -> str:
         lines.append(f"build {o}: gxx_asan {os.path.join(CSRC, 'core', s)}")
         aobjs.append(o)
     lines.append(f"build {asan_path()}: link_gxx_asan {' '.join(aobjs)}")
+    fobjs = []
+    for s in CORE_SRCS + ["hf2d_main.cpp"]:
+        o = f"fp32_{s[:-4]}.o"
+        lines.append(f"build {o}: gxx_fp32 {os.path.join(CSRC, 'core', s)}")
+        fobjs.append(o)
+    lines.append(f"build {fp32_path()}: link_gxx {' '.join(fobjs)}")
     lines.append(f"default {ext_path()} {os.path.join(HERE, 'bin', 'hf2d')} {os.path.join(HERE, 'bin', 'hf2d_cpu')}")
     return "\n".join(lines) + "\n"
+
+
+def fp32_path() -> str:
+    return os.path.join(HERE, "bin", "hf2d_cpu_fp32")
+
+
+def build_fp32(verbose: bool = False) -> str:
+    """FP32 build of the CPU CLI (real = float; not part of the default build)."""
+    build(verbose=verbose, targets=[fp32_path()])
+    return fp32_path()
 
 
 def asan_path() -> str:

@@ -39,23 +39,25 @@ struct GasSource {
 
 enum class Semantics { MPI = 0, SERIAL = 1 };
 
+// (scalars in double in every build: the FP32 build keeps the deck's geometry
+// and parameters in double and rounds only the flow state)
 struct Config {
   // files
   std::string project, out_file, err_file, swap_file, tecplot_file;
   // globals
   int isVerboseOutput = 0, bff = 0;
   int MaxX = 0, MaxY = 0;
-  real dx = 0, dy = 0;
-  real SigW = 0, SigF = 0, delta_bl = 0;
+  double dx = 0, dy = 0;
+  double SigW = 0, SigF = 0, delta_bl = 0;
   int TurbMod = 0, TurbStartIter = 0, TurbExtModel = 0, isTurbulenceReset = 0;
   int FT = FT_FLAT, ProblemType = SM_EULER;
-  real CFL = 0;
+  double CFL = 0;
   // new key (not in the reference): viscous time-step bound for N-S,
   // dt <= ViscousCFL * rho / ((mu + mu_t) (1/dx^2 + 1/dy^2)); 0 = off (reference)
-  real ViscousCFL = 0;
+  double ViscousCFL = 0;
   // new key: k-omega SST wall omega = 60 nu / (beta1 d1^2) with d1 = SSTWallDistance *
   // min(dx, dy): 1.0 (default) is Menter's distance of the first cell off the wall node
-  real SSTWallDistance = 1.0;
+  double SSTWallDistance = 1.0;
   // new key: lagged time step.  0 (default, the reference):
   // step n+1 uses dt = MIN over every rank's cells of the local dt of step n.
   // 1: step n+1 uses the MIN of step n-1, so a strip only waits for its two
@@ -72,28 +74,28 @@ struct Config {
   // ... keeping this fraction of the wall-normal neighbours' weight (0: none;
   // removing it altogether leaves the wide-stencil viscous term without
   // odd-even damping: the SST plate went unstable within 2000 steps)
-  real WallBlendFactor = 0.0;
+  double WallBlendFactor = 0.0;
   // UG item 162 (CUDA in the reference): 0 = auto-calibrate the kernel
   // geometry on the device (DeviceSolver::autotune), > 0 = fixed heuristic
   int ThreadBlockSize = 0;
   Table CFL_Scenario, beta_Scenario;
   int NSaveStep = 1, Nmax = 1, NOutStep = 1;
   int isAlternateRMS = 0, isIgnoreUnsetNodes = 0, MonitorIndex = 0;
-  real ExitMonitorValue = 0;
+  double ExitMonitorValue = 0;
   std::vector<MonitorPoint> monitors;
-  real beta0 = 0, nrbc_beta0 = 0;
+  double beta0 = 0, nrbc_beta0 = 0;
   SpeciesProps species;
   int isAdiabaticWall = 1;
-  real Hu[NSPEC] = {0, 0, 0, 0};
+  double Hu[NSPEC] = {0, 0, 0, 0};
   // pre-processor
-  real Ts0 = 0;
+  double Ts0 = 0;
   int isOutHeatFluxX = 0, Cp_Flow_index = 0, y_max = 0, y_min = 0, isOutHeatFluxY = 0;
   int is_p_asterisk_out = 0;
   int is_Cx_calc = 0, Cx_Flow_index = 0;
-  real x0_body = 0, y0_body = 0, dx_body = 0, dy_body = 0;
+  double x0_body = 0, y0_body = 0, dx_body = 0, dy_body = 0;
   int is_Cd_calc = 0, Cd_Flow_index = 0;
-  real x0_nozzle = 0, y0_nozzle = 0, dy_nozzle = 0, p_ambient = 0;
-  real InitTime = 0;
+  double x0_nozzle = 0, y0_nozzle = 0, dy_nozzle = 0, p_ambient = 0;
+  double InitTime = 0;
   std::vector<XCut> xcuts;
   std::vector<GasSource> sources;
   // runtime options (not in decks; defaults reproduce the reference MPI build)
@@ -106,7 +108,7 @@ struct Config {
   std::string mechanism;
   std::shared_ptr<MechInfo> mech;
   int chem_nsub = 1;
-  real chem_tmin = 300.0;
+  double chem_tmin = 300.0;
   bool mech_mode() const { return chem_model == CRM_ARRENIUS && mech != nullptr; }
   int mech_ns() const { return mech ? mech->data.ns : 0; }
 

@@ -21,7 +21,11 @@
 
 namespace hf2d {
 
-using real = double;
+#ifdef HF2D_FP32
+using real = float;   // FP32 build option (host CLI hf2d_cpu_fp32; the reference's -DFP=float)
+#else
+using real = double;   // FP64 default (the reference's FP_OPTS = -DFP=double, gcc.compiler:22)
+#endif
 using u64 = std::uint64_t;
 
 
@@ -196,6 +200,10 @@ struct CellRecord {
   HF_HD bool is_turb(u64 mask) const { return (TurbType & mask) == mask; }
 };
 
+// (FP64: the reference's 1248-byte record; the FP32 build writes the float
+// layout of the reference's -DFP=float build, whose checkpoints are not
+// interchangeable with FP64 ones either)
+#ifndef HF2D_FP32
 static_assert(sizeof(CellRecord) == 1248, "CellRecord must match the 1248-byte .hf2d record");
 static_assert(offsetof(CellRecord, TurbType) == 216, "layout");
 static_assert(offsetof(CellRecord, x) == 296, "layout");
@@ -208,6 +216,7 @@ static_assert(offsetof(CellRecord, Y) == 1072, "layout");
 static_assert(offsetof(CellRecord, droYdx) == 1120, "layout");
 static_assert(offsetof(CellRecord, dUdx) == 1184, "layout");
 static_assert(offsetof(CellRecord, BGX) == 1232, "layout");
+#endif
 
 // ---------------------------------------------------------------------------
 // Correctly rounded FP64 division and square root for operands of ordinary
@@ -261,10 +270,12 @@ HF_HD inline double hf_sqrt(double x) {
 // (obj_data/obj_data.cpp:1822-1859).  Plain-old-data so it can live in device
 // constant/global memory.
 constexpr int MAX_TABLE_PTS = 64;
+// (double in every build: deck tables also carry the contour / area
+// coordinates, which the FP32 build converts to cell indices in double)
 struct TableData {
   int n = 0;
-  real x[MAX_TABLE_PTS];
-  real y[MAX_TABLE_PTS];
+  double x[MAX_TABLE_PTS];
+  double y[MAX_TABLE_PTS];
 };
 
 HF_HD inline real table_eval(const TableData& t, real xv) {

@@ -9,7 +9,7 @@
 
 namespace hf2d {
 
-real Table::eval(real xv) const {
+double Table::eval(double xv) const {
   const int n = size();
   if (n == 0) return 0.0;   // the reference's zero table
   if (n == 1) return y[0];
@@ -163,11 +163,11 @@ int InputDeck::get_int(const std::string& key) {
   return v;
 }
 
-real InputDeck::get_float(const std::string& key) {
+double InputDeck::get_float(const std::string& key) {
   Entry* e = find(key);
   if (!e) throw DeckError("Data object \"" + key + "\" not found in \"" + name_ + "\".");
   if (!float_chars_ok(e->value)) throw DeckError("Data object \"" + key + "\" have not FLOAT type.");
-  real v = std::atof(e->value.c_str());
+  double v = std::atof(e->value.c_str());
   char buf[64];
   std::snprintf(buf, sizeof buf, "%g", v);
   e->value = buf;
@@ -191,7 +191,7 @@ int InputDeck::get_int_or(const std::string& key, int def) {
   if (!e || !int_chars_ok(e->value)) return def;
   return get_int(key);
 }
-real InputDeck::get_float_or(const std::string& key, real def) {
+double InputDeck::get_float_or(const std::string& key, double def) {
   Entry* e = find(key);
   if (!e || !float_chars_ok(e->value)) return def;
   return get_float(key);

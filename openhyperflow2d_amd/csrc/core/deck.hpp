@@ -31,11 +31,11 @@ class DeckError : public std::runtime_error {
 
 struct Table {
   std::string name;
-  std::vector<real> x, y;
+  std::vector<double> x, y;
   int size() const { return (int)x.size(); }
-  real eval(real xv) const;   // reference interpolation/extrapolation rule
-  real X(int i) const { return (i >= 0 && i < size()) ? x[i] : 0.0; }
-  real Y(int i) const { return (i >= 0 && i < size()) ? y[i] : 0.0; }
+  double eval(double xv) const;   // reference interpolation/extrapolation rule
+  double X(int i) const { return (i >= 0 && i < size()) ? x[i] : 0.0; }
+  double Y(int i) const { return (i >= 0 && i < size()) ? y[i] : 0.0; }
   TableData pack() const;     // POD copy for device use (<= MAX_TABLE_PTS)
 };
 
@@ -50,13 +50,13 @@ class InputDeck {
   bool has_table(const std::string& key) const;
 
   int get_int(const std::string& key);
-  real get_float(const std::string& key);
+  double get_float(const std::string& key);
   std::string get_string(const std::string& key) const;
   const Table& get_table(const std::string& key) const;
 
   // Non-throwing variants (return def when the key is absent or malformed).
   int get_int_or(const std::string& key, int def);
-  real get_float_or(const std::string& key, real def);
+  double get_float_or(const std::string& key, double def);
   std::string get_string_or(const std::string& key, const std::string& def) const;
 
   // Overrides / programmatic construction (used by deck generators).

@@ -799,11 +799,11 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
   // ---- initial dt from the flow lists ----
   dt0 = 1;
   {
-    const real CFL_min = std::min(C.CFL, C.CFL_Scenario.eval(0));
+    const real CFL_min = std::min<real>(C.CFL, C.CFL_Scenario.eval(0));
     for (auto& f : flows)
-      dt0 = std::min(dt0, CFL_min * std::min(C.dx / (f.Asound() + f.flow_Wg()), C.dy / (f.Asound() + f.flow_Wg())));
+      dt0 = std::min<real>(dt0, CFL_min * std::min<real>(C.dx / (f.Asound() + f.flow_Wg()), C.dy / (f.Asound() + f.flow_Wg())));
     for (auto& f : flows2d)
-      dt0 = std::min(dt0, CFL_min * std::min(C.dx / (f.Asound() + f.Wg2d()), C.dy / (f.Asound() + f.Wg2d())));
+      dt0 = std::min<real>(dt0, CFL_min * std::min<real>(C.dx / (f.Asound() + f.Wg2d()), C.dy / (f.Asound() + f.Wg2d())));
   }
 
   if (!PreloadFlag) {

@@ -304,9 +304,9 @@ StepParams SolverBase::make_params(long it) const {
   P.dxx = C.dy / (C.dx + C.dy);
   const real beta_scen = C.beta_Scenario.eval((real)it);
   const real cfl_scen = C.CFL_Scenario.eval((real)it);
-  P.beta_min = std::min(C.beta0, beta_scen);
+  P.beta_min = std::min<real>(C.beta0, beta_scen);
   P.nrbc_beta0 = C.nrbc_beta0;
-  P.CFL_min = std::min(C.CFL, cfl_scen);
+  P.CFL_min = std::min<real>(C.CFL, cfl_scen);
   P.visc_cfl = C.ViscousCFL;
   P.bff = C.bff;
   P.alternate_rms = C.isAlternateRMS;
@@ -1250,7 +1250,7 @@ StepResult RefSolver::do_step(const StepParams& P, bool /*want_res*/) {
           return r;
         } else {
           const real AAA = std::sqrt(c.k * c.R * c.Tg);
-          dtmin = std::min(dtmin, P.CFL_min * std::min(C.dx / (AAA + std::fabs(c.U)), C.dy / (AAA + std::fabs(c.V))));
+          dtmin = std::min<real>(dtmin, P.CFL_min * std::min<real>(C.dx / (AAA + std::fabs(c.U)), C.dy / (AAA + std::fabs(c.V))));
           if (C.chem_model != NO_REACTIONS) chemistry_zeldovich(c, C.species, C.ProblemType, C.chem_model);
           if (C.chem_model == CRM_ARRENIUS) chemistry_arrhenius_src(c, C.species, P.dt);
         }
