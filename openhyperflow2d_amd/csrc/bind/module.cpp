@@ -135,6 +135,10 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
+  m.def(
+      "profiler_region",
+      [](bool on) { DeviceSolver::profiler_region(on); },
+      py::arg("on"), "rocprofv3 --selected-regions: collect only between profiler_region(True) and (False)");
   // hf_div / hf_sqrt evaluated on the GPU (csrc/hip/numerics.hip): (a / b, sqrt(a))
   m.def("div_probe", [](py::array_t<double, py::array::c_style | py::array::forcecast> a,
                         py::array_t<double, py::array::c_style | py::array::forcecast> b) {
@@ -764,6 +768,15 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readonly("lnm_turb", &DeviceSolver::lnm_turb)
       .def_readonly("lnm_steps", &DeviceSolver::lnm_steps)
       .def_readwrite("lnm_ti", &DeviceSolver::lnm_ti)
+      .def_readwrite("lnm_timing", &DeviceSolver::lnm_timing)
+      .def_property(
+          "lnm_phase_ms",
+          [](const DeviceSolver& s) {
+            return std::vector<double>(s.lnm_phase_ms, s.lnm_phase_ms + 4);
+          },
+          [](DeviceSolver& s, const std::vector<double>& v) {
+            for (int q = 0; q < 4; q++) s.lnm_phase_ms[q] = q < (int)v.size() ? v[q] : 0.0;
+          })
       .def("lnm_trace_fetch", &DeviceSolver::lnm_trace_fetch, py::call_guard<py::gil_scoped_release>())
       .def_readonly("overlap_steps", &DeviceSolver::overlap_steps)
       .def_readonly("lns_fx_steps", &DeviceSolver::lns_fx_steps)

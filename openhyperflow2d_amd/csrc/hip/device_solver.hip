@@ -1932,6 +1932,7 @@ struct DeviceSolver::Impl {
   // only waits
   bool sc_mirrored = false;
   unsigned* host_done = nullptr;   // host_tail's completion counters
+  hipEvent_t lnm_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // DeviceSolver::lnm_timing
   ResidualPack* partials = nullptr;
   ResidualPack* res_out = nullptr;
   ResidualPack* res_host = nullptr;   // pinned
@@ -2314,6 +2315,8 @@ DeviceSolver::~DeviceSolver() {
     if (impl->comm_stream) (void)hipStreamSynchronize(impl->comm_stream);
     if (impl->ev_edge) (void)hipEventDestroy(impl->ev_edge);
     if (impl->ev_halo) (void)hipEventDestroy(impl->ev_halo);
+    for (hipEvent_t e : impl->lnm_ev)
+      if (e) (void)hipEventDestroy(e);
     if (impl->comm_stream) (void)hipStreamDestroy(impl->comm_stream);
     if (impl->stream) (void)hipStreamDestroy(impl->stream);
   }
@@ -2761,6 +2764,14 @@ void DeviceSolver::poison_cell(int gi, int j) {
 // driver phases as roctx ranges (rocprofv3 --marker-trace)
 void DeviceSolver::trace_push(const char* name) { roctxRangePush(name); }
 void DeviceSolver::trace_pop() { roctxRangePop(); }
+// rocprofv3 --selected-regions: collection only between profiler_region(true)
+// and profiler_region(false) (bench.py --prof-region)
+void DeviceSolver::profiler_region(bool on) {
+  if (on)
+    roctxProfilerResume(0);
+  else
+    roctxProfilerPause(0);
+}
 
 void DeviceSolver::sync_scalars() {
   flush_pending();
@@ -3866,8 +3877,16 @@ void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const Lea
     (void)hipGetLastError();
     attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip] = true;
   }
+  // lnm_timing: events around the three phases (measurement only: the host
+  // waits for each step's events, so the steps serialise with the host)
+  if (lnm_timing) {
+    if (!m.lnm_ev[0])
+      for (auto& e : m.lnm_ev) HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(m.lnm_ev[0], st));
+  }
   hipLaunchKernelGGL(k, dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot, slot_next, serial, m.partials);
   HIP_CHECK(hipGetLastError());
+  if (lnm_timing) HIP_CHECK(hipEventRecord(m.lnm_ev[1], st));
   // kinetics of the listed cells (T^m >= Tchem), in place on the new species
   const MechData& md = *cs.cfg.mech->data_ptr();
   SoA mid;
@@ -3891,9 +3910,20 @@ void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const Lea
       throw std::runtime_error("hf2d_rtc_chem list launch failed");
     chem_kernel_used = "hf2d_rtc_chem";
   }
+  if (lnm_timing) HIP_CHECK(hipEventRecord(m.lnm_ev[2], st));
   const unsigned nb = (unsigned)std::min<long>((c1 - c0 + BLOCK - 1) / BLOCK, 1024);
   hipLaunchKernelGGL(hf2d_lnm_hot, dim3(nb), dim3(BLOCK), 0, st, P, a, m.sc, slot, slot_next, serial);
   HIP_CHECK(hipGetLastError());
+  if (lnm_timing) {
+    HIP_CHECK(hipEventRecord(m.lnm_ev[3], st));
+    HIP_CHECK(hipEventSynchronize(m.lnm_ev[3]));
+    for (int q = 0; q < 3; q++) {
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, m.lnm_ev[q], m.lnm_ev[q + 1]));
+      lnm_phase_ms[q] += ms;
+    }
+    lnm_phase_ms[3] += 1.0;
+  }
 }
 
 // The lean N-S kernel applies to this step (lean_ns.hpp; eligibility lns_ok)

@@ -98,6 +98,7 @@ class DeviceSolver : public SolverBase {
   // timing stand-in: rank `rank` of `nranks` with every peer ready and the
   // neighbours' mailboxes looped back into this rank's own (device_solver.hip)
   void p2p_loopback(int rank, int nranks);
+  static void profiler_region(bool on);
   bool p2p_active() const;
   bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
   bool fx_step = false, fx_pending = false;
@@ -211,6 +212,11 @@ class DeviceSolver : public SolverBase {
   int lnm_turb = 0;       // fill_node turbulence set of the kernel: 0 none, 3 SST
   long lnm_steps = 0;
   int lnm_ti = 16;   // mechanism tile columns (16 rows): 16 or 12 (lean_mech.hpp lnm_tile)
+  // measurement: per-phase device time of the lean mechanism step (tile
+  // kernel, kinetics, reacting-cell state kernel; ms summed) and the number of
+  // launches timed (lnm_phase_ms[3]); the host waits for every step's events
+  bool lnm_timing = false;
+  double lnm_phase_ms[4] = {0, 0, 0, 0};
   // HF2D_STAGGER: staggered start of the inviscid tile kernel's resident
   // dispatch rounds, 10 ns ticks per round of cu_count workgroups; > 0 whole
   // rounds, < 0 a linear ramp (headline 2000x200, 1x MI355X, after the fast
