@@ -135,10 +135,6 @@ PYBIND11_MODULE(_hf2d, m) {
   m.attr("CELL_RECORD_BYTES") = (int)sizeof(CellRecord);
   m.attr("NEQ") = NEQ;
   m.def("gpu_available", &gpu_available);
-  m.def(
-      "profiler_region",
-      [](bool on) { DeviceSolver::profiler_region(on); },
-      py::arg("on"), "rocprofv3 --selected-regions: collect only between profiler_region(True) and (False)");
   // hf_div / hf_sqrt evaluated on the GPU (csrc/hip/numerics.hip): (a / b, sqrt(a))
   m.def("div_probe", [](py::array_t<double, py::array::c_style | py::array::forcecast> a,
                         py::array_t<double, py::array::c_style | py::array::forcecast> b) {
@@ -148,6 +144,57 @@ PYBIND11_MODULE(_hf2d, m) {
     div_probe(a.data(), b.data(), q.mutable_data(), s.mutable_data(), n);
     return py::make_tuple(q, s);
   });
+  // k-omega SST source / flux terms of single interior, active nodes
+  // (physics.hpp turb_sst) for an independent NumPy oracle
+  // (tests/test_sst_oracle.py): inputs [17, n] rows rho, rho k, rho omega, mu,
+  // U, V, y, l_min, dU/dx, dU/dy, dV/dx, dV/dy, dk/dx, dk/dy, domega/dx,
+  // domega/dy, CP; returns [9, n]: mu_t, Src_k, Src_omega, RX_k, RX_omega,
+  // RY_k, RY_omega, F_k, F_omega
+  m.def(
+      "sst_probe",
+      [](py::array_t<double, py::array::c_style | py::array::forcecast> in, double dt, double dx, double dy, int FT,
+         double turb_I) {
+        if (in.ndim() != 2 || in.shape(0) != 17) throw std::runtime_error("sst_probe: inputs [17, n]");
+        const long n = (long)in.shape(1);
+        py::array_t<double> out({9L, n});
+        const double* a = in.data();
+        double* o = out.mutable_data();
+        FillParams P;
+        P.dt = dt;
+        P.dx = dx;
+        P.dy = dy;
+        P.FT = FT;
+        P.turb_I = turb_I;
+        for (long q = 0; q < n; q++) {
+          CellLocal c{};
+          auto v = [&](int r) { return a[(long)r * n + q]; };
+          c.S[I_RHO] = v(0);
+          c.S[I_K] = v(1);
+          c.S[I_OMEGA] = v(2);
+          c.mu = v(3);
+          c.U = v(4);
+          c.V = v(5);
+          c.y = v(6);
+          c.l_min = v(7);
+          c.dUdx = v(8);
+          c.dUdy = v(9);
+          c.dVdx = v(10);
+          c.dVdy = v(11);
+          c.dkdx = v(12);
+          c.dkdy = v(13);
+          c.depsdx = v(14);
+          c.depsdy = v(15);
+          c.CP = v(16);
+          c.CT = 0;
+          c.TurbType = TCT_k_omega_SST_Model;
+          turb_sst(c, P, 1, 0);
+          const double r[9] = {c.mu_t, c.Src[I_K], c.Src[I_OMEGA], c.RX[I_K], c.RX[I_OMEGA], c.RY[I_K], c.RY[I_OMEGA],
+                               c.F[I_K], c.F[I_OMEGA]};
+          for (int k = 0; k < 9; k++) o[(long)k * n + q] = r[k];
+        }
+        return out;
+      },
+      py::arg("inputs"), py::arg("dt"), py::arg("dx"), py::arg("dy"), py::arg("FT") = 0, py::arg("turb_I") = 0.005);
   // K12 kinetics for runtime mechanisms on the MFMA cores (csrc/hip/chem_mech.hip): mechanism
   // given as a built-in name or the text of a .mech file; returns (rhoY, T, mean ms)
   m.def(

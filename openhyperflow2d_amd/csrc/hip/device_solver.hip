@@ -2764,14 +2764,6 @@ void DeviceSolver::poison_cell(int gi, int j) {
 // driver phases as roctx ranges (rocprofv3 --marker-trace)
 void DeviceSolver::trace_push(const char* name) { roctxRangePush(name); }
 void DeviceSolver::trace_pop() { roctxRangePop(); }
-// rocprofv3 --selected-regions: collection only between profiler_region(true)
-// and profiler_region(false) (bench.py --prof-region)
-void DeviceSolver::profiler_region(bool on) {
-  if (on)
-    roctxProfilerResume(0);
-  else
-    roctxProfilerPause(0);
-}
 
 void DeviceSolver::sync_scalars() {
   flush_pending();

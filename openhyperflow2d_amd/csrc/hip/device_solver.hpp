@@ -98,7 +98,6 @@ class DeviceSolver : public SolverBase {
   // timing stand-in: rank `rank` of `nranks` with every peer ready and the
   // neighbours' mailboxes looped back into this rank's own (device_solver.hip)
   void p2p_loopback(int rank, int nranks);
-  static void profiler_region(bool on);
   bool p2p_active() const;
   bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
   bool fx_step = false, fx_pending = false;

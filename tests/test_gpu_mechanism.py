@@ -190,3 +190,22 @@ def test_lean_mech_equals_split(gpu, deck):
     ra[np.isnan(ra)] = 0
     rb[np.isnan(rb)] = 0
     np.testing.assert_array_equal(ra.view(np.uint64), rb.view(np.uint64))
+
+
+def test_lnm_phase_timing_is_measurement_only(gpu):
+    """DeviceSolver.lnm_timing (hipEvents around the tile kernel, the
+    kinetics and the reacting-cell state kernel; tools/scramjet_phases.py)
+    times every lean mechanism step and leaves the results bit for bit."""
+    text = decks.with_mechanism(decks.scramjet(300, 48, nmax=10 ** 6, nout=10 ** 5), tmin=200.0)
+    a = gpu.Simulation(text, "gpu")
+    b = gpu.Simulation(text, "gpu")
+    a.solver.use_graph = b.solver.use_graph = False
+    a.solver.lnm_timing = True
+    a.step(20)
+    b.step(20)
+    tile, chem, state, n = a.solver.lnm_phase_ms
+    assert n == a.solver.lnm_steps > 0
+    assert tile > 0 and chem > 0 and state > 0
+    assert a.summary()["dt"] == b.summary()["dt"]
+    for f in ("rho", "U", "T", "Y:H2", "Y:OH"):
+        np.testing.assert_array_equal(a.field(f), b.field(f), err_msg=f)
