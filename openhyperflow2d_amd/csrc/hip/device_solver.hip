@@ -748,10 +748,13 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile_tr(StepParams P, LeanSoA
 
 // Same step with the multi-GPU exchange fused in (FusedX).
 template <bool RES, bool OUT, bool SG, int CPT>
+// (the exchange arguments by pointer, read where they are used: by value
+// they took ~26 SGPRs of the kernel arguments, and the 64-thread fused
+// kernel spilled 96 SGPRs to VGPR lanes against 28 for the plain one)
 __global__ __launch_bounds__(BLOCK) void hf2d_lean_tile_fx(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
                                                             int slot, int slot_next, int serial,
-                                                            ResidualPack* partials, FusedX X) {
-  lean_tile_body<RES, OUT, SG, CPT, true>(P, L, T, sc, slot, slot_next, serial, partials, X);
+                                                            ResidualPack* partials, const FusedX* __restrict__ X) {
+  lean_tile_body<RES, OUT, SG, CPT, true>(P, L, T, sc, slot, slot_next, serial, partials, *X);
 }
 
 // Small-strip geometries (single gas): NT = 128 / 64 threads per workgroup
@@ -766,8 +769,8 @@ __global__ __launch_bounds__(NT) void hf2d_lean_tile_nt(StepParams P, LeanSoA L,
 template <bool RES, bool OUT, int NT, int CPT>
 __global__ __launch_bounds__(NT) void hf2d_lean_tile_fx_nt(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
                                                           int slot, int slot_next, int serial,
-                                                          ResidualPack* partials, FusedX X) {
-  lean_tile_body<RES, OUT, true, CPT, true, false, NT>(P, L, T, sc, slot, slot_next, serial, partials, X);
+                                                          ResidualPack* partials, const FusedX* __restrict__ X) {
+  lean_tile_body<RES, OUT, true, CPT, true, false, NT>(P, L, T, sc, slot, slot_next, serial, partials, *X);
 }
 template <int NT, int CPT>
 __global__ __launch_bounds__(NT) void hf2d_lean_tile_tr_nt(StepParams P, LeanSoA L, LeanTile T, DevScalars* sc,
@@ -1777,7 +1780,7 @@ static const FillK kFill[4][4] = {
     {hf2d_fill<SK_MECH, 9>, hf2d_fill_occ<SK_MECH, 9, 2>, hf2d_fill_occ<SK_MECH, 9, 3>, hf2d_fill_occ<SK_MECH, 9, 4>}};
 
 using TileK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*, int);
-using TileFxK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*, FusedX);
+using TileFxK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*, const FusedX*);
 using TileTrK = void (*)(StepParams, LeanSoA, LeanTile, DevScalars*, int, int, int, ResidualPack*,
                          unsigned long long*);
 // [single gas][cells per thread - 1][0 plain, 1 outputs, 2 residual]
@@ -1933,6 +1936,9 @@ struct DeviceSolver::Impl {
   bool sc_mirrored = false;
   unsigned* host_done = nullptr;   // host_tail's completion counters
   hipEvent_t lnm_ev[4] = {nullptr, nullptr, nullptr, nullptr};   // DeviceSolver::lnm_timing
+  FusedX* fx_dev = nullptr;   // fx_device: the tile kernels' copy of fused_args()
+  FusedX fx_dev_host{};
+  bool fx_dev_valid = false;
   ResidualPack* partials = nullptr;
   ResidualPack* res_out = nullptr;
   ResidualPack* res_host = nullptr;   // pinned
@@ -3447,6 +3453,24 @@ void DeviceSolver::exchange_dt(int dt_slot) {
   HIP_CHECK(hipGetLastError());
 }
 
+// Device copy of the fused-exchange arguments for the tile kernels (uploaded
+// when they change: at the first fused step, which is never inside a graph
+// capture -- the lean entry step runs eagerly)
+const FusedX* DeviceSolver::fx_device(const FusedX& X) {
+  Impl& m = *impl;
+  if (!m.fx_dev) m.fx_dev = m.mem.alloc<FusedX>(1);
+  if (!m.fx_dev_valid || std::memcmp(&m.fx_dev_host, &X, sizeof X) != 0) {
+    hipStreamCaptureStatus cs_ = hipStreamCaptureStatusNone;
+    HIP_CHECK(hipStreamIsCapturing(m.stream, &cs_));
+    if (cs_ != hipStreamCaptureStatusNone) throw std::runtime_error("fused exchange arguments changed inside a graph capture");
+    HIP_CHECK(hipStreamSynchronize(m.stream));
+    HIP_CHECK(hipMemcpy(m.fx_dev, &X, sizeof X, hipMemcpyHostToDevice));
+    m.fx_dev_host = X;
+    m.fx_dev_valid = true;
+  }
+  return m.fx_dev;
+}
+
 FusedX DeviceSolver::fused_args() const {
   const Impl& m = *impl;
   const Impl::P2P& p = m.p2p;
@@ -4044,7 +4068,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
                          st, P, L, T, m.sc, slot, slot_next, serial, m.partials, tile_trace);
     else if (fx_step)
       hipLaunchKernelGGL(nt == BLOCK ? kTileFx[sg][cpt - 1][var] : kTileFxNt[nts][cpt - 1][var], dim3(ntile),
-                         dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials, X);
+                         dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials, fx_device(X));
     else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace && nt == BLOCK)
       hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                          m.sc, slot, slot_next, serial, m.partials);

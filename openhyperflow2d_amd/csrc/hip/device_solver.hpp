@@ -103,6 +103,7 @@ class DeviceSolver : public SolverBase {
   bool fx_step = false, fx_pending = false;
   void p2p_complete();
   struct FusedX fused_args() const;
+  const struct FusedX* fx_device(const struct FusedX& X);
   void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import
   int comm_rank() const;
   int comm_size() const;
