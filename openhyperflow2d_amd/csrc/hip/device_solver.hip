@@ -1055,6 +1055,9 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
 }
 
+// (LnsArrays by value: passed by device pointer instead, the k-eps
+// kernel spilled 215 instead of 254 SGPRs but the resonator ran 2.5 % and
+// Step 3.8 % slower: the fields were re-loaded inside the fills)
 template <bool RES, int MODE, int TURB = 2>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
                                                         int slot, int slot_next, int serial, ResidualPack* partials,
