@@ -48,7 +48,8 @@ def _ninja_file() -> str:
         "ninja_required_version = 1.5",
         f"hipcc = {hipcc}",
         f"cxxflags = {common} -x c++ -I{CSRC}",
-        f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC} -I{os.path.abspath(BUILD)}",
+        f"hipflags = {common} -x hip --offload-arch={ARCH} -ffp-contract=off -munsafe-fp-atomics -I{CSRC} -I{os.path.abspath(BUILD)}"
+        + ((" " + os.environ["HF2D_HIPFLAGS_EXTRA"]) if os.environ.get("HF2D_HIPFLAGS_EXTRA") else ""),
         f"pyflags = -I{_pybind_include()} -I{py_inc}",
         f"ldflags = -L{ROCM}/lib -Wl,-rpath,{ROCM}/lib -lamdhip64 -lhiprtc -lrccl -lrocprofiler-sdk-roctx",
         f"python = {sys.executable}",
