@@ -29,8 +29,11 @@ template <class M>
 __global__ __launch_bounds__(256) void hf2d_chem_fast_mark(ChemArgs a) {
   chemk::chem_mark_body<M>(a);
 }
+// (a 2-wave register budget: 256 VGPRs with 42 spilled (116 B scratch)
+// instead of 286 registers at one wave per SIMD; the developed scramjet
+// state's kinetics 0.202 -> 0.165 ms per step, profiles/scramjet_phases_r05.log)
 template <class M>
-__global__ __launch_bounds__(256) void hf2d_chem_fast_list(ChemArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void hf2d_chem_fast_list(ChemArgs a) {
   chemk::chem_list_body<M>(a);
 }
 template <class M>

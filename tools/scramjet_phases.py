@@ -44,6 +44,7 @@ def main():
     sim.solver.synchronize()
     wall = (time.perf_counter() - t1) / a.steps * 1e3
     sim.solver.lnm_phase_ms = [0, 0, 0, 0]
+    sim.solver.use_graph = False   # (every timed step through the host launch path)
     sim.solver.lnm_timing = True
     sim.step(a.steps)
     sim.solver.lnm_timing = False
