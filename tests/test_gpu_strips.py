@@ -25,6 +25,17 @@ def _outputs_deck():
     return t
 
 
+def _assert_same_bytes(a, b):
+    """Byte equality with a short report (pytest's own diff of megabyte files
+    outruns the test time limit)."""
+    x, y = a.read_bytes(), b.read_bytes()
+    if x == y:
+        return
+    k = next((i for i in range(min(len(x), len(y))) if x[i] != y[i]), min(len(x), len(y)))
+    pytest.fail("%s: %d / %d bytes, first difference at byte %d: %r / %r" % (
+        a.name, len(x), len(y), k, x[max(0, k - 60):k + 60], y[max(0, k - 60):k + 60]))
+
+
 def _cut_lines(log):
     return [ln for ln in log.splitlines() if ln.startswith(("Cut(", "Cx ="))]
 
@@ -69,7 +80,7 @@ def test_virtual_rank_driver_outputs_match_single_gpu(gpu, tmp_path, nranks):
     stem = "Wedge15_160x40"
     for name in [stem + ".plt", "tp-" + stem + ".plt", stem + ".hf2d", "HeatFlux-X-" + stem + ".plt",
                  "HeatFlux-Y-" + stem + ".plt"]:
-        assert (one / name).read_bytes() == (many / name).read_bytes(), name
+        _assert_same_bytes(one / name, many / name)
     assert _cut_lines(logs[0]) == _cut_lines(log1) and len(_cut_lines(log1)) >= 3
     # each host keeps only its strip and one ghost column each side
     for r, (a, b) in enumerate(parts):
@@ -100,5 +111,5 @@ def test_native_cli_two_gpu_ranks_match_one(gpu, tmp_path):
     assert "halo transport p2p" in logs[2], logs[2][-2000:]
     stem = "Wedge15_160x40"
     for name in [stem + ".plt", "tp-" + stem + ".plt", stem + ".hf2d", "HeatFlux-X-" + stem + ".plt"]:
-        assert (tmp_path / "r1" / name).read_bytes() == (tmp_path / "r2" / name).read_bytes(), name
+        _assert_same_bytes(tmp_path / "r1" / name, tmp_path / "r2" / name)
     assert _cut_lines(logs[1]) == _cut_lines(logs[2])
