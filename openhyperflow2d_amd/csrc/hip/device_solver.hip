@@ -4078,6 +4078,8 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace && nt == BLOCK)
       hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                          m.sc, slot, slot_next, serial, m.partials);
+    // (multi-gas, one cell per thread, at a 5-wave register budget -- 96
+    // VGPRs + 10 spilled instead of 103: the triple point ran 351 -> 365 us)
     else {
       // single GPU, last step of the host call: the scalars go to the host
       // mirror from the kernel's own tail (host_tail)
