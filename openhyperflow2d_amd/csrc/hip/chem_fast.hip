@@ -21,8 +21,9 @@ namespace {
 
 using chemk::ChemArgs;
 
+// (the integrating kernels at a 2-wave register budget, as hf2d_chem_fast_list)
 template <class M>
-__global__ __launch_bounds__(256) void hf2d_chem_fast(ChemArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void hf2d_chem_fast(ChemArgs a) {
   chemk::chem_dense_body<M>(a);
 }
 template <class M>
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void h
   chemk::chem_list_body<M>(a);
 }
 template <class M>
-__global__ __launch_bounds__(256) void hf2d_chem_fast_op(double* rhoY, const double* rho, const double* e, double* T,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void hf2d_chem_fast_op(double* rhoY, const double* rho, const double* e, double* T,
                                                          long n, double dt, int nsub) {
   chemk::chem_op_body<M>(rhoY, rho, e, T, n, dt, nsub);
 }
