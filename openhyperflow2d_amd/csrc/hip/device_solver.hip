@@ -1070,6 +1070,9 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
 // the same step with the xGMI mailbox exchange fused in (the register
 // budgets of the default kernels: laminar unbounded, k-eps / SST / SA 3
 // waves per SIMD)
+// (FusedX and the halo column list by device pointer, as the fused tile
+// kernels: SGPR spills 170 -> 252 and the resonator's 4-rank loopback
+// exchange 15.8 -> 16.5 us; kept by value)
 template <bool RES, int MODE, int TURB>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step_fx(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
                                                            int slot, int slot_next, int serial,
