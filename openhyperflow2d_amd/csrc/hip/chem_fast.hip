@@ -77,6 +77,8 @@ bool chem_fast_launch(const std::string& mech, const StepParams& P, const SoA& m
   const unsigned nb = (unsigned)((c1 - c0 + 255) / 256);
   if (nb == 0) return true;
   const ChemArgs a = chem_args(mid, out, Tprev, c0, c1, sc, slot, Tchem, nsub, list, count);
+  // (grid-stride over the list; 4096 workgroups measured best in the developed
+  // scramjet state: kinetics 0.166 ms vs 0.172 / 0.173 ms at 1024 / 512)
   if (list && count && list_ready) {
     hipLaunchKernelGGL(hf2d_chem_fast_list<Mech_h2_air_li2004>, dim3(std::min(nb, 4096u)), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess;
