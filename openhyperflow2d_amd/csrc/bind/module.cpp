@@ -795,6 +795,8 @@ PYBIND11_MODULE(_hf2d, m) {
       .def("p2p_fallback", &DeviceSolver::p2p_fallback, py::call_guard<py::gil_scoped_release>())
       .def_property("p2p_active", &DeviceSolver::p2p_active, &DeviceSolver::p2p_set)
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
+      .def_readwrite("p2p_queue_check", &DeviceSolver::p2p_queue_check)
+      .def_readwrite("dt_read_mode", &DeviceSolver::dt_read_mode)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("split_xcd", &DeviceSolver::split_xcd)
       .def_readwrite("grad_every", &DeviceSolver::grad_every)

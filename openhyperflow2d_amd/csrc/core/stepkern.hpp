@@ -142,6 +142,12 @@ struct StepParams {
   // (hip/device_solver.hip host_tail; nullptr: hf2d_scalars_out does it)
   void* host_sc = nullptr;
   unsigned* host_done = nullptr;
+  // device lean tile kernel, single GPU (speed only, the value is the same):
+  // dt_fold = 1: the last workgroup to finish folds the dt shards of the next
+  // slot into its word (completion count on host_done); dt_read = 2: the
+  // step reads only the word (the previous launch folded), 1: the word and
+  // the shards with one vector load per lane, 0: with scalar loads
+  int dt_fold = 0, dt_read = 0;
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

@@ -82,9 +82,30 @@ __host__ inline void dt_set_host(DevScalars& s, int slot, unsigned long long b) 
   for (int k = 0; k < DT_SHARDS; k++) s.dt_sh[slot][k][0] = b;
 }
 
+// dt_get with one vector load per lane (lane k < DT_SHARDS: shard k, lane
+// DT_SHARDS: the word) and a cross-lane MIN: the loads wait on vmcnt with the
+// tile staging instead of on lgkmcnt with its LDS stores.  Every lane of the
+// wavefront must be active.
+__device__ inline double dt_get_wave(const DevScalars* sc, int slot) {
+  const int lane = (int)(threadIdx.x & 63);
+  unsigned long long b = ~0ull;
+  if (lane < DT_SHARDS) b = sc->dt_sh[slot][lane][0];
+  else if (lane == DT_SHARDS) b = sc->dt_bits[slot];
+#pragma unroll
+  for (int off = 1; off < 32; off <<= 1) b = dt_bits_min(b, (unsigned long long)__shfl_xor((long long)b, off, 64));
+  return bits_to_d((unsigned long long)__shfl((long long)b, 0, 64));
+}
+
 // dt of the step reading the slot
 __device__ inline double dt_cur(const StepParams& P, const DevScalars* sc, int slot) {
   return __builtin_expect(P.lag_dt != 0, 0) ? bits_to_d(sc->dt_lag[slot]) : dt_get(sc, slot);
+}
+// the lean tile kernel's read (StepParams::dt_read)
+__device__ inline double dt_cur_tile(const StepParams& P, const DevScalars* sc, int slot) {
+  if (__builtin_expect(P.lag_dt != 0, 0)) return bits_to_d(sc->dt_lag[slot]);
+  if (P.dt_read == 2) return bits_to_d(sc->dt_bits[slot]);
+  if (P.dt_read == 1) return dt_get_wave(sc, slot);
+  return dt_get(sc, slot);
 }
 // first kernel of a lagged step, one thread, before the slot's word is
 // overwritten with this step's dt: the previous step's MIN goes to the next
@@ -96,8 +117,8 @@ __device__ inline void lag_head(const StepParams& P, DevScalars* sc, int slot, i
   }
 }
 
-__device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot) {
-  const double dt = dt_cur(P, sc, slot);
+__device__ inline void apply_dt(StepParams& P, const DevScalars* sc, int slot, bool tile = false) {
+  const double dt = tile ? dt_cur_tile(P, sc, slot) : dt_cur(P, sc, slot);
   P.dt = dt;
   P.dtdx = dt / P.dx;
   P.dtdy = dt / P.dy;

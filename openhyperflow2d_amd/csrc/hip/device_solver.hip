@@ -23,6 +23,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -521,12 +522,24 @@ __device__ __forceinline__ void host_mirror_tail(const StepParams& P, DevScalars
     }
   }
   if (!__shfl(last, 0, WAVE)) return;
+  unsigned long long b = ~0ull;
+  if (lane < DT_SHARDS) b = __hip_atomic_load(&sc->dt_sh[slot_next][lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == DT_SHARDS) b = __hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (P.dt_fold) {
+    // the step's MIN into the slot's word: the next step reads one word
+    // (StepParams::dt_read = 2) instead of the word and 16 shards
+    unsigned long long m = b;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) m = dt_bits_min(m, (unsigned long long)__shfl_xor((long long)m, off, WAVE));
+    m = (unsigned long long)__shfl((long long)m, 0, WAVE);
+    if (lane == DT_SHARDS) {
+      b = m;
+      __hip_atomic_store(&sc->dt_bits[slot_next], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (!P.host_sc) return;
   DevScalars* h = static_cast<DevScalars*>(P.host_sc);
-  if (lane < DT_SHARDS)
-    h->dt_sh[slot_next][lane][0] =
-        __hip_atomic_load(&sc->dt_sh[slot_next][lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lane == DT_SHARDS)
-    h->dt_bits[slot_next] = __hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane <= DT_SHARDS) (lane < DT_SHARDS ? h->dt_sh[slot_next][lane][0] : h->dt_bits[slot_next]) = b;
   if (lane == DT_SHARDS + 1) h->neg_T = __hip_atomic_load(&sc->neg_T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // (workgroup 0's head, thread 0, after its updates of the slot words)
@@ -593,7 +606,7 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
   const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
-  apply_dt(P, sc, slot);
+  apply_dt(P, sc, slot, true);
   if (b == 0 && threadIdx.x < WAVE) {
     // lagged dt with the fold deferred (X.defer): the previous step's tail
     // waited for the two neighbours only; the other ranks' dt of that step
@@ -729,7 +742,8 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
     }
   }
   if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev);
-  if (OUT && !RES && !FX && !TR && P.host_sc && threadIdx.x < WAVE) host_mirror_tail(P, sc, slot_next);
+  if (!FX && !TR && (P.dt_fold || (OUT && !RES && P.host_sc)) && threadIdx.x < WAVE)
+    host_mirror_tail(P, sc, slot_next);
 }
 
 // No occupancy attribute on the default kernel: the backend's own register
@@ -2221,6 +2235,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_STAGGER")) tile_stagger = std::atoi(e);
   if (const char* e = std::getenv("HF2D_SC_KERNEL")) impl->sc_kernel = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_HOST_TAIL")) host_tail = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_DT_READ")) dt_read_mode = std::atoi(e);
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
@@ -2785,7 +2800,11 @@ void DeviceSolver::sync_scalars() {
   p2p_complete();
   Impl& m = *impl;
   if (m.sc_mirrored) {
-    // the last step wrote the mirror (host_tail)
+    // the last step wrote the mirror (host_tail).  It refreshes ONLY the dt
+    // shards, dt_bits, dt_lag, time_part and neg_T of sc_host; the other
+    // DevScalars fields there (iter, scenario beta / CFL, dt_val, hot counts)
+    // are stale, so this function must read nothing else below this point
+    // (hf2d_scalars_out / the memcpy refresh the whole header).
   } else if (m.sc_kernel) {
     hipLaunchKernelGGL(hf2d_scalars_out, dim3(1), dim3(WAVE), 0, m.stream, m.sc, m.sc_host, (int)(nstep % 3));
     HIP_CHECK(hipGetLastError());
@@ -3035,6 +3054,36 @@ void DeviceSolver::p2p_import(const std::vector<std::string>& descs) {
   Impl::P2P& p = m.p2p;
   if (!p.base) throw std::runtime_error("p2p_import before p2p_export");
   if ((int)descs.size() != m.nranks) throw std::runtime_error("p2p_import: need one descriptor per rank");
+  if (p2p_queue_check) {
+    // In-process ranks on one device (virtual ranks: tests, one-GPU boxes).
+    // Every rank's exchange kernel ends in a workgroup that spins until all
+    // peers have published, so the ranks' kernels must run concurrently.  HIP
+    // maps a process's streams onto at most GPU_MAX_HW_QUEUES hardware queues
+    // per device (default 4) and past that puts two streams on one queue,
+    // whose packets run in order: a spinning kernel then holds back the peer
+    // kernel queued behind it until the bounded wait expires ("rank 0 timed
+    // out waiting for its peers", the round-5 4-rank probe).  Measured on
+    // MI355X (tools/hwq_probe.py, profiles/hwq_probe_r06.md): n ranks in one
+    // process co-schedule iff GPU_MAX_HW_QUEUES >= n + 1 (3 and 4 queues,
+    // 4 and 8, 8 and 16 pass; 4 and 4, 8 and 8 time out).  Separate
+    // processes (the multi-GPU layout) have queues of their own.
+    int local = 0;
+    for (const std::string& s : descs) {
+      P2PDesc d;
+      if (s.size() != sizeof d) continue;
+      std::memcpy(&d, s.data(), sizeof d);
+      local += (d.pid == (int32_t)getpid() && d.device == dev) ? 1 : 0;
+    }
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int hwq = (q && std::atoi(q) > 0) ? std::atoi(q) : 4;
+    if (local > 1 && local + 1 > hwq)
+      throw std::runtime_error("p2p_import: " + std::to_string(local) + " mailbox ranks share device " +
+                               std::to_string(dev) + " in one process, which has " + std::to_string(hwq) +
+                               " HIP hardware queues (GPU_MAX_HW_QUEUES); their exchange kernels wait for each "
+                               "other, so each rank needs a queue of its own plus one for the default stream: set "
+                               "GPU_MAX_HW_QUEUES >= " + std::to_string(local + 1) +
+                               " before the first HIP call, or run the ranks as separate processes");
+  }
   p.peer_base.assign(m.nranks, nullptr);
   for (int q = 0; q < m.nranks; q++) {
     P2PDesc d;
@@ -3581,8 +3630,9 @@ uint64_t DeviceSolver::mode_signature() const {
 
 StepResult DeviceSolver::do_step(const StepParams& P0, bool want_res) {
   Impl& m = *impl;
-  // (the in-process host transport synchronises on the host: eager only)
-  const bool plain = use_graph && !want_res && !step_outputs && (!m.local || m.p2p.on) &&
+  // (the in-process host transport synchronises on the host: eager only;
+  // so does lnm_timing, which waits for each step's phase events)
+  const bool plain = use_graph && !want_res && !step_outputs && !lnm_timing && (!m.local || m.p2p.on) &&
                      !(lean && lean_ok && lean_state == 0) &&
                      !(lns_state == 0 && lns_entry(P0));   // lean N-S entry step: eager
   if (!plain || (pending.empty() && nstep % GRAPH_STEPS != 0)) {
@@ -3610,6 +3660,7 @@ void DeviceSolver::run_graph() {
   if (!graph) graph.reset(new GraphCache);
   if (graph->exec && graph->sig == sig) {
     HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
+    dt_word_valid = false;   // (conservative: the next eager step reads the shards too)
     nstep += GRAPH_STEPS;   // ping-pong parities are unchanged after an even number of steps
     pending.clear();
     graph_launches++;
@@ -3621,6 +3672,8 @@ void DeviceSolver::run_graph() {
   std::vector<StepParams> q;
   q.swap(pending);
   hipGraph_t g = nullptr;
+  // (a replayed window may follow any launch: its first step reads the shards)
+  dt_word_valid = false;
   bool ok = hipStreamBeginCapture(m.stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
   if (ok) {
     try {
@@ -3896,11 +3949,18 @@ void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const Lea
   const size_t shmem = (size_t)L.total() * sizeof(real);
   const int strip = P.i1 < P.nx ? 1 : 0;
   const LnmK k = kLnm[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip];
-  static bool attr_set[2][2][2] = {};
-  if (!attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip]) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-    (void)hipGetLastError();
-    attr_set[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip] = true;
+  // the dynamic-LDS limit is a property of the kernel function, shared by
+  // every solver of the process (virtual ranks run on threads): raise it to
+  // the largest layout asked for so far (tile width / species count vary)
+  static std::atomic<int> attr_bytes[2][2][2] = {};
+  static std::mutex attr_mu;
+  std::atomic<int>& ab = attr_bytes[want_res ? 1 : 0][lnm_turb == 3 ? 1 : 0][strip];
+  if (ab.load(std::memory_order_acquire) < (int)shmem) {
+    std::lock_guard<std::mutex> lk(attr_mu);
+    if (ab.load(std::memory_order_relaxed) < (int)shmem) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+      ab.store((int)shmem, std::memory_order_release);
+    }
   }
   // lnm_timing: events around the three phases (measurement only: the host
   // waits for each step's events, so the steps serialise with the host)
@@ -3983,6 +4043,9 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   int nres_waves = BLOCK / WAVE;   // ... and partials per workgroup
   const bool sg_now = lean_sg && lean_sg_ok;
   fx_step = false;
+  // the slot's word holds the MIN only right after a folding tile launch
+  const bool dt_word_ok = dt_word_valid;
+  dt_word_valid = false;
   const bool tile_path = euler && lean && lean_ok && lean_tile &&
                          lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ;
   if (!tile_path) p2p_complete();
@@ -4091,6 +4154,15 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
         P.host_sc = m.sc_host;
         P.host_done = m.host_done;
       }
+      // dt read of the tile kernel (StepParams::dt_read): with dt_read_mode
+      // 2 every step's last workgroup folds the shards into the word and the
+      // next step's workgroups read that one word
+      const bool fold = dt_read_mode == 2 && !tile_trace && m.nranks == 1 && !m.local && !m.p2p.on;
+      P.dt_read = (fold && dt_word_ok) ? 2 : dt_read_mode == 1 ? 1 : 0;
+      if (fold) {
+        P.dt_fold = 1;
+        P.host_done = m.host_done;
+      }
       if (nt != BLOCK)
         hipLaunchKernelGGL(kTileNt[nts][cpt - 1][var], dim3(ntile), dim3(nt), shmem, st, P, L, T, m.sc, slot,
                            slot_next, serial, m.partials, 0);
@@ -4098,6 +4170,7 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
         hipLaunchKernelGGL(kTile[sg][cpt - 1][var], dim3(ntile), dim3(BLOCK), shmem, st, P, L, T, m.sc, slot,
                            slot_next, serial, m.partials, 0);
       m.sc_mirrored = mirror;
+      dt_word_valid = fold;
     }
     HIP_CHECK(hipGetLastError());
     nres = ntile;

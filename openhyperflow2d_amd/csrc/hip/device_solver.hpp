@@ -2,10 +2,13 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../core/solver.hpp"
@@ -24,18 +27,39 @@ bool gpu_available();
 // (RCCL refuses two ranks on one device).
 struct LocalGroup {
   explicit LocalGroup(int n_)
-      : n(n_), send_l(n_), send_r(n_), dt_src(n_, nullptr), vals(n_), packs(n_), blobs(n_) {}
+      : n(n_), send_l(n_), send_r(n_), dt_src(n_, nullptr), vals(n_), packs(n_), blobs(n_) {
+    const char* j = std::getenv("HF2D_LOCAL_JITTER_US");
+    jitter_us = j ? std::max(0, std::atoi(j)) : 0;
+  }
   int n;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   long gen = 0;
+  // race probe (HF2D_LOCAL_JITTER_US = J > 0): every rank sleeps a
+  // pseudo-random 0..J us before each barrier, so the threads reach the
+  // collectives and the D2D halo copies in varying orders; a result that
+  // depends on that order is an ordering hole (tools/strip_outputs_check.py)
+  int jitter_us = 0;
+  unsigned long long jitter_state = 0x9E3779B97F4A7C15ull;
+  void jitter() {
+    unsigned long long x;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      jitter_state ^= jitter_state << 13;
+      jitter_state ^= jitter_state >> 7;
+      jitter_state ^= jitter_state << 17;
+      x = jitter_state;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds((long)(x % (unsigned long long)jitter_us)));
+  }
   std::vector<real*> send_l, send_r;
   std::vector<const unsigned long long*> dt_src;   // device dt slot of each rank
   std::vector<double> vals;
   std::vector<ResidualPack> packs;
   std::vector<std::string> blobs;   // allgather_bytes slots
   void barrier() {
+    if (jitter_us > 0) jitter();
     std::unique_lock<std::mutex> lk(mu);
     const long g = gen;
     if (++arrived == n) {
@@ -100,6 +124,12 @@ class DeviceSolver : public SolverBase {
   void p2p_loopback(int rank, int nranks);
   bool p2p_active() const;
   bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
+  bool p2p_queue_check = true;
+  // lean tile dt read (StepParams::dt_read / dt_fold; HF2D_DT_READ): 0 word +
+  // shards by scalar loads, 1 by one vector load per lane, 2 the previous
+  // step's last workgroup folds them into the word (single GPU)
+  int dt_read_mode = 1;
+  bool dt_word_valid = false;   // p2p_import refuses more in-process ranks than HIP hardware queues allow
   bool fx_step = false, fx_pending = false;
   void p2p_complete();
   struct FusedX fused_args() const;

@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# In-process virtual ranks (one DeviceSolver + HIP stream per rank, one host
+# thread each) with the xGMI mailbox transport need every rank's stream on a
+# hardware queue of its own plus one for the default stream: n ranks need
+# GPU_MAX_HW_QUEUES >= n + 1 (tools/hwq_probe.py, profiles/hwq_probe_r06.md;
+# DeviceSolver::p2p_import refuses fewer).  The GPU suite runs up to 8 such
+# ranks, so it asks HIP for 16 queues before the first HIP call.  (Real
+# multi-GPU runs are one process per GPU and need no such setting.)
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -392,7 +392,8 @@ def test_graph_windows_after_a_download_replay_the_right_buffers(gpu, deck):
 @pytest.mark.parametrize("deck,nranks,p2p", [("step", 3, False), ("resonator", 4, False), ("sst_plate", 3, False),
                                             ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True),
                                             ("resonator", 3, "fx"), ("step", 2, "fx"), ("sst_plate", 3, "fx"),
-                                            ("scramjet", 3, "fx")])
+                                            ("scramjet", 3, "fx"), ("resonator", 4, "fx"), ("resonator", 8, "fx"),
+                                            ("scramjet", 4, "fx"), ("scramjet", 8, "fx")])
 def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     """Lean N-S / mechanism tiles on strips (two ghost columns: the tile
     evaluates the fill of the first one, which reads the second; HALO_LNS
@@ -493,13 +494,15 @@ def test_comm_overlap_split_step_matches_single_gpu(gpu):
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
 
 
-# <= 3 in-process ranks: their streams must land on distinct hardware queues
-# (GPU_MAX_HW_QUEUES=4) or a spinning exchange could sit in front of the step
-# it waits for; separate processes (the real deployment) have no such limit.
+# In-process ranks need a hardware queue each plus one (conftest sets
+# GPU_MAX_HW_QUEUES=16; test_p2p_import_refuses_too_few_queues covers the
+# guard); separate processes (the real deployment) have queues of their own.
 @pytest.mark.parametrize("nranks,physics,lean,fuse,nt", [(2, "euler", True, False, 256), (3, "euler", True, False, 256),
                                                          (3, "kes", False, True, 256), (2, "euler", True, True, 256),
                                                          (3, "euler", True, True, 256), (3, "euler", True, "toggle", 256),
-                                                         (3, "euler", True, True, 64), (2, "euler", True, True, 128)])
+                                                         (3, "euler", True, True, 64), (2, "euler", True, True, 128),
+                                                         (4, "euler", True, True, 256), (8, "euler", True, True, 256),
+                                                         (4, "kes", False, True, 256), (8, "euler", True, False, 256)])
 def test_p2p_virtual_ranks_match_single_gpu(gpu, nranks, physics, lean, fuse, nt):
     """xGMI mailbox transport (hf2d_p2p_xchg: direct peer stores, system-scope
     flags, device-side dt MIN; fuse: the same exchange folded into the lean
@@ -536,6 +539,30 @@ def test_p2p_self_validation_failure_falls_back(gpu):
     assert summ["dt"] == ref.summary()["dt"]
     for f in FIELDS:
         np.testing.assert_array_equal(got[f], ref.field(f), err_msg=f)
+
+
+def test_p2p_import_refuses_too_few_queues(gpu):
+    """More in-process mailbox ranks than the process's HIP hardware queues
+    can co-schedule (n ranks need GPU_MAX_HW_QUEUES >= n + 1): p2p_import
+    refuses with a message naming the setting, instead of a start-up probe
+    that times out (the round-5 4-rank failure, tools/hwq_probe.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from tests.conftest import ROOT
+
+    tool = os.path.join(ROOT, "tools", "hwq_probe.py")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="4")
+    out = {}
+    for n in (3, 4):
+        r = subprocess.run([sys.executable, tool, "--ranks", str(n), "--nx", "120", "--ny", "24"], env=env,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        out[n] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out[3].get("ok") is True, out[3]
+    assert "GPU_MAX_HW_QUEUES >= 5" in out[4].get("refused", ""), out[4]
 
 
 def _p2p_proc_worker(rank, world, port, text, schedule, out):
@@ -879,6 +906,30 @@ def test_tile_stagger_is_timing_only(gpu, monkeypatch, stagger):
         np.testing.assert_array_equal(s.field(f), ref.field(f), err_msg=f)
 
 
+@pytest.mark.parametrize("mode,nt,graphs", [(0, 256, True), (2, 256, True), (2, 64, False), (2, 128, True)])
+def test_tile_dt_read_modes_match_cpu(gpu, monkeypatch, mode, nt, graphs):
+    """How the tile kernel reads the step's dt (StepParams::dt_read): one
+    vector load per lane of the word + 16 shards (1), or the one word that the
+    previous step's last workgroup folded the shards into (2, dt_fold) -- the
+    same MIN, so the dt sequence and the fields equal the CPU stepper bit for
+    bit across residual steps, one-step calls (host mirror tail), downloads
+    and graph windows."""
+    text = decks.wedge15(600, 80, nmax=10 ** 6, nout=10 ** 5)
+    monkeypatch.setenv("HF2D_AUTOTUNE", "0")
+    g = gpu.Simulation(text, "gpu")
+    g.solver.dt_read_mode = mode
+    g.solver.lean_nt = nt
+    g.solver.use_graph = graphs
+    c = gpu.Simulation(text, "cpu")
+    for n, res in [(1, False), (5, True), (25, False), (1, False), (13, False), (3, True), (12, False)]:
+        g.step(n, residual=res)
+        c.step(n, residual=res)
+        assert g.summary()["dt"] == c.summary()["dt"], n
+    assert g.summary()["time"] == c.summary()["time"]
+    for f in FIELDS:
+        np.testing.assert_array_equal(g.field(f), c.field(f), err_msg=f)
+
+
 def _lagged(text):
     return decks.set_key(text, "LaggedDt", 1)
 
@@ -911,7 +962,9 @@ def test_lagged_dt_gpu_equals_cpu(gpu, deck):
     assert std.summary()["dt"] != g.summary()["dt"]
 
 
-@pytest.mark.parametrize("deck,nranks,p2p", [("wedge", 3, "fx"), ("wedge", 3, False), ("resonator", 3, "fx")])
+@pytest.mark.parametrize("deck,nranks,p2p", [("wedge", 4, "fx"), ("wedge", 8, "fx"), ("wedge", 3, "fx"),
+                                            ("wedge", 3, False), ("resonator", 3, "fx"), ("resonator", 4, "fx"),
+                                            ("resonator", 8, "fx")])
 def test_lagged_dt_strips_match_single_gpu(gpu, deck, nranks, p2p):
     """Lagged dt on strips: with the fused mailbox exchange the tail of a
     step waits for its two neighbours only and the next step's first

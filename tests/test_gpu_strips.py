@@ -113,3 +113,50 @@ def test_native_cli_two_gpu_ranks_match_one(gpu, tmp_path):
     for name in [stem + ".plt", "tp-" + stem + ".plt", stem + ".hf2d", "HeatFlux-X-" + stem + ".plt"]:
         _assert_same_bytes(tmp_path / "r1" / name, tmp_path / "r2" / name)
     assert _cut_lines(logs[1]) == _cut_lines(logs[2])
+
+
+def _mailbox_deck(deck, lagged):
+    if deck == "wedge":       # the headline deck family (inviscid, fused mailbox exchange in the tile kernel)
+        t = decks.wedge15(320, 60, nmax=24, nout=12)
+    elif deck == "resonator":  # axisymmetric k-eps, lean N-S tiles, fused push in the tile kernel
+        t = decks.resonator(320, 40, nmax=24, nout=12)
+    else:                      # SST + 9-species kinetics, lean mechanism step + push / unpack
+        t = decks.scramjet(320, 48, nmax=24, nout=12)
+    return decks.set_key(t, "LaggedDt", int(lagged))
+
+
+@pytest.mark.parametrize("deck", ["wedge", "resonator", "scramjet"])
+def test_native_cli_mailbox_ranks_match_one(gpu, tmp_path, deck):
+    """The default multi-GPU transport (xGMI mailboxes, IPC-mapped, validated
+    at start-up) at the BASELINE rank counts: 4 and 8 native processes (one
+    GPU here, so the ranks share it) write the same bytes as one process, with
+    lagged dt off and on.  Separate OS processes, because in-process virtual
+    ranks cannot co-schedule more spinning exchange kernels than the process
+    has HIP hardware queues (DeviceSolver::p2p_import refuses that case)."""
+    import os
+    import subprocess
+
+    from tests.conftest import ROOT
+
+    sh = os.path.join(ROOT, "openhyperflow2d_amd", "bin", "OpenHyperFLOW2D.sh")
+    port = 29820 + 10 * ["wedge", "resonator", "scramjet"].index(deck)
+    for lagged in (0, 1):
+        text = _mailbox_deck(deck, lagged)
+        dirs = {}
+        for k in (1, 4, 8):
+            d = tmp_path / ("l%d_r%d" % (lagged, k))
+            d.mkdir()
+            (d / "D.dat").write_text(text)
+            r = subprocess.run(["timeout", "-k", "10", "240", sh, "D", str(k), "--backend", "gpu", "--cycles", "2"],
+                               cwd=d, capture_output=True, text=True, timeout=300,
+                               env=dict(os.environ, HF2D_MASTER_PORT=str(port + k), HF2D_AUTOTUNE="0"))
+            assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+            if k > 1:
+                assert "halo transport p2p" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+                assert "using RCCL" not in r.stderr, r.stderr[-2000:]
+            dirs[k] = d
+        names = sorted(p.name for p in dirs[1].iterdir() if p.suffix in (".plt", ".hf2d", ".species", ".meta"))
+        assert any(n.endswith(".hf2d") for n in names), names
+        for k in (4, 8):
+            for name in names:
+                _assert_same_bytes(dirs[1] / name, dirs[k] / name)

@@ -4,7 +4,12 @@ transport, generic path) against one GPU: which output files differ and where
 (tests/test_gpu_strips.py::test_virtual_rank_driver_outputs_match_single_gpu
 without pytest's diff of megabyte files).
 
-  python tools/strip_outputs_check.py --ranks 4 [--repeat 2]"""
+  python tools/strip_outputs_check.py --ranks 4 [--repeat 2] [--jitter 200]
+
+--jitter J sets HF2D_LOCAL_JITTER_US: every virtual rank sleeps a random
+0..J us before each LocalGroup barrier (host collectives and halo copies), so
+the ranks' threads interleave differently on every collective.  Equal files
+under jitter mean no host-side ordering hole on this path."""
 import argparse
 import os
 import sys
@@ -20,7 +25,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=4)
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--jitter", type=int, default=0)
     a = ap.parse_args()
+    if a.jitter:
+        os.environ["HF2D_LOCAL_JITTER_US"] = str(a.jitter)
     import openhyperflow2d_amd as hf
     from openhyperflow2d_amd.parallel.strips import balanced_columns
 
