@@ -797,6 +797,9 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("p2p_fuse", &DeviceSolver::p2p_fuse)
       .def_readwrite("p2p_queue_check", &DeviceSolver::p2p_queue_check)
       .def_readwrite("dt_read_mode", &DeviceSolver::dt_read_mode)
+      .def_readwrite("tile_skip_same", &DeviceSolver::tile_skip_same)
+      .def_readwrite("lns_ghost_prologue", &DeviceSolver::lns_ghost_prologue)
+      .def_readonly("lns_prologue_steps", &DeviceSolver::lns_prologue_steps)
       .def_readwrite("fill_occ", &DeviceSolver::fill_occ)
       .def_readwrite("split_xcd", &DeviceSolver::split_xcd)
       .def_readwrite("grad_every", &DeviceSolver::grad_every)

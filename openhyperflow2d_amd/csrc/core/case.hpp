@@ -193,8 +193,13 @@ class Case {
   std::vector<GasFlow> flows, flows2d;
   std::vector<std::pair<int, int>> wall_nodes;     // (i, j)
   // per wall node: directions into the flow (WD_* bits: the neighbour there
-  // is gas, the opposite one solid or outside the grid); WallBlendCells
+  // is gas, the opposite one a solid cell or the lower / upper grid edge); WallBlendCells
   std::vector<uint8_t> wall_dirs;
+  // WallBlendCells: per wall node and direction (x+, x-, y+, y-) the number of
+  // cells the blend covers -- the ray stops at the first solid cell or the
+  // grid edge.  Measured on the whole grid (collect_wall_nodes), so every
+  // strip of a decomposition flags the same cells.
+  std::vector<uint8_t> wall_rays;
   std::vector<std::pair<int, int>> subdomains;     // ScanArea [start, end) pairs
   real dt0 = 1.0;
   real global_time = 0.0;

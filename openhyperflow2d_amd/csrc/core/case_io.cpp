@@ -210,6 +210,7 @@ std::string Case::pack_strip_header(int a, int b) const {
   w.vec(flows2d);
   w.vec(pairs_flat(wall_nodes));
   w.vec(wall_dirs);
+  w.vec(wall_rays);
   w.vec(pairs_flat(subdomains));
   w.pod(dt0);
   w.pod(global_time);
@@ -298,6 +299,7 @@ Case Case::unpack_strip_header(const char* data, size_t size, std::ostream* log,
   r.vec(flat);
   cs.wall_nodes = pairs_of(flat);
   r.vec(cs.wall_dirs);
+  r.vec(cs.wall_rays);
   r.vec(flat);
   cs.subdomains = pairs_of(flat);
   r.pod(cs.dt0);

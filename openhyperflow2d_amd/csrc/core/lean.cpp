@@ -271,22 +271,20 @@ void compute_generic_flags(const Case& cs, HostArrays& h, int gx0) {
     h.gf[idx] = g;
   }
   // WallBlendCells: the first N cells off every no-slip wall node along its
-  // directions into the flow (the global wall list: decomposition independent)
+  // directions into the flow.  The ray lengths come from the whole grid
+  // (Case::wall_rays: the first solid cell or the grid edge ends a ray,
+  // whichever strip holds it), so every decomposition flags the same cells.
   const int nwb = cs.cfg.WallBlendCells;
-  if (nwb > 0 && cs.cfg.ProblemType == SM_NS && cs.wall_dirs.size() == cs.wall_nodes.size()) {
+  if (nwb > 0 && cs.cfg.ProblemType == SM_NS && cs.wall_rays.size() == 4 * cs.wall_nodes.size()) {
     static const int di[4] = {1, -1, 0, 0}, dj[4] = {0, 0, 1, -1};
-    static const uint8_t bit[4] = {WD_XP, WD_XM, WD_YP, WD_YM};
     for (size_t w = 0; w < cs.wall_nodes.size(); w++) {
       for (int d = 0; d < 4; d++) {
-        if (!(cs.wall_dirs[w] & bit[d])) continue;
-        for (int n = 1; n <= nwb; n++) {
+        const int len = cs.wall_rays[4 * w + d];
+        for (int n = 1; n <= len; n++) {
           const int gi = cs.wall_nodes[w].first + n * di[d], j = cs.wall_nodes[w].second + n * dj[d];
           const int li = gi - gx0;
-          if (j < 0 || j >= h.ny || gi < 0 || gi >= cs.J.nx) break;
           if (li < 0 || li >= h.nx) continue;   // (another strip's column)
-          const long idx = (long)li * h.ny + j;
-          if (has_all(h.CT[idx], CT_SOLID)) break;
-          h.gf[idx] |= d < 2 ? GF_WBX : GF_WBY;
+          h.gf[(long)li * h.ny + j] |= d < 2 ? GF_WBX : GF_WBY;
         }
       }
     }

@@ -33,10 +33,19 @@
 #pragma once
 
 #include <algorithm>
+#include <cstring>
 
 #include "stepkern.hpp"
 
 namespace hf2d {
+
+// the two doubles have the same bits (+0 / -0 and NaNs told apart)
+HF_HD inline bool same_bits(real a, real b) {
+  u64 x, y;
+  std::memcpy(&x, &a, sizeof x);
+  std::memcpy(&y, &b, sizeof y);
+  return x == y;
+}
 
 // per-cell lean byte: neighbour bits (NB_*) | who must publish dS/dx, dS/dy
 // LB_PLAIN: interior node on the flag-free predictor fast path (predict_core
@@ -140,6 +149,7 @@ struct LeanIOCommon {
   bool noslip = false;
   real FT = 0;
   const real* obeta = nullptr;   // LeanOwn::beta
+  bool skip_same = false;        // StepParams::skip_same
   real sm[NEQ];
 
   HF_HD LeanIOCommon(const LeanSoA& l, long i) : L(l), N(l.N), idx(i), iL(i), iR(i), iU(i), iD(i) {}
@@ -157,7 +167,9 @@ struct LeanIOCommon {
   HF_HD real Src(int) const { return 0.0; }
   HF_HD real SrcAdd(int k) const { return noslip ? L.SrcAdd[k * N + idx] : 0.0; }
   HF_HD void put_S(int k, real v) { sm[k] = v; }
-  HF_HD void put_beta(int k, real v) const { L.beta[k * N + idx] = v; }
+  HF_HD void put_beta(int k, real v) const {
+    if (!skip_same || !same_bits(v, obeta[k])) L.beta[k * N + idx] = v;
+  }
   HF_HD void put_dS(int k, real a, real b) const {
     if (lb & LB_DX_OUT) L.dSdx_out[k * N + idx] = a;
     if (lb & LB_DY_OUT) L.dSdy_out[k * N + idx] = b;
@@ -265,6 +277,7 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
   constexpr bool SG = IO::NE == 4;        // single-gas specialisation
   io.lb = lb;
   io.obeta = own.beta;
+  io.skip_same = P.skip_same != 0;
   if (!own.filled) {
     // neither transported nor filled: carry the state into the other buffers
     for (int k = 0; k < NE; k++) io.out_S(k, io.S(k));
@@ -385,7 +398,7 @@ HF_HD inline real lean_cell(const StepParams& P, const LeanSoA& L, IO& io, const
         else
           chemistry_zeldovich(c, *P.species, P.sm, P.chem_model);
         if (c.R != own.R) io.out_R(c.R);   // constant for a frozen mixture
-        io.out_CP(c.CP);
+        if (!io.skip_same || !same_bits(c.CP, own.CP)) io.out_CP(c.CP);
         // Y is output-only except for the no-slip SrcAdd of the next step
         if (OUT || noslip)
           for (int q = 0; q < NSPEC; q++) L.Y[q * N + idx] = c.Y[q];

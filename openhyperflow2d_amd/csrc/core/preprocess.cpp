@@ -1177,18 +1177,31 @@ void Case::set_wall_nodes() {
 void Case::collect_wall_nodes() {
   wall_nodes.clear();
   wall_dirs.clear();
-  auto solid_or_out = [&](int i, int j) { return !J.in(i, j) || J.is(i, j, CT_SOLID); };
+  wall_rays.clear();
+  // (a wall behind the node: a solid cell, or the lower / upper grid edge --
+  // a plate on the domain boundary -- but not the inflow / outflow column,
+  // which is no wall in x)
+  auto solid = [&](int i, int j) { return (J.in(i, j) && J.is(i, j, CT_SOLID)) || (i >= 0 && i < J.nx && (j < 0 || j >= J.ny)); };
   auto gas = [&](int i, int j) { return J.in(i, j) && !J.is(i, j, CT_SOLID); };
+  static const int di[4] = {1, -1, 0, 0}, dj[4] = {0, 0, 1, -1};
+  static const uint8_t bit[4] = {WD_XP, WD_XM, WD_YP, WD_YM};
+  const int nwb = std::min(std::max(cfg.WallBlendCells, 0), 255);
   for (int j = 0; j < J.ny; j++)
     for (int i = 0; i < J.nx; i++)
       if (!J.is(i, j, CT_SOLID) && (J.is(i, j, CT_WALL_LAW) || J.is(i, j, CT_WALL_NO_SLIP))) {
         wall_nodes.push_back({i, j});
         uint8_t d = 0;
-        if (gas(i + 1, j) && solid_or_out(i - 1, j)) d |= WD_XP;
-        if (gas(i - 1, j) && solid_or_out(i + 1, j)) d |= WD_XM;
-        if (gas(i, j + 1) && solid_or_out(i, j - 1)) d |= WD_YP;
-        if (gas(i, j - 1) && solid_or_out(i, j + 1)) d |= WD_YM;
+        if (gas(i + 1, j) && solid(i - 1, j)) d |= WD_XP;
+        if (gas(i - 1, j) && solid(i + 1, j)) d |= WD_XM;
+        if (gas(i, j + 1) && solid(i, j - 1)) d |= WD_YP;
+        if (gas(i, j - 1) && solid(i, j + 1)) d |= WD_YM;
         wall_dirs.push_back(d);
+        for (int q = 0; q < 4; q++) {
+          int n = 0;
+          if (d & bit[q])
+            while (n < nwb && gas(i + (n + 1) * di[q], j + (n + 1) * dj[q])) n++;
+          wall_rays.push_back((uint8_t)n);
+        }
       }
 }
 

@@ -148,6 +148,10 @@ struct StepParams {
   // step reads only the word (the previous launch folded), 1: the word and
   // the shards with one vector load per lane, 0: with scalar loads
   int dt_fold = 0, dt_read = 0;
+  // lean tile kernel: stores of the in-place per-cell arrays (beta, CP) are
+  // skipped when the new value has the old value's bits (converged regions;
+  // speed only -- the array holds the same bits either way)
+  int skip_same = 0;
 };
 
 // Register-resident cell used by fill_node / turb_model / chemistry.

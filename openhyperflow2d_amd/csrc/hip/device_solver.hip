@@ -570,6 +570,15 @@ __device__ inline unsigned tile_of_part(unsigned bl, int part, const LeanTile& T
   return bl;
 }
 
+// all tiles, the strip's edge tile columns first (the first one, then the
+// last T.ne), then the interior ones in order
+__device__ inline unsigned tile_edge_first(unsigned bl, const LeanTile& T) {
+  const unsigned nbj = (unsigned)T.nbj, ne = (unsigned)T.ne, nbi = (unsigned)T.nbi;
+  if (nbi < 2 + ne || bl < nbj) return bl;
+  if (bl < (1 + ne) * nbj) return (nbi - ne) * nbj + (bl - nbj);
+  return nbj + (bl - (1 + ne) * nbj);
+}
+
 // NT: threads per workgroup (BLOCK, or 128 / 64 for the small strips of a
 // multi-GPU run: at 250 x 200 cells per GPU a 256-thread tiling leaves ~50 of
 // the 256 CUs without a workgroup, and the step is one workgroup's
@@ -866,6 +875,36 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lean_materialize(StepParams P, Lea
 // ---------------------------------------------------------------------------
 constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho == 0 or k < 1)
 
+// Ghost prologue of a fused lean N-S / mechanism step (replaces the separate
+// hf2d_p2p_unpack launch after the previous fused step): a tile whose fills
+// read a ghost column copies the rows it reads, [j0 - 1, j0 + TJ], of every
+// HALO_LNS entry of the previous step's list Lg from this rank's mailbox of
+// parity seq_prev (the previous kernel's tail acquired the peers' flags) into
+// the ghost columns; the workgroup barrier makes them visible to its own
+// loads.  Vertically adjacent edge tiles write the rows they share with the
+// same values, and every ghost value a tile reads it wrote itself: a
+// workgroup reads its own stores through its CU's L1 (workgroup-scope
+// coherence needs no cache maintenance outside thread-group-split mode; an
+// agent-scope acquire here invalidates the XCD's L2 lines and measured
+// 14.8 -> 23.3 us of exchange cost on the 4-rank Step strip).
+__device__ inline void fx_ghost_prologue(const StepParams& P, const FusedX& X, const ColList* Lg, int i0, int j0,
+                                         int TI, int TJ, unsigned long long seq_prev) {
+  const bool gl = (X.sides & 1) && i0 <= P.i0 + 1;
+  const bool gr = (X.sides & 2) && i0 + TI + 1 >= P.i1;
+  if (!gl && !gr) return;
+  const int par = (int)(seq_prev & 1), nf = Lg->nf;
+  const int jlo = j0 > 0 ? j0 - 1 : 0, jhi = j0 + TJ + 1 < P.ny ? j0 + TJ + 1 : P.ny;
+  const int rows = jhi - jlo, per_side = nf * rows;
+  for (int t = (int)threadIdx.x; t < 2 * per_side; t += (int)blockDim.x) {
+    const int side = t < per_side ? 0 : 1;
+    if (side == 0 ? !gl : !gr) continue;
+    const int tt = t - side * per_side, f = tt / rows, j = jlo + (tt - f * rows);
+    const real v = p2p_load(X.my_recv + ((long)par * 2 + side) * X.cap + (long)f * P.ny + j);
+    Lg->f[f][(long)(side == 0 ? P.i0 - 1 - Lg->o[f] : P.i1 + Lg->o[f]) * P.ny + j] = v;
+  }
+  __syncthreads();
+}
+
 // FX: the multi-GPU exchange fused in (xGMI mailboxes): the cells of the
 // strip's first / last two columns store this step's HALO_LNS values (Lc:
 // the post-step pointers, DeviceSolver::halo_list) into the neighbour's
@@ -874,13 +913,17 @@ constexpr int LNS_SKIP_ERR = 8;   // neg_T bit: fill_node() skipped a node (rho 
 template <bool RES, int MODE, int TURB, bool FX = false>
 __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials,
-                                              int part, const FusedX& X = FusedX{}, const ColList* Lc = nullptr) {
+                                              int part, const FusedX& X = FusedX{}, const ColList* Lc = nullptr,
+                                              const ColList* Lg = nullptr) {
   extern __shared__ real lds[];
   constexpr int NL = Lns<MODE>::NL;
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
   // part: 0 every tile, 1 / 2 the edge / interior tiles (comm overlap)
-  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
+  // (a ghost prologue delays the strip's edge tiles: they go first, so they
+  // do not finish the kernel late)
+  const unsigned b = (FX && Lg != nullptr) ? tile_edge_first(xcd_remap(blockIdx.x, gridDim.x), T)
+                                           : tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   apply_dt(P, sc, slot);
   if (b == 0 && threadIdx.x == 0) {
     dt_reset(sc, slot_reset(slot));
@@ -900,6 +943,8 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   int i, j, c, i0, j0;
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
   int dummy = 0, skip = 0;
+  // 0. the previous fused step's halo from the mailbox into the ghost columns
+  if (FX && Lg != nullptr && seq_prev > 0) fx_ghost_prologue(P, X, Lg, i0, j0, T.TI, T.TJ, seq_prev);
   // 1a. ring cells first (only their S, A, B are kept)
   const int nring = 2 * (T.TI + T.TJ);
   // 1a'. a strip's first ghost column inside a partial last tile: its fill
@@ -1090,14 +1135,15 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lns_step(StepParams P, LnsArrays a
 template <bool RES, int MODE, int TURB>
 __global__ __launch_bounds__(BLOCK) void hf2d_lns_step_fx(StepParams P, LnsArrays a, LeanTile T, DevScalars* sc,
                                                            int slot, int slot_next, int serial,
-                                                           ResidualPack* partials, FusedX X, ColList Lc) {
-  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc);
+                                                           ResidualPack* partials, FusedX X, ColList Lc,
+                                                           const ColList* Lg) {
+  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc, Lg);
 }
 template <bool RES, int MODE, int TURB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void hf2d_lns_step_fx3(
     StepParams P, LnsArrays a, LeanTile T, DevScalars* sc, int slot, int slot_next, int serial,
-    ResidualPack* partials, FusedX X, ColList Lc) {
-  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc);
+    ResidualPack* partials, FusedX X, ColList Lc, const ColList* Lg) {
+  lns_step_body<RES, MODE, TURB, true>(P, a, T, sc, slot, slot_next, serial, partials, 0, X, &Lc, Lg);
 }
 
 // Multi-workgroup mailbox exchange, push half (the mechanism step and every
@@ -1230,7 +1276,8 @@ template <bool RES, int TURB, bool STRIP = true>
 __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a, const LeanTile& T, DevScalars* sc,
                                               int slot, int slot_next, int serial, ResidualPack* partials) {
   extern __shared__ real lds[];
-  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), a.part, T);
+  const unsigned b = a.lg ? tile_edge_first(xcd_remap(blockIdx.x, gridDim.x), T)
+                          : tile_of_part(xcd_remap(blockIdx.x, gridDim.x), a.part, T);
   const LnmLayout L(T.TI, T.TJ, a.nsp - 1);
   // phase trace: wavefront 0 (slots 0..8) and the last wavefront (9, 10) of the workgroup
   unsigned long long* tr = a.tr ? a.tr + (long)b * 12 : nullptr;
@@ -1260,6 +1307,12 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
   const int ii = (int)threadIdx.x / T.TJ, jj = (int)threadIdx.x - ii * T.TJ;
   int skip = 0;
+  // 0. the previous step's halo from the mailbox into the ghost columns
+  if (a.lg) {
+    const FusedX& X = *a.xg;
+    const unsigned long long seq_prev = *X.seq;
+    if (seq_prev > 0) fx_ghost_prologue(P, X, a.lg, i0, j0, T.TI, T.TJ, seq_prev);
+  }
   // 1a. ring cells: S, A or B only (on the threads after the tile's cells when
   // they fit in the workgroup, else on the first ones as a second fill)
   const int nring = 2 * (T.TI + T.TJ), own = T.TI * T.TJ;
@@ -1857,7 +1910,8 @@ static const LnsK kLns[4][2][3] = {
     {{hf2d_lns_step<false, SK_SGT, 4>, hf2d_lns_step_occ<false, SK_SGT, 3, 4>, hf2d_lns_step_occ<false, SK_SGT, 5, 4>},
      {hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>, hf2d_lns_step<true, SK_SGT, 4>}}};
 
-using LnsFxK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*, FusedX, ColList);
+using LnsFxK = void (*)(StepParams, LnsArrays, LeanTile, DevScalars*, int, int, int, ResidualPack*, FusedX, ColList,
+                        const ColList*);
 // [laminar, k-eps, SST, SA][residual] (the default kernels' register budgets)
 static const LnsFxK kLnsFx[4][2] = {
     {hf2d_lns_step_fx<false, SK_SGL, 2>, hf2d_lns_step_fx<true, SK_SGL, 2>},
@@ -1962,6 +2016,14 @@ struct DeviceSolver::Impl {
   FusedX* fx_dev = nullptr;   // fx_device: the tile kernels' copy of fused_args()
   FusedX fx_dev_host{};
   bool fx_dev_valid = false;
+  // fused lean N-S / mechanism steps: the HALO_LNS list of the last fused
+  // step, whose halo is still in the mailbox (lns_ghost_pending), and device
+  // copies of the lists of both buffer parities (the next step's prologue)
+  ColList lns_pend{};
+  ColList* lc_dev = nullptr;
+  ColList lc_host[2]{};
+  bool lc_valid[2] = {false, false};
+  int lc_next = 0;
   ResidualPack* partials = nullptr;
   ResidualPack* res_out = nullptr;
   ResidualPack* res_host = nullptr;   // pinned
@@ -2236,6 +2298,8 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_SC_KERNEL")) impl->sc_kernel = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_HOST_TAIL")) host_tail = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_DT_READ")) dt_read_mode = std::atoi(e);
+  if (const char* e = std::getenv("HF2D_SKIP_SAME")) tile_skip_same = std::string(e) != "0";
+  if (const char* e = std::getenv("HF2D_GHOST_PROLOGUE")) lns_ghost_prologue = std::string(e) != "0";
   gi0 = gi0_;
   gi1 = gi1_ < 0 ? c.J.nx : gi1_;
   // ghost columns: N-S strips keep two (the lean N-S / mechanism tiles
@@ -3042,6 +3106,7 @@ void DeviceSolver::p2p_loopback(int rank, int nranks) {
   std::vector<double*> dr(nranks, (double*)(p.base + p.off_dtr));
   p.d_flags = m.mem.alloc<unsigned long long*>(nranks);
   p.d_dtr = m.mem.alloc<double*>(nranks);
+  if (!m.lc_dev) m.lc_dev = m.mem.alloc<ColList>(2);
   HIP_CHECK(hipMemcpy(p.d_flags, fl.data(), nranks * sizeof(void*), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(p.d_dtr, dr.data(), nranks * sizeof(void*), hipMemcpyHostToDevice));
   p.loop = true;
@@ -3117,6 +3182,7 @@ void DeviceSolver::p2p_import(const std::vector<std::string>& descs) {
   }
   p.d_flags = m.mem.alloc<unsigned long long*>(m.nranks);
   p.d_dtr = m.mem.alloc<double*>(m.nranks);
+  if (!m.lc_dev) m.lc_dev = m.mem.alloc<ColList>(2);   // (fused lean N-S ghost prologue lists)
   HIP_CHECK(hipDeviceSynchronize());
   HIP_CHECK(hipMemcpy(p.d_flags, fl.data(), m.nranks * sizeof(void*), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy(p.d_dtr, dr.data(), m.nranks * sizeof(void*), hipMemcpyHostToDevice));
@@ -3127,6 +3193,8 @@ bool DeviceSolver::p2p_active() const { return impl->p2p.on; }
 
 void DeviceSolver::p2p_set(bool on) {
   flush_pending();
+  p2p_complete();
+  lns_last_valid = false;
   if (on && (impl->p2p.peer_base.empty() || impl->nranks < 2)) throw std::runtime_error("p2p_set: no imported peers");
   impl->p2p.on = on;
   graph.reset();   // captured exchanges belong to the old transport
@@ -3259,6 +3327,7 @@ void DeviceSolver::halo_fields(int group, std::vector<real*>& f, std::vector<uns
 void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) {
   Impl& m = *impl;
   p2p_complete();
+  lns_last_valid = false;
   if ((!m.comm && !m.local && !m.p2p.on) || m.nranks == 1) return;
   const int ny = h.ny;
   std::vector<real*> fl;
@@ -3290,10 +3359,17 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     hipLaunchKernelGGL(hf2d_p2p_push, dim3(nbp), dim3(BLOCK), 0, st, L, first, last, ny, cnt, X, m.sc,
                        dt_slot >= 0 ? dt_slot : 0, dt_slot >= 0 ? 1 : 0, 1);
     HIP_CHECK(hipGetLastError());
+    p2p_mwg_exchanges++;
+    if (group == CpuSolver::HALO_LNS && dt_slot >= 0 && lns_ghost_prologue && !on_stream) {
+      // the mechanism step's halo: the next mechanism step's edge tiles
+      // unpack it (fx_ghost_prologue), any other consumer p2p_complete
+      m.lns_pend = L;
+      lns_ghost_pending = lns_last_valid = true;
+      return;
+    }
     hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
                        dim3(BLOCK), 0, st, L, l_off - 1, l_off + (gi1 - gi0), ny, cnt, X);
     HIP_CHECK(hipGetLastError());
-    p2p_mwg_exchanges++;
     return;
   }
   if (m.p2p.on) {
@@ -3529,6 +3605,37 @@ const FusedX* DeviceSolver::fx_device(const FusedX& X) {
   return m.fx_dev;
 }
 
+// Device copy of a HALO_LNS list for a fused step's ghost prologue (the two
+// buffer parities' lists are uploaded once, outside graph captures; nullptr
+// when a new list shows up inside a capture: that step unpacks separately)
+namespace {
+bool same_list(const ColList& a, const ColList& b) {   // (the entries only: padding bytes are unspecified)
+  if (a.nf != b.nf) return false;
+  for (int k = 0; k < a.nf; k++)
+    if (a.f[k] != b.f[k] || a.o[k] != b.o[k]) return false;
+  return true;
+}
+}  // namespace
+
+const ColList* DeviceSolver::lc_device(const ColList& L) {
+  Impl& m = *impl;
+  if (!m.lc_dev) return nullptr;   // (allocated by p2p_import)
+  for (int k = 0; k < 2; k++)
+    if (m.lc_valid[k] && same_list(m.lc_host[k], L)) return m.lc_dev + k;
+  // a slot is written once (a captured window may reference it); the two
+  // buffer parities' lists fill both, anything else unpacks separately
+  if (m.lc_next >= 2) return nullptr;
+  hipStreamCaptureStatus cs_ = hipStreamCaptureStatusNone;
+  HIP_CHECK(hipStreamIsCapturing(m.stream, &cs_));
+  if (cs_ != hipStreamCaptureStatusNone) return nullptr;
+  const int k = m.lc_next++;
+  m.lc_host[k] = L;
+  // stream-ordered from the persistent host copy: no host wait in the step
+  HIP_CHECK(hipMemcpyAsync(m.lc_dev + k, &m.lc_host[k], sizeof L, hipMemcpyHostToDevice, m.stream));
+  m.lc_valid[k] = true;
+  return m.lc_dev + k;
+}
+
 FusedX DeviceSolver::fused_args() const {
   const Impl& m = *impl;
   const Impl::P2P& p = m.p2p;
@@ -3555,10 +3662,19 @@ FusedX DeviceSolver::fused_args() const {
 
 // After fused-exchange steps the newest ghost columns and the peers' dt live
 // only in the mailbox: materialise them before any other consumer.
-void DeviceSolver::p2p_complete() {
+void DeviceSolver::p2p_complete(bool keep_lns) {
+  Impl& m = *impl;
+  if (lns_ghost_pending && !keep_lns) {
+    // the last fused lean N-S / mechanism step's halo: mailbox -> ghost columns
+    lns_ghost_pending = false;
+    const ColList& Lc = m.lns_pend;
+    const int cnt = Lc.nf * h.ny;
+    hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
+                       dim3(BLOCK), 0, m.stream, Lc, l_off - 1, l_off + (gi1 - gi0), h.ny, cnt, fused_args());
+    HIP_CHECK(hipGetLastError());
+  }
   if (!fx_pending) return;
   fx_pending = false;
-  Impl& m = *impl;
   const long N = h.N;
   ColList L;
   L.nf = 0;
@@ -3602,6 +3718,11 @@ uint64_t graph_signature(const StepParams& P, uint64_t mode) {
 struct DeviceSolver::GraphCache {
   hipGraphExec_t exec = nullptr;
   uint64_t sig = 0;
+  // fused lean N-S windows: the first step unpacks the previous step's halo
+  // in its prologue (needs the mailbox to hold an lns list's publication at
+  // replay), and the window ends with its last step's halo pending
+  bool lns_pro = false, lns_end = false;
+  ColList lns_end_list{};
   ~GraphCache() {
     if (exec) (void)hipGraphExecDestroy(exec);
   }
@@ -3659,7 +3780,16 @@ void DeviceSolver::run_graph() {
   }
   if (!graph) graph.reset(new GraphCache);
   if (graph->exec && graph->sig == sig) {
+    if (graph->lns_pro && !lns_last_valid) {   // (the mailbox holds another exchange's layout)
+      flush_pending();
+      return;
+    }
+    if (!graph->lns_pro) p2p_complete();
     HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
+    if (graph->lns_end) {
+      m.lns_pend = graph->lns_end_list;
+      lns_ghost_pending = lns_last_valid = true;
+    }
     dt_word_valid = false;   // (conservative: the next eager step reads the shards too)
     nstep += GRAPH_STEPS;   // ping-pong parities are unchanged after an even number of steps
     pending.clear();
@@ -3674,10 +3804,17 @@ void DeviceSolver::run_graph() {
   hipGraph_t g = nullptr;
   // (a replayed window may follow any launch: its first step reads the shards)
   dt_word_valid = false;
+  const bool s_pend = lns_ghost_pending, s_valid = lns_last_valid;
+  const ColList s_list = m.lns_pend;
+  bool first_pro = false;
   bool ok = hipStreamBeginCapture(m.stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
   if (ok) {
     try {
-      for (const StepParams& p : q) do_step_eager(p, false);
+      for (size_t k = 0; k < q.size(); k++) {
+        lns_pro_uses = 0;
+        do_step_eager(q[k], false);
+        if (k == 0) first_pro = lns_pro_uses > 0;
+      }
     } catch (const std::exception&) {
       ok = false;
     }
@@ -3700,12 +3837,18 @@ void DeviceSolver::run_graph() {
   lean_state = ls;
   if (!ok) {
     use_graph = false;   // eager from now on
+    lns_ghost_pending = s_pend;   // (nothing of the capture ran)
+    lns_last_valid = s_valid;
+    m.lns_pend = s_list;
     for (const StepParams& p : q) do_step_eager(p, false);
     return;
   }
   if (graph->exec) (void)hipGraphExecDestroy(graph->exec);
   graph->exec = exec;
   graph->sig = sig;
+  graph->lns_pro = first_pro;
+  graph->lns_end = lns_ghost_pending && lns_last_valid;
+  graph->lns_end_list = m.lns_pend;
   HIP_CHECK(hipGraphLaunch(graph->exec, m.stream));
   nstep += GRAPH_STEPS;
   graph_launches++;
@@ -3878,8 +4021,21 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
     a.hot = m.chem_list;
     a.hot_n = &m.sc->hot_cnt[slot];
     a.part = 0;
+    // mailboxes: the previous step's halo (pushed after its state kernel,
+    // exchange()) is unpacked by this step's edge tiles (fx_ghost_prologue)
+    if (m.p2p.on && p2p_fuse && m.nranks > 1 && lns_prev_valid && lns_ghost_prologue) {
+      a.lg = lc_device(m.lns_pend);
+      if (a.lg) {
+        a.xg = fx_device(fused_args());
+        lns_ghost_pending = false;
+        lns_pro_uses++;
+        lns_prologue_steps++;
+      }
+    }
+    p2p_complete();
     lnm_launch(P, a, T, want_res, slot, slot_next, serial, (unsigned)(T.nbi * T.nbj));
   } else {
+    p2p_complete();
     if (!m.comm_stream) {
       HIP_CHECK(hipStreamCreateWithFlags(&m.comm_stream, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&m.ev_edge, hipEventDisableTiming));
@@ -4046,11 +4202,21 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
   // the slot's word holds the MIN only right after a folding tile launch
   const bool dt_word_ok = dt_word_valid;
   dt_word_valid = false;
+  // the mailbox holds a fused lean N-S step's halo (list m.lns_pend) only
+  // right after such a step (every other step or exchange publishes another
+  // layout or nothing)
+  lns_prev_valid = lns_last_valid;
+  lns_last_valid = false;
   const bool tile_path = euler && lean && lean_ok && lean_tile &&
                          lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ;
-  if (!tile_path) p2p_complete();
+  // (a fused lean N-S step unpacks the previous fused step's halo itself)
+  const bool lns_fx_next = !euler && (lnm_step_ok(P) || lns_step_ok(P)) && lns_state == 1 && lean_state == 0 &&
+                           m.p2p.on && p2p_fuse && m.nranks > 1;
+  if (!tile_path) p2p_complete(lns_fx_next);
   if (euler && lean && lean_ok && lean_tile && lean_state == 1 && P.ny >= LEAN_TILE_MIN_TJ) {
     LeanSoA L = m.lean_view(h, sbuf, abuf, dsbuf, pbuf, false);
+    P.skip_same = tile_skip_same ? 1 : 0;
+    P.dt_read = dt_read_mode == 1 ? 1 : 0;
     // two cells per thread unless that leaves fewer than ~2 workgroups per CU
     // (small strips of a multi-GPU run)
     // (256-thread tiles only: the small-workgroup geometries are explicit
@@ -4138,10 +4304,16 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
     if (tile_trace && var == 0 && !fx_step)
       hipLaunchKernelGGL(nt == BLOCK ? kTileTr[sg][cpt - 1] : kTileTrNt[nts][cpt - 1], dim3(ntile), dim3(nt), shmem,
                          st, P, L, T, m.sc, slot, slot_next, serial, m.partials, tile_trace);
-    else if (fx_step)
+    else if (fx_step) {
+      // the fused tail folds every rank's dt into the next slot's word
+      // (fx_tail): the next fused step reads that one word (not when the
+      // fold is deferred, lagged dt)
+      const bool word = dt_read_mode >= 1 && !X.defer;
+      if (word && dt_word_ok) P.dt_read = 2;
       hipLaunchKernelGGL(nt == BLOCK ? kTileFx[sg][cpt - 1][var] : kTileFxNt[nts][cpt - 1][var], dim3(ntile),
                          dim3(nt), shmem, st, P, L, T, m.sc, slot, slot_next, serial, m.partials, fx_device(X));
-    else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace && nt == BLOCK)
+      dt_word_valid = word;
+    } else if (sg && cpt == 1 && var == 0 && lean_occ == 6 && !tile_trace && nt == BLOCK)
       hipLaunchKernelGGL((hf2d_lean_tile_occ<false, false, true, 6>), dim3(ntile), dim3(BLOCK), shmem, st, P, L, T,
                          m.sc, slot, slot_next, serial, m.partials);
     // (multi-gas, one cell per thread, at a 5-wave register budget -- 96
@@ -4276,12 +4448,28 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
                   cs.cfg.isAdiabaticWall;
       const bool lparts = T.nbi >= 2 + T.ne;
       if (lns_fx) {
+        // the previous fused step's halo is still in the mailbox: this
+        // kernel's edge tiles copy it into the ghost columns they read
+        // (fx_ghost_prologue) instead of a separate unpack launch
+        // (valid whenever the mailbox's last publication was a fused lean
+        // N-S step: its parity stays untouched until this step publishes,
+        // so the copy is exact even if p2p_complete already unpacked it)
+        const ColList* Lg = nullptr;
+        if (lns_prev_valid && lns_ghost_prologue) {
+          Lg = lc_device(m.lns_pend);
+          if (Lg) {
+            lns_ghost_pending = false;
+            lns_pro_uses++;
+            lns_prologue_steps++;
+          }
+        }
+        p2p_complete();   // (a list new inside a capture: the separate unpack)
         hipLaunchKernelGGL(kLnsFx[tv][want_res ? 1 : 0], dim3(ntile), dim3(BLOCK), shmem, st, P, a, T, m.sc, slot,
-                           slot_next, serial, m.partials, fused_args(), Lc);
+                           slot_next, serial, m.partials, fused_args(), Lc, Lg);
         HIP_CHECK(hipGetLastError());
-        const int cnt = Lc.nf * h.ny;
-        hipLaunchKernelGGL(hf2d_p2p_unpack, dim3((unsigned)std::max(1, std::min((2 * cnt + BLOCK - 1) / BLOCK, 1024))),
-                           dim3(BLOCK), 0, st, Lc, l_off - 1, l_off + (gi1 - gi0), h.ny, cnt, fused_args());
+        m.lns_pend = Lc;
+        lns_ghost_pending = lns_last_valid = true;   // unpacked by the next fused step or p2p_complete
+        if (lns_ghost_prologue) (void)lc_device(Lc);   // (uploaded now, outside any capture, when eager)
         ghost_stale = true;   // lean representation in the ghosts
         lns_fx_steps++;
       } else if (lns_split) {

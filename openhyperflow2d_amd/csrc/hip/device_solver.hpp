@@ -124,14 +124,22 @@ class DeviceSolver : public SolverBase {
   void p2p_loopback(int rank, int nranks);
   bool p2p_active() const;
   bool p2p_fuse = false;     // fold the p2p exchange into the lean tile kernel (hf2d_lean_tile_fx)
-  bool p2p_queue_check = true;
+  bool p2p_queue_check = true;   // p2p_import refuses more in-process ranks than HIP hardware queues allow
   // lean tile dt read (StepParams::dt_read / dt_fold; HF2D_DT_READ): 0 word +
   // shards by scalar loads, 1 by one vector load per lane, 2 the previous
   // step's last workgroup folds them into the word (single GPU)
   int dt_read_mode = 1;
-  bool dt_word_valid = false;   // p2p_import refuses more in-process ranks than HIP hardware queues allow
+  bool dt_word_valid = false;
+  // lean tile: skip stores of beta / CP whose bits did not change (HF2D_SKIP_SAME)
+  bool tile_skip_same = false;
   bool fx_step = false, fx_pending = false;
-  void p2p_complete();
+  // fused lean N-S steps: the last step's halo is still in the mailbox; the
+  // next fused step's edge tiles unpack it (lns_ghost_prologue, HF2D_GHOST_PROLOGUE)
+  bool lns_ghost_pending = false, lns_ghost_prologue = true, lns_last_valid = false, lns_prev_valid = false;
+  int lns_pro_uses = 0;
+  long lns_prologue_steps = 0;   // fused lean N-S steps that unpacked the previous halo themselves
+  const struct ColList* lc_device(const struct ColList& L);
+  void p2p_complete(bool keep_lns = false);
   struct FusedX fused_args() const;
   const struct FusedX* fx_device(const struct FusedX& X);
   void p2p_set(bool on);   // off: fall back to RCCL/local; on: only after p2p_import

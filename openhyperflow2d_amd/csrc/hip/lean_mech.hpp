@@ -79,6 +79,11 @@ struct LnmArrays {
   unsigned* hot_n = nullptr;   // ... and their count (DevScalars::hot_cnt / hot_cnt2 of the slot)
   int part = 0;   // tiles of this launch: 0 all, 1 the strip's edge tile columns, 2 the others (comm overlap)
   unsigned long long* tr = nullptr;   // phase trace (HF2D_LNM_TRACE): 12 clocks per workgroup
+  // xGMI mailboxes: the previous step's HALO_LNS list (lg) and the exchange
+  // arguments (xg, device copies): the edge tiles copy that step's halo from
+  // the mailbox into the ghost columns first (fx_ghost_prologue)
+  const struct FusedX* xg = nullptr;
+  const struct ColList* lg = nullptr;
 };
 
 // Tile of the lean mechanism step: TI columns x LNM_TILE rows, one cell per
