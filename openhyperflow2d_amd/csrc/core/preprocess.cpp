@@ -441,7 +441,7 @@ void Field::resize_window(int X, int Y, int a, int b) {
   i0 = a;
   nxl = std::max(b - a, 0);
   c.assign((size_t)nxl * Y, CellRecord{});
-  std::memset((void*)c.data(), 0, c.size() * sizeof(CellRecord));
+  if (!c.empty()) std::memset((void*)c.data(), 0, c.size() * sizeof(CellRecord));
   g.assign((size_t)X * Y, CellFlags{});
 }
 

@@ -418,6 +418,7 @@ void SolverBase::merge_wall_uw(const std::vector<int32_t>& slots, const std::vec
     const size_t n = b.size() / (sizeof(int32_t) + sizeof(real));
     std::vector<int32_t> sl(n);
     std::vector<real> v(n);
+    if (n == 0) continue;
     std::memcpy(sl.data(), b.data(), n * sizeof(int32_t));
     std::memcpy(v.data(), b.data() + n * sizeof(int32_t), n * sizeof(real));
     take(sl.data(), v.data(), n);

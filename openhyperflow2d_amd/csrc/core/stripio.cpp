@@ -235,7 +235,7 @@ void strip_heat_flux_y(Comm& comm, const std::string& path, const Case& cs, cons
         comm.allgather_bytes(std::string((const char*)jq.data(), jq.size() * sizeof(real)));
     for (const std::string& s : all) {
       std::vector<real> t(s.size() / sizeof(real));
-      std::memcpy(t.data(), s.data(), t.size() * sizeof(real));
+      if (!t.empty()) std::memcpy(t.data(), s.data(), t.size() * sizeof(real));
       fold_heat_flux_y(Q, t);
     }
   }
