@@ -1081,16 +1081,26 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     }
   }
   if (FX && mine) {
-    // an edge cell's new HALO_LNS values (its own stores above, read back
-    // after they completed) -> the neighbour's mailbox of parity seq_prev + 1
+    // an edge cell's new HALO_LNS values (its own stores above, read back:
+    // a thread's load after its own store to the address returns that store)
+    // -> the neighbour's mailbox of parity seq_prev + 1, in batches of 8
+    // independent loads then 8 stores (one load per store in turn cost a
+    // memory latency per field, ~20-40 of them per edge cell)
     const int pn = (int)((seq_prev + 1) & 1);
+    constexpr int PB = 8;
     for (int side = 0; side < 2; side++) {
       const int o = side == 0 ? i - P.i0 : P.i1 - 1 - i;
       if (!(X.sides & (1 << side)) || o > 1) continue;
-      vm_drain();
       real* mb = side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap;
-      for (int f = 0; f < Lc->nf; f++)
-        if (Lc->o[f] == o) p2p_store(mb + (long)f * P.ny + j, Lc->f[f][idx]);
+      const int nf = Lc->nf;
+      for (int f0 = 0; f0 < nf; f0 += PB) {
+        real v[PB];
+#pragma unroll
+        for (int u = 0; u < PB; u++) v[u] = (f0 + u < nf && Lc->o[f0 + u] == o) ? Lc->f[f0 + u][idx] : 0.0;
+#pragma unroll
+        for (int u = 0; u < PB; u++)
+          if (f0 + u < nf && Lc->o[f0 + u] == o) p2p_store(mb + (long)(f0 + u) * P.ny + j, v[u]);
+      }
       vm_drain();
     }
   }
