@@ -905,6 +905,52 @@ __device__ inline void fx_ghost_prologue(const StepParams& P, const FusedX& X, c
   __syncthreads();
 }
 
+// Edge push of a fused lean N-S step, by every thread of an edge tile after
+// the tile's barrier: the HALO_LNS values of the tile's cells in the strip's
+// first / last two columns (entry f of Lc at column P.i0 + o[f] / P.i1 - 1 -
+// o[f], stored by their owner threads before the barrier) -> the neighbour's
+// mailbox of parity seq_prev + 1, K independent loads then K stores per
+// thread; drained, then a barrier, so the tail counts a workgroup whose
+// mailbox stores have completed.  (The owner threads pushing their own
+// cells -- one column of 20 threads per offset, ~20 fields each -- kept the
+// edge tiles, the last to finish in a one-round grid, ~4.6 us longer on the
+// resonator's 4-rank strip, tools/exchange_loopback.py.)
+__device__ inline void fx_edge_push(const StepParams& P, const FusedX& X, const ColList* Lc, const LeanTile& T, int i0,
+                                    int j0, unsigned long long seq_prev) {
+  const bool el = (X.sides & 1) && i0 <= P.i0 + 1;
+  const bool er = (X.sides & 2) && i0 + T.TI >= P.i1 - 1;
+  if (!el && !er) return;   // (uniform over the workgroup)
+  const int pn = (int)((seq_prev + 1) & 1);
+  const int jhi = j0 + T.TJ < P.ny ? j0 + T.TJ : P.ny, rows = jhi - j0, nf = Lc->nf;
+  const int per = nf * rows, total = (el && er ? 2 : 1) * per;
+  constexpr int K = 4;
+  for (int base = (int)threadIdx.x; base < total; base += K * BLOCK) {
+    real v[K];
+    real* dst[K];
+#pragma unroll
+    for (int u = 0; u < K; u++) {
+      const int t = base + u * BLOCK;
+      dst[u] = nullptr;
+      v[u] = 0.0;
+      if (t < total) {
+        const int side = (el && er) ? t / per : (el ? 0 : 1);
+        const int tt = (el && er) ? t - side * per : t, f = tt / rows, j = j0 + (tt - f * rows), o = Lc->o[f];
+        const int col = side == 0 ? P.i0 + o : P.i1 - 1 - o;
+        if (col >= i0 && col < i0 + T.TI && col >= P.i0 && col < P.i1) {
+          dst[u] = (side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap) +
+                   (long)f * P.ny + j;
+          v[u] = Lc->f[f][(long)col * P.ny + j];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < K; u++)
+      if (dst[u]) p2p_store(dst[u], v[u]);
+  }
+  vm_drain();
+  __syncthreads();
+}
+
 // FX: the multi-GPU exchange fused in (xGMI mailboxes): the cells of the
 // strip's first / last two columns store this step's HALO_LNS values (Lc:
 // the post-step pointers, DeviceSolver::halo_list) into the neighbour's
@@ -944,7 +990,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   const bool mine = lean_tile_cell(P, T, (int)b, (int)threadIdx.x, &i, &j, &c, &i0, &j0);
   int dummy = 0, skip = 0;
   // 0. the previous fused step's halo from the mailbox into the ghost columns
-  if (FX && Lg != nullptr && seq_prev > 0) fx_ghost_prologue(P, X, Lg, i0, j0, T.TI, T.TJ, seq_prev);
+  if (FX && Lg != nullptr && seq_prev > 0 && !(X.skip & 4)) fx_ghost_prologue(P, X, Lg, i0, j0, T.TI, T.TJ, seq_prev);
   // 1a. ring cells first (only their S, A, B are kept)
   const int nring = 2 * (T.TI + T.TJ);
   // 1a'. a strip's first ghost column inside a partial last tile: its fill
@@ -1080,30 +1126,6 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
                                                          &f2);
     }
   }
-  if (FX && mine) {
-    // an edge cell's new HALO_LNS values (its own stores above, read back:
-    // a thread's load after its own store to the address returns that store)
-    // -> the neighbour's mailbox of parity seq_prev + 1, in batches of 8
-    // independent loads then 8 stores (one load per store in turn cost a
-    // memory latency per field, ~20-40 of them per edge cell)
-    const int pn = (int)((seq_prev + 1) & 1);
-    constexpr int PB = 8;
-    for (int side = 0; side < 2; side++) {
-      const int o = side == 0 ? i - P.i0 : P.i1 - 1 - i;
-      if (!(X.sides & (1 << side)) || o > 1) continue;
-      real* mb = side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap;
-      const int nf = Lc->nf;
-      for (int f0 = 0; f0 < nf; f0 += PB) {
-        real v[PB];
-#pragma unroll
-        for (int u = 0; u < PB; u++) v[u] = (f0 + u < nf && Lc->o[f0 + u] == o) ? Lc->f[f0 + u][idx] : 0.0;
-#pragma unroll
-        for (int u = 0; u < PB; u++)
-          if (f0 + u < nf && Lc->o[f0 + u] == o) p2p_store(mb + (long)(f0 + u) * P.ny + j, v[u]);
-      }
-      vm_drain();
-    }
-  }
   if (RES) {
 #pragma unroll
     for (int off = 1; off < WAVE; off <<= 1) shfl_merge(r, off);
@@ -1121,10 +1143,11 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
     if (serial) m = fmin(m, P.dt);
     dt_min(sc, slot_next, m);
   }
+  if (FX && !(X.skip & 2)) fx_edge_push(P, X, Lc, T, i0, j0, seq_prev);
   // (unpacking the peers' halo in this last workgroup instead of a separate
   // hf2d_p2p_unpack launch measured 2x the exchange cost: one workgroup's
   // serial rounds of uncached mailbox loads, profiles/exchange_loopback_r05.md)
-  if (FX && threadIdx.x < WAVE) fx_tail(X, sc, slot_next, seq_prev);
+  if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev);
 }
 
 // (LnsArrays by value: passed by device pointer instead, the k-eps

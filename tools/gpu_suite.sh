@@ -21,7 +21,7 @@ mode=${1:-all}
 shift || true
 
 run_tests() {
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_gpu.log 2>&1 &&
   timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 }
