@@ -1192,11 +1192,14 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
   const unsigned long long seq_prev = *X.seq;
   const int pn = (int)((seq_prev + 1) & 1);
   constexpr int PER = 16;
-  const long base = ((long)blockIdx.x * BLOCK + threadIdx.x) * PER;
+  // value u of a thread: base + u * BLOCK (consecutive lanes, consecutive
+  // addresses: with PER consecutive values per thread every load and mailbox
+  // store instruction touched 64 different lines)
+  const long base = (long)blockIdx.x * BLOCK * PER + threadIdx.x;
   real v[PER];
 #pragma unroll
   for (int u = 0; u < PER; u++) {
-    const long t = base + u;
+    const long t = base + (long)u * BLOCK;
     if (t < 2L * cnt) {
       const int side = t < cnt ? 0 : 1;
       const int tt = (int)(t - (long)side * cnt), f = tt / ny, j = tt - f * ny;
@@ -1206,7 +1209,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
   }
 #pragma unroll
   for (int u = 0; u < PER; u++) {
-    const long t = base + u;
+    const long t = base + (long)u * BLOCK;
     if (t < 2L * cnt) {
       const int side = t < cnt ? 0 : 1;
       const int tt = (int)(t - (long)side * cnt);
