@@ -773,6 +773,15 @@ PYBIND11_MODULE(_hf2d, m) {
              for (const auto& b : d) v.push_back(std::string(b));
              s.p2p_import(v);
            })
+      .def("fx_trace",
+           [](DeviceSolver& s) {
+             std::vector<unsigned long long> v;
+             {
+               py::gil_scoped_release nogil;
+               v = s.fx_trace();
+             }
+             return v;
+           })
       .def("p2p_probe",
            [](DeviceSolver& s) {
              std::string b;

@@ -369,7 +369,13 @@ __device__ inline void p2p_store(double* p, double v) {
 // have completed: the ordering point for the relaxed system-coherent stores
 __device__ inline void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+__device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memrealtime(); }
 constexpr int FX_DONE_STRIDE = 32;   // completion counters on lines of their own
+// tail phase trace (HF2D_FX_SKIP bit 4, loopback timing runs only): after the
+// counters, FX_TRACE_N records of FX_TRACE_W clocks, one per step (seq mod N)
+constexpr int FX_TRACE_N = 64, FX_TRACE_W = 8;
+constexpr unsigned FX_COUNT1_MAX = 512;
+constexpr int FX_DONE_WORDS = (DT_SHARDS + 1) * FX_DONE_STRIDE + 2 * FX_TRACE_N * FX_TRACE_W;
 struct FusedX {
   real* peer_recv_l;   // left neighbour's mailbox recv base (we are its right side)
   real* peer_recv_r;
@@ -387,9 +393,20 @@ struct FusedX {
   // hf2d_p2p_complete
   int defer;
   // cost attribution of the fused exchange (HF2D_FX_SKIP, timing only, wrong
-  // results): bit 0 no tail, bit 1 no edge pushes, bit 2 ghosts staged from
-  // the state arrays instead of the mailbox
+  // results): bit 0 no tail, bit 1 no edge pushes / mailbox stores, bit 2
+  // ghosts staged from the state arrays instead of the mailbox (no ghost
+  // prologue), bit 3 no loads of the push kernel
   int skip;
+  int edge_first;   // inviscid fused tile kernel: edge tile columns dispatched first (HF2D_FX_EDGE_FIRST)
+  // tail completion count: one per dt shard + one for the shards, or one
+  // counter where the caller asks for it (fused lean N-S kernel, grids of <=
+  // FX_COUNT1_MAX workgroups); HF2D_FX_COUNT1 = 1 / 2 forces one / two levels.
+  // Loopback tail trace: the resonator's 4-rank strip (420 workgroups that
+  // finish spread out) 0.96 -> 0.52 us of counting and 4.4 -> 3.4 us of
+  // exchange with one counter; workgroups that finish together contend on it:
+  // the headline's 8-rank strip (719 single-wave workgroups) 5.5 -> 11.7 us,
+  // the scramjet's push kernel (135) 1.5 - 1.7 us of counting
+  int count1;
 };
 
 // Peer waits and publications are spread over the lanes of one wavefront:
@@ -446,16 +463,26 @@ __device__ inline bool p2p_wait_all(const FusedX& x, unsigned long long target, 
 // slot the next step reads.
 // Returns true (every lane) in the last workgroup, after the wait.
 __device__ __forceinline__ bool fx_tail(const FusedX& X, DevScalars* sc, int slot_next,
-                                        unsigned long long seq_prev, bool fold = true) {
+                                        unsigned long long seq_prev, bool fold = true, bool one_level = false) {
   const int lane = (int)(threadIdx.x & (WAVE - 1));
+  const bool trace = (X.skip & 16) != 0;
+  unsigned long long c[FX_TRACE_W] = {};
+  if (trace) c[0] = rt_clock();
   // the workgroup barrier drained every wave's mailbox stores; drain lane
   // 0's dt atomic before counting this workgroup as done
   vm_drain();
+  if (trace) c[1] = rt_clock();
   // completion count in two levels (one counter per dt shard, then one for
   // the shards): a single counter serialises every workgroup's returning
   // atomic at the memory side
   int last = 0;
-  if (lane == 0) {
+  if (lane == 0 && (X.count1 == 1 || (X.count1 == 0 && one_level))) {
+    unsigned* ct = X.done + DT_SHARDS * FX_DONE_STRIDE;
+    if (__hip_atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(ct, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = 1;
+    }
+  } else if (lane == 0) {
     const unsigned G = gridDim.x, sh = blockIdx.x % DT_SHARDS;
     const unsigned pop = (G - sh + DT_SHARDS - 1) / DT_SHARDS, nsh = G < DT_SHARDS ? G : DT_SHARDS;
     unsigned* cs = X.done + sh * FX_DONE_STRIDE;
@@ -469,6 +496,7 @@ __device__ __forceinline__ bool fx_tail(const FusedX& X, DevScalars* sc, int slo
     }
   }
   if (!__shfl(last, 0, WAVE)) return false;
+  if (trace) c[2] = rt_clock();
   // last workgroup: this rank's dt (word + shards, one per lane), published
   // to every peer (one peer per lane), then the flags, then the peers'
   const unsigned long long sn = seq_prev + 1;
@@ -478,21 +506,33 @@ __device__ __forceinline__ bool fx_tail(const FusedX& X, DevScalars* sc, int slo
     b = __hip_atomic_load(&sc->dt_sh[slot_next][lane][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lane == DT_SHARDS) b = __hip_atomic_load(&sc->dt_bits[slot_next], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double d = wave_min(b == ~0ull ? 1.0 : bits_to_d(b));
+  if (trace) c[3] = rt_clock();
   for (int q = lane; q < X.nranks; q += WAVE)
     if (q != X.rank) p2p_store(X.peer_dtr[q] + pn * X.nranks + X.rank, d);
   vm_drain();   // (the wavefront's stores: every lane's)
+  if (trace) c[4] = rt_clock();
   for (int q = lane; q < X.nranks; q += WAVE)
     if (q != X.rank) __hip_atomic_store(&X.peer_flags[q][X.rank], sn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (trace) c[5] = rt_clock();
   const bool defer = X.defer != 0;
   const int r = X.rank;
   bool ok;
   const double peers = p2p_wait_wave(X, sn, sc, [=](int q) { return !defer || q == r - 1 || q == r + 1; },
                                      fold && !defer, pn, &ok);
   d = fmin(d, peers);
+  if (trace) c[6] = rt_clock();
   if (lane == 0) {
     if (fold && !defer && ok)
       __hip_atomic_store(&sc->dt_bits[slot_next], d_to_bits(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *X.seq = sn;
+    if (trace) {
+      vm_drain();
+      c[7] = rt_clock();
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(X.done + (DT_SHARDS + 1) * FX_DONE_STRIDE) +
+                              (long)(sn % FX_TRACE_N) * FX_TRACE_W;
+#pragma unroll
+      for (int k = 0; k < FX_TRACE_W; k++) o[k] = c[k];
+    }
   }
   return true;
 }
@@ -559,7 +599,6 @@ constexpr int TILE_TRACE_WORDS = 8;
 #define HF2D_TILE_STAGGER 1
 #endif
 constexpr int LDS_PER_CU = 160 * 1024;
-__device__ inline unsigned long long rt_clock() { return __builtin_amdgcn_s_memrealtime(); }
 
 // part: 0 every tile; 1 the tiles of the strip's first and last tile column
 // (their results feed the halo exchange); 2 the other tiles.  The grid of a
@@ -612,7 +651,10 @@ __device__ __forceinline__ void lean_tile_body(StepParams& P, const LeanSoA& L, 
       while (rt_clock() - t0 < d) __builtin_amdgcn_s_sleep(2);
     }
   }
-  const unsigned b = tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
+  // (fused exchange: the strip's edge tile columns first -- they push the
+  // halo and stage the ghost columns from the mailbox)
+  const unsigned b = (FX && X.edge_first) ? tile_edge_first(xcd_remap(blockIdx.x, gridDim.x), T)
+                                          : tile_of_part(xcd_remap(blockIdx.x, gridDim.x), part, T);
   unsigned long long seq_prev = 0;
   if (FX) seq_prev = *X.seq;
   apply_dt(P, sc, slot, true);
@@ -1147,7 +1189,7 @@ __device__ __forceinline__ void lns_step_body(StepParams& P, const LnsArrays& a,
   // (unpacking the peers' halo in this last workgroup instead of a separate
   // hf2d_p2p_unpack launch measured 2x the exchange cost: one workgroup's
   // serial rounds of uncached mailbox loads, profiles/exchange_loopback_r05.md)
-  if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev);
+  if (FX && threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, slot_next, seq_prev, true, gridDim.x <= FX_COUNT1_MAX);
 }
 
 // (LnsArrays by value: passed by device pointer instead, the k-eps
@@ -1187,11 +1229,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(3))) void
 // publish = 0: the pushes only (drained); a later hf2d_p2p_finish publishes
 // the step -- the mechanism step pushes its edge tiles' halo before its
 // interior tiles run.
+template <int PER>
 __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, int last, int ny, int cnt, FusedX X,
                                                       DevScalars* sc, int dslot, int fold, int publish) {
   const unsigned long long seq_prev = *X.seq;
   const int pn = (int)((seq_prev + 1) & 1);
-  constexpr int PER = 16;
   // value u of a thread: base + u * BLOCK (consecutive lanes, consecutive
   // addresses: with PER consecutive values per thread every load and mailbox
   // store instruction touched 64 different lines)
@@ -1203,7 +1245,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
     if (t < 2L * cnt) {
       const int side = t < cnt ? 0 : 1;
       const int tt = (int)(t - (long)side * cnt), f = tt / ny, j = tt - f * ny;
-      if (X.sides & (1 << side))
+      if ((X.sides & (1 << side)) && !(X.skip & 8))
         v[u] = Lc.f[f][(long)(side == 0 ? first + Lc.o[f] : last - Lc.o[f]) * ny + j];
     }
   }
@@ -1214,7 +1256,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
       const int side = t < cnt ? 0 : 1;
       const int tt = (int)(t - (long)side * cnt);
       // the left neighbour receives "from right", the right one "from left"
-      if (X.sides & (1 << side))
+      if ((X.sides & (1 << side)) && !(X.skip & 2))
         p2p_store((side == 0 ? X.peer_recv_l + ((long)pn * 2 + 1) * X.cap : X.peer_recv_r + ((long)pn * 2) * X.cap) +
                       tt,
                   v[u]);
@@ -1223,7 +1265,21 @@ __global__ __launch_bounds__(BLOCK) void hf2d_p2p_push(ColList Lc, int first, in
   vm_drain();
   if (!publish) return;
   __syncthreads();
-  if (threadIdx.x < WAVE) fx_tail(X, sc, dslot, seq_prev, fold != 0);
+  if (threadIdx.x < WAVE && !(X.skip & 1)) fx_tail(X, sc, dslot, seq_prev, fold != 0);
+}
+
+using PushK = void (*)(ColList, int, int, int, int, FusedX, DevScalars*, int, int, int);
+// values per thread of the push kernel (HF2D_PUSH_PER: 1, 4 or 16) and its
+// grid: one value per thread (135 workgroups on the scramjet's 8-rank strip)
+// pushed the 43-field mechanism halo in 7.0 us against 15.4 us with 16 values
+// per thread on 9 workgroups (rocprofv3 kernel trace of tools/exchange_loopback.py;
+// loopback exchange 18.7 -> 8.2 us)
+inline PushK push_kernel(int per) {
+  return per == 16 ? hf2d_p2p_push<16> : per == 4 ? hf2d_p2p_push<4> : hf2d_p2p_push<1>;
+}
+inline unsigned push_grid(int per, int cnt) {
+  const int p = per == 16 || per == 4 ? per : 1;
+  return (unsigned)std::max(1, (2 * cnt + BLOCK * p - 1) / (BLOCK * p));
 }
 
 // One workgroup: publish the step whose halo an earlier hf2d_p2p_push
@@ -1347,7 +1403,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
   if (a.lg) {
     const FusedX& X = *a.xg;
     const unsigned long long seq_prev = *X.seq;
-    if (seq_prev > 0) fx_ghost_prologue(P, X, a.lg, i0, j0, T.TI, T.TJ, seq_prev);
+    if (seq_prev > 0 && !(X.skip & 4)) fx_ghost_prologue(P, X, a.lg, i0, j0, T.TI, T.TJ, seq_prev);
   }
   // 1a. ring cells: S, A or B only (on the threads after the tile's cells when
   // they fit in the workgroup, else on the first ones as a second fill)
@@ -2330,6 +2386,7 @@ DeviceSolver::DeviceSolver(Case& c, int device, int gi0_, int gi1_) : SolverBase
   if (const char* e = std::getenv("HF2D_CHEM_KERNEL")) chem_kernel = std::atoi(e);   // 1 compiled 2 MFMA 3 generic 4 hiprtc
   if (const char* e = std::getenv("HF2D_GRAD_EVERY")) grad_every = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_LNM_TI")) lnm_ti = std::atoi(e);
+  if (const char* e = std::getenv("HF2D_PUSH_PER")) push_per = std::atoi(e);
   if (const char* e = std::getenv("HF2D_STAGGER")) tile_stagger = std::atoi(e);
   if (const char* e = std::getenv("HF2D_SC_KERNEL")) impl->sc_kernel = std::string(e) != "0";
   if (const char* e = std::getenv("HF2D_HOST_TAIL")) host_tail = std::string(e) != "0";
@@ -3101,7 +3158,7 @@ std::string DeviceSolver::p2p_export(int rank, int nranks) {
   p.base = (char*)b;
   HIP_CHECK(hipMemset(p.base, 0, p.bytes));
   p.seq = m.mem.alloc<unsigned long long>(1);
-  p.done = m.mem.alloc<unsigned>((DT_SHARDS + 1) * FX_DONE_STRIDE);
+  p.done = m.mem.alloc<unsigned>(FX_DONE_WORDS);
   HIP_CHECK(hipDeviceSynchronize());
   P2PDesc d{};
   d.magic = P2P_MAGIC;
@@ -3391,8 +3448,8 @@ void DeviceSolver::exchange(int group, int dt_slot, void* on_stream, bool full) 
     // 23-43-field N-S / mechanism halos on the step's critical path
     if (L.nf * ny > m.halo_cap) throw std::runtime_error("p2p halo exceeds mailbox capacity");
     const FusedX X = fused_args();
-    const unsigned nbp = (unsigned)std::max(1, (2 * cnt + BLOCK * 16 - 1) / (BLOCK * 16));
-    hipLaunchKernelGGL(hf2d_p2p_push, dim3(nbp), dim3(BLOCK), 0, st, L, first, last, ny, cnt, X, m.sc,
+    hipLaunchKernelGGL(push_kernel(push_per), dim3(push_grid(push_per, cnt)), dim3(BLOCK), 0, st, L, first, last, ny,
+                       cnt, X, m.sc,
                        dt_slot >= 0 ? dt_slot : 0, dt_slot >= 0 ? 1 : 0, 1);
     HIP_CHECK(hipGetLastError());
     p2p_mwg_exchanges++;
@@ -3672,6 +3729,19 @@ const ColList* DeviceSolver::lc_device(const ColList& L) {
   return m.lc_dev + k;
 }
 
+// Tail phase clocks of the last FX_TRACE_N fused exchanges (HF2D_FX_SKIP bit
+// 4 on a loopback run): FX_TRACE_W words per step, zero where none ran.
+std::vector<unsigned long long> DeviceSolver::fx_trace() {
+  flush_pending();
+  Impl& m = *impl;
+  std::vector<unsigned long long> v((size_t)FX_TRACE_N * FX_TRACE_W, 0ull);
+  if (!m.p2p.done) return v;
+  HIP_CHECK(hipStreamSynchronize(m.stream));
+  HIP_CHECK(hipMemcpy(v.data(), m.p2p.done + (DT_SHARDS + 1) * FX_DONE_STRIDE, v.size() * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost));
+  return v;
+}
+
 FusedX DeviceSolver::fused_args() const {
   const Impl& m = *impl;
   const Impl::P2P& p = m.p2p;
@@ -3693,6 +3763,10 @@ FusedX DeviceSolver::fused_args() const {
   X.on = 1;
   static const int skip = std::getenv("HF2D_FX_SKIP") ? std::atoi(std::getenv("HF2D_FX_SKIP")) : 0;
   X.skip = m.p2p.loop ? skip : 0;   // (loopback timing runs only)
+  static const int ef = std::getenv("HF2D_FX_EDGE_FIRST") ? std::atoi(std::getenv("HF2D_FX_EDGE_FIRST")) : 0;
+  static const int c1 = std::getenv("HF2D_FX_COUNT1") ? std::atoi(std::getenv("HF2D_FX_COUNT1")) : 0;
+  X.edge_first = ef;
+  X.count1 = c1;
   return X;
 }
 
@@ -4088,8 +4162,7 @@ void DeviceSolver::lnm_step(const StepParams& P, bool want_res, int slot, int sl
     lnm_launch(P, a, T, want_res, slot, slot_next, serial, (unsigned)(parts ? (1 + T.ne) * T.nbj : T.nbi * T.nbj));
     const int cnt = Lc.nf * h.ny;
     if (m.p2p.on) {
-      hipLaunchKernelGGL(hf2d_p2p_push, dim3((unsigned)std::max(1, (2 * cnt + BLOCK * 16 - 1) / (BLOCK * 16))),
-                         dim3(BLOCK), 0, st, Lc, l_off, l_off + (gi1 - gi0) - 1, h.ny, cnt, fused_args(), m.sc, slot_next,
+      hipLaunchKernelGGL(push_kernel(push_per), dim3(push_grid(push_per, cnt)), dim3(BLOCK), 0, st, Lc, l_off, l_off + (gi1 - gi0) - 1, h.ny, cnt, fused_args(), m.sc, slot_next,
                          1, 0);
       HIP_CHECK(hipGetLastError());
     } else {

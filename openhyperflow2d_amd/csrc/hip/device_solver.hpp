@@ -178,6 +178,7 @@ class DeviceSolver : public SolverBase {
   // returns this rank's checksums of the columns it sent and received and of
   // the folded dt.  p2p_probe_ok checks the all-gathered blobs of every rank.
   std::string p2p_probe();
+  std::vector<unsigned long long> fx_trace();   // fused-exchange tail phase clocks (HF2D_FX_SKIP bit 4)
   static bool p2p_probe_ok(const std::vector<std::string>& blobs, int rank, std::string* why);
   void p2p_fallback();   // p2p off, ghost columns refilled over RCCL / the local group
 
@@ -195,6 +196,7 @@ class DeviceSolver : public SolverBase {
   bool lean_sg = true;     // single-gas specialisation (lean_euler.hpp) if eligible
   int lean_tj = 0;         // tile height override (0: auto, ny split in <= 64)
   int lean_wgcu = 0;       // >0: at most this many tile workgroups resident per CU (LDS request)
+  int push_per = 1;        // halo values per thread of the mailbox push kernel (1, 4, 16)
   int lean_occ = 0;        // occupancy target (waves/SIMD) for the hot kernel: 0 or 6 (cpt 1)
   int lean_cpt = 2;        // cells per thread in the tiled kernel: 1 or 2 (2: measured ~20% faster)
   int lean_nt = 256;       // threads per tile workgroup: 256, or 128 / 64 (single gas; small strips)

@@ -40,10 +40,19 @@ def _cut_lines(log):
     return [ln for ln in log.splitlines() if ln.startswith(("Cut(", "Cx ="))]
 
 
-@pytest.mark.parametrize("nranks", [4, 8])
-def test_virtual_rank_driver_outputs_match_single_gpu(gpu, tmp_path, nranks):
+@pytest.mark.parametrize("nranks,jitter", [(4, 0), (8, 0), (4, 300)])
+def test_virtual_rank_driver_outputs_match_single_gpu(gpu, tmp_path, monkeypatch, nranks, jitter):
+    """N DeviceSolvers on threads (LocalGroup transport, generic k-eps path,
+    outputs without a gather) write the same bytes as one GPU.  jitter > 0:
+    every rank sleeps a random 0..jitter us before each LocalGroup barrier
+    (HF2D_LOCAL_JITTER_US), so the threads reach every host collective and
+    halo copy in a different order -- an ordering hole on this path would
+    show as a byte difference (README, round 6: the one unexplained round-5
+    mismatch)."""
     from openhyperflow2d_amd.parallel.strips import balanced_columns
 
+    if jitter:
+        monkeypatch.setenv("HF2D_LOCAL_JITTER_US", str(jitter))
     nat = gpu.native()
     text = _outputs_deck()
     one, many = tmp_path / "one", tmp_path / "many"

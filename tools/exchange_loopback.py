@@ -39,7 +39,10 @@ def main():
     ap.add_argument("--repeat", type=int, default=3)
     ap.add_argument("--lagged-dt", action="store_true")
     ap.add_argument("--nofuse", action="store_true", help="separate exchange kernel instead of the fused tail")
+    ap.add_argument("--trace", action="store_true", help="phase clocks of the fused tail (last workgroup), median us")
     a = ap.parse_args()
+    if a.trace:   # (read once, at the first fused step)
+        os.environ["HF2D_FX_SKIP"] = str(int(os.environ.get("HF2D_FX_SKIP", "0")) | 16)
     import openhyperflow2d_amd as hf
     from openhyperflow2d_amd.models import decks
     from openhyperflow2d_amd.models.simulation import maybe_autotune
@@ -89,6 +92,13 @@ def main():
            "exchange_rel": round(min(res["loopback"]) / min(res["alone"]) - 1.0, 4),
            "stats": {"overlap_steps": loop.overlap_steps, "lns_fx_steps": loop.lns_fx_steps,
                      "p2p_mwg_exchanges": loop.p2p_mwg_exchanges, "lnm_steps": loop.lnm_steps}}
+    if a.trace:
+        tr = np.asarray(loop.fx_trace(), dtype=np.float64).reshape(-1, 8)
+        tr = tr[tr[:, 7] > 0]
+        names = ["drain", "count", "dt_min", "dt_publish", "flags", "wait_fold", "store", "total"]
+        d = np.diff(tr, axis=1) / 100.0   # 100 MHz clock -> us
+        med = np.median(d, axis=0).tolist() + [float(np.median((tr[:, 7] - tr[:, 0]) / 100.0))]
+        rec["tail_us"] = {k: round(v, 3) for k, v in zip(names, med)}
     print(json.dumps(rec), flush=True)
 
 
