@@ -122,12 +122,32 @@ def _ninja_file() -> str:
         lines.append(f"build {o}: gxx_fp32 {os.path.join(CSRC, 'core', s)}")
         fobjs.append(o)
     lines.append(f"build {fp32_path()}: link_gxx {' '.join(fobjs)}")
-    lines.append(f"default {ext_path()} {os.path.join(HERE, 'bin', 'hf2d')} {os.path.join(HERE, 'bin', 'hf2d_cpu')}")
+    # FP32 build of the GPU CLI (every kernel with real = float; the
+    # finite-rate kinetics stay FP64-only and are refused at run time)
+    f2objs = []
+    for s in CORE_SRCS + ["hf2d_main.cpp"]:
+        o = f"f32_{s[:-4]}.o"
+        lines.append(f"build {o}: cxx {os.path.join(CSRC, 'core', s)}")
+        lines.append("  extra = -DHF2D_FP32")
+        f2objs.append(o)
+    for s in HIP_SRCS:
+        o = f"f32hip_{s[:-4]}.o"
+        lines.append(f"build {o}: hip {os.path.join(CSRC, 'hip', s)}" + (f" || {emb}" if s == "chem_rtc.hip" else ""))
+        lines.append("  hipflags = $hipflags -DHF2D_FP32")
+        f2objs.append(o)
+    lines.append(f"build {gpu_fp32_path()}: link_exe {' '.join(f2objs)}")
+    lines.append(f"default {ext_path()} {os.path.join(HERE, 'bin', 'hf2d')} {os.path.join(HERE, 'bin', 'hf2d_cpu')} "
+                 f"{gpu_fp32_path()}")
     return "\n".join(lines) + "\n"
 
 
 def fp32_path() -> str:
     return os.path.join(HERE, "bin", "hf2d_cpu_fp32")
+
+
+def gpu_fp32_path() -> str:
+    """FP32 build of the GPU CLI (the reference's -DFP=float for the device solver)."""
+    return os.path.join(HERE, "bin", "hf2d_fp32")
 
 
 def build_fp32(verbose: bool = False) -> str:

@@ -979,7 +979,7 @@ void Case::preprocess(InputDeck& d, const std::string& workdir, bool use_checkpo
       return s;
     };
     auto mean_x = [&](real t) {
-      const real p[5] = {0.0, pp / 2., pp, (pp + 1.) / 2., 1.0};
+      const real p[5] = {0.0, (real)(pp / 2.), pp, (real)((pp + 1.) / 2.), 1.0};
       real s = 0;
       for (int i = 0; i < 5; i++) s += p[i] * b4(i, t);
       return s;

@@ -45,11 +45,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void h
 
 }  // namespace
 
+// (FP32 build, HF2D_FP32: the kinetics kernels work on FP64 state only; the
+// mechanism mode is not available there)
+#ifdef HF2D_FP32
+bool chem_fast_available(const std::string&) { return false; }
+#else
 bool chem_fast_available(const std::string& mech) { return mech == "h2_air_li2004"; }
+#endif
 
 ChemArgs chem_args(const SoA& mid, const SoA& out, const real* Tprev, long c0, long c1, DevScalars* sc, int slot,
                    double Tchem, int nsub, int* list, unsigned* count) {
   ChemArgs a;
+#ifdef HF2D_FP32
+  (void)mid, (void)out, (void)Tprev, (void)c0, (void)c1, (void)sc, (void)slot, (void)Tchem, (void)nsub, (void)list,
+      (void)count;
+  throw std::runtime_error("FP32 build: the finite-rate kinetics kernels need the FP64 build");
+#else
   a.S = mid.S;
   a.Yin = mid.Ys;
   a.Yout = out.Ys;
@@ -66,6 +77,7 @@ ChemArgs chem_args(const SoA& mid, const SoA& out, const real* Tprev, long c0, l
   a.fc_bits = NT_FC;
   a.list = list;
   a.count = count;
+#endif
   return a;
 }
 

@@ -448,7 +448,9 @@ __global__ __launch_bounds__(64) void hf2d_chem_rt_valu(const MechData* md, Mech
   const double rho = q.S[cell];
   const double e = q.S[3 * q.N + cell] / rho;   // (at rest: the standalone operator's states)
   double T = q.Tprev[cell];
+#ifndef HF2D_FP32   // (FP32 build: the FP64 kinetics of this comparison kernel are not compiled)
   mech_chem_cell<MECH_MAXSP>(*md, rho, e, rhoY, &T, dt, nsub);
+#endif
   for (int s = 0; s < ns; s++) q.Yout[(long)s * q.N + cell] = rhoY[s];
   q.Tout[cell] = T;
 }

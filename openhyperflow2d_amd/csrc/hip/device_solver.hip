@@ -344,6 +344,10 @@ __device__ inline double p2p_load(const double* p) {
   return __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
                                                            __HIP_MEMORY_SCOPE_SYSTEM));
 }
+// (FP32 build: the halo values are floats; the dt words stay doubles)
+__device__ inline float p2p_load(const float* p) {
+  return __int_as_float((int)__hip_atomic_load((const unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
 
 // Multi-GPU exchange fused into the lean tile kernel (xGMI mailboxes, see
 // hf2d_p2p_xchg for the layout and the parity argument).  Step s of a rank:
@@ -364,6 +368,9 @@ __device__ inline double p2p_load(const double* p) {
 __device__ inline void p2p_store(double* p, double v) {
   __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void p2p_store(float* p, float v) {
+  __hip_atomic_store((unsigned*)p, (unsigned)__float_as_int(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // outstanding vector-memory operations of this wave (stores included on gfx9)
 // have completed: the ordering point for the relaxed system-coherent stores
@@ -1520,7 +1527,7 @@ __device__ __forceinline__ void lnm_step_body(StepParams& P, const LnmArrays& a,
 #pragma unroll
     for (int k = 0; k < NEQ; k++) r.eq[k].i = r.eq[k].j = -1;
   }
-  double dtl = 1.0;
+  real dtl = 1.0;
   int neg = 0;
   const int nsp = a.nsp, bath = a.bath;
   if (mine) {
@@ -1652,7 +1659,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lnm_hot(StepParams P, LnmArrays a,
   apply_dt(P, sc, slot);
   const unsigned n = *a.hot_n;
   const long N = a.N;
-  double dtl = 1.0;
+  real dtl = 1.0;
   int neg = 0, skip = 0;
   for (unsigned q = blockIdx.x * BLOCK + threadIdx.x; q < n; q += gridDim.x * BLOCK) {
     const long idx = a.hot[q];
@@ -1662,7 +1669,7 @@ __global__ __launch_bounds__(BLOCK) void hf2d_lnm_hot(StepParams P, LnmArrays a,
 #pragma unroll
     for (int s = 0; s < LNM_NSB; s++) ys[s] = a.Ys_out[(long)(s < a.nsp ? s : a.nsp - 1) * N + idx];
     LnmState st;
-    double d = 1.0;
+    real d = 1.0;
     if (!mech_state_node(P, *a.mech, a.nsp, S4, ys, a.Uo[idx], a.Vo[idx], a.To[idx], a.ksi[idx], a.CT[idx],
                          a.BGX[idx], a.BGY[idx], &st, &d, &neg))
       skip = 1;
@@ -4250,6 +4257,10 @@ void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const Lea
   mid.nsp = m.nsp;
   const long c0 = (long)P.i0 * P.ny, c1 = (long)P.i1 * P.ny;
   const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : 4);
+#ifdef HF2D_FP32
+  (void)kind, (void)c0, (void)c1, (void)md;
+  throw std::runtime_error("FP32 build: finite-rate kinetics need the FP64 build");
+#else
   if (kind == 1) {
     if (!chem_fast_launch(cs.cfg.mech->name, P, mid, mid, a.To, c0, c1, m.sc, slot, md.Tchem, md.nsub, st, a.hot,
                           a.hot_n, true))
@@ -4260,6 +4271,7 @@ void DeviceSolver::lnm_launch(const StepParams& P, const LnmArrays& a, const Lea
       throw std::runtime_error("hf2d_rtc_chem list launch failed");
     chem_kernel_used = "hf2d_rtc_chem";
   }
+#endif
   if (lnm_timing) HIP_CHECK(hipEventRecord(m.lnm_ev[2], st));
   const unsigned nb = (unsigned)std::min<long>((c1 - c0 + BLOCK - 1) / BLOCK, 1024);
   hipLaunchKernelGGL(hf2d_lnm_hot, dim3(nb), dim3(BLOCK), 0, st, P, a, m.sc, slot, slot_next, serial);
@@ -4665,6 +4677,10 @@ StepResult DeviceSolver::do_step_eager(const StepParams& P0, bool want_res) {
 void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& out, long k0, long k1, unsigned nb,
                                int slot) {
   Impl& m = *impl;
+#ifdef HF2D_FP32
+  (void)P, (void)mid, (void)out, (void)k0, (void)k1, (void)nb, (void)slot, (void)m;
+  throw std::runtime_error("FP32 build: finite-rate kinetics need the FP64 build");
+#else
   const real* Tprev = m.Tg[pbuf];
   const MechData& md = *cs.cfg.mech->data_ptr();
   const int kind = chem_kernel ? chem_kernel : ((chem_fast && chem_fast_ok) ? 1 : (chem_rtc && chem_rtc_ok) ? 4 : 2);
@@ -4721,6 +4737,7 @@ void DeviceSolver::launch_chem(const StepParams& P, const SoA& mid, const SoA& o
     hipLaunchKernelGGL(hf2d_chem_generic<MECH_MAXSP>, dim3(nb), dim3(BLOCK), 0, m.stream, P, mid, out, Tprev, k0, k1,
                        m.sc, slot);
   HIP_CHECK(hipGetLastError());
+#endif
 }
 
 void DeviceSolver::synchronize() {

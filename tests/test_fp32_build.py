@@ -67,3 +67,14 @@ def test_fp32_cli_tracks_the_fp64_cli(fp32_cli, tmp_path, name):
     assert rel.max() > 0.0   # it is a float build
     rec32 = glob.glob(str(tmp_path / "fp32" / "*.hf2d"))[0]
     assert os.path.getsize(rec32) == nx * ny * 680
+
+
+def test_fp32_gpu_cli_is_built():
+    """The default build also links the FP32 GPU CLI (bin/hf2d_fp32, every
+    device kernel with real = float; tests/test_gpu_fp32.py runs it)."""
+    from openhyperflow2d_amd import _build
+
+    exe = _build.gpu_fp32_path()
+    assert os.path.isfile(exe) and os.access(exe, os.X_OK)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)   # (no deck: the banner)
+    assert "(FP32)" in r.stdout, r.stdout[-500:] + r.stderr[-500:]
