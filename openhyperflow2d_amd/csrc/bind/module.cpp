@@ -856,6 +856,7 @@ PYBIND11_MODULE(_hf2d, m) {
       .def_readwrite("lean_tj", &DeviceSolver::lean_tj)
       .def_readwrite("tile_stagger", &DeviceSolver::tile_stagger)
       .def_readwrite("lean_occ", &DeviceSolver::lean_occ)
+      .def_readwrite("push_per", &DeviceSolver::push_per)
       .def_readwrite("lean_wgcu", &DeviceSolver::lean_wgcu)
       .def_readwrite("use_graph", &DeviceSolver::use_graph)
       .def_readwrite("chem_fast", &DeviceSolver::chem_fast)

@@ -394,7 +394,7 @@ def test_graph_windows_after_a_download_replay_the_right_buffers(gpu, deck):
                                             ("scramjet", 8, False), ("resonator", 3, True), ("scramjet", 3, True),
                                             ("resonator", 3, "fx"), ("step", 2, "fx"), ("sst_plate", 3, "fx"),
                                             ("scramjet", 3, "fx"), ("resonator", 4, "fx"), ("resonator", 8, "fx"),
-                                            ("scramjet", 4, "fx"), ("scramjet", 8, "fx")])
+                                            ("scramjet", 4, "fx"), ("scramjet", 8, "fx"), ("scramjet", 4, "fx16")])
 def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     """Lean N-S / mechanism tiles on strips (two ghost columns: the tile
     evaluates the fill of the first one, which reads the second; HALO_LNS
@@ -422,12 +422,16 @@ def test_lean_ns_strips_match_single_gpu(gpu, deck, nranks, p2p):
     stats = {}
     # (mechanism: the edge-first split step is opt-in, lnm_overlap; the fused
     # mailbox case runs the default: all tiles, then push / unpack)
-    setup = (lambda s: setattr(s, "lnm_overlap", True)) if deck == "scramjet" and p2p != "fx" else None
-    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=bool(p2p), fuse=p2p == "fx",
+    # ("fx16": the mailbox push kernel with 16 halo values per thread instead of one)
+    fx = p2p in ("fx", "fx16")
+    setup = (lambda s: setattr(s, "lnm_overlap", True)) if deck == "scramjet" and not fx else None
+    if p2p == "fx16":
+        setup = lambda s: setattr(s, "push_per", 16)  # noqa: E731
+    got, summ = _virtual_ranks(gpu, text, nranks, schedule, lean=True, p2p=bool(p2p), fuse=fx,
                                stats=stats, fields=fields, setup=setup)
     lean_steps = stats["lnm_steps"] if deck == "scramjet" else stats["lns_steps"]
     assert min(lean_steps) > 0, stats
-    if p2p == "fx":
+    if fx:
         assert min(stats["p2p_mwg_exchanges" if deck == "scramjet" else "lns_fx_steps"]) > 0, stats
         if deck != "scramjet":   # the next fused step unpacked the halo in its edge tiles
             assert min(stats["lns_prologue_steps"]) > 0, stats
