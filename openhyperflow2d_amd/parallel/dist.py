@@ -38,6 +38,27 @@ def init_from_env(backend: Optional[str] = None):
     return rank, world
 
 
+def any_rank(flag, device: bool = False) -> bool:
+    """True on every rank if ``flag`` is true on any rank (all-reduce MAX).
+
+    For host loops whose trip count must agree across ranks although their
+    condition is rank-local -- bench.py's step-graph priming: each rank's
+    autotune picks graphs on or off from its own timings, and every step
+    exchanges with the other ranks, so a rank-local loop condition deadlocked a
+    4-rank run (profiles/bench_rehearsal_shared_gpu_r06.txt).  ``device``: the
+    process group is NCCL/RCCL (the flag travels as a device tensor)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    if device:
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item()) == 1
+
+
 class DistributedSimulation:
     """A strip of a deck run on this rank."""
 

@@ -249,3 +249,42 @@ def test_wall_blend_changes_only_the_tangential_momentum_near_walls(hf):
     assert set(d[:, 1].tolist()) <= set(range(1, 6)), sorted(set(d[:, 1].tolist()))
     i_le = int(round(0.2 * 60))
     assert d[:, 0].min() >= i_le - 1
+
+
+def _any_rank_worker(rank, world, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import json
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from openhyperflow2d_amd.parallel.dist import any_rank
+
+        flags = [any_rank(rank == world - 1), any_rank(False), any_rank(True)]
+        # a loop whose rank-local condition differs (rank r wants r + 1 trips):
+        # every rank must make the same number of trips (bench.py graph priming)
+        n = 0
+        while any_rank(n < rank + 1):
+            dist.barrier()   # the collective a trip makes on every rank
+            n += 1
+        with open(os.path.join(outdir, "r%d.json" % rank), "w") as f:
+            json.dump({"flags": flags, "trips": n}, f)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_any_rank_agrees_across_ranks(tmp_path):
+    """parallel.dist.any_rank: the same answer on every rank, so host loops with
+    a rank-local condition run the same trip count everywhere (gloo, 3 ranks)."""
+    import json
+
+    world = 3
+    mp.start_processes(_any_rank_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        d = json.load(open(tmp_path / ("r%d.json" % r)))
+        assert d["flags"] == [True, False, True]
+        assert d["trips"] == world
