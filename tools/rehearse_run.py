@@ -11,7 +11,7 @@ one process -- the strip decomposition is bitwise by design:
 
 The compare step checks every file both runs wrote (checkpoint slabs are
 per rank, so files only one run has are listed, not compared) and exits
-non-zero on the first difference.  Deck: Wedge15 400 x 80 Euler, 2 cycles of
+non-zero on the first difference.  Deck: Wedge15 400 x 80 Euler, up to 2 cycles of
 40 steps, outputs every 20, autotune on (ThreadBlockSize 0): each rank's
 tuning choices come from its own timings, as on a multi-GPU node."""
 import hashlib
